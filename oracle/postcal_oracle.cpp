@@ -1,0 +1,1050 @@
+// =============================================================================
+// ORACLE — TEST INFRASTRUCTURE ONLY.  NOT PART OF THE PRODUCT.
+//
+// A single-threaded CPU restatement of the reference PIPSORT posterior
+// calculation (CAST-genomics/pipsort, read-only at /root/reference) used as the
+// parity checker for the MI355X engine.  Only tests/, __graft_entry__.smoke()
+// and bench.py's cpu_baseline leg may build, load or run anything in oracle/.
+// The product path (pipsort_amd/, include/) never links or calls this file.
+//
+// Parity pinning: the reference itself is unbuildable in this image (util.cpp
+// needs GSL, Armadillo needs an external BLAS/LAPACK).
+// This restatement is pinned against the reference's own golden vectors in
+// /root/reference/tests/example/expected_* (copied to tests/golden/example/),
+// which it reproduces byte-for-byte (tests/test_oracle_golden.py).
+//
+// Every function cites the reference file:line it restates.  Where the
+// reference materialises N x N temporaries, the default ("reduced") mode works
+// on the k x k system those temporaries collapse to (exact algebra, see
+// lowrank_ll_reduced); mode "literal" keeps the N x N formulation of
+// postcal.cpp:214-304 and is used for the CPU-baseline timing and to pin the
+// reduction on small loci.
+// =============================================================================
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <numeric>
+#include <random>
+#include <sstream>
+#include <string>
+#include <unordered_map>
+#include <vector>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+#include <getopt.h>
+
+using std::string;
+using std::vector;
+
+namespace orc {
+
+// ---------------------------------------------------------------------------
+// util.cpp restatements
+// ---------------------------------------------------------------------------
+
+// util.cpp:51-62  fact / nCr (long int arithmetic, same overflow behaviour)
+static long fact(int n) { return n == 0 ? 1 : n * fact(n - 1); }
+static long nCr(int n, int r) {
+    long result = 1;
+    for (int i = n; i > n - r; i--) result *= i;
+    return result / fact(r);
+}
+
+// util.cpp:86-96  importData: whitespace separated doubles until first failure
+static bool import_data(const string& fn, vector<double>& out) {
+    std::ifstream f(fn.c_str());
+    if (!f) { std::cout << "Unable to open file; This is why"; return false; }
+    double d;
+    while (f >> d) out.push_back(d);
+    return true;
+}
+
+// util.cpp:132-159  importDataFirstColumn / importDataSecondColumn
+static void import_columns(const string& fn, vector<string>& names, vector<double>& vals) {
+    std::ifstream fin(fn.c_str());
+    string line, s;
+    double d = 0.0;
+    string first = "";
+    while (std::getline(fin, line)) {
+        std::istringstream a(line);
+        a >> first;
+        names.push_back(first);
+        std::istringstream b(line);
+        b >> s;
+        b >> d;
+        vals.push_back(d);
+    }
+}
+
+// util.cpp:99-126  importSnpMap (comma separated: rsid, idx_study0, idx_study1 ...)
+static bool import_snp_map(const string& fn, int ncols, vector<string>& first,
+                           vector<vector<int>>& rest) {
+    std::ifstream f(fn.c_str());
+    if (!f.is_open()) { std::cout << "Could not open file\n"; return false; }
+    string line, word;
+    while (std::getline(f, line)) {
+        std::stringstream s(line);
+        for (int i = 0; i < ncols; i++) {
+            std::getline(s, word, ',');
+            if (i == 0) first.push_back(word);
+            else rest[i - 1].push_back(std::stoi(word));
+        }
+    }
+    return true;
+}
+
+// util.cpp:195-226  makeSigmaPositiveSemiDefinite: add 0.01 to the diagonal until
+// the LU determinant (partial pivoting, GSL-2.5 right-looking elimination,
+// det = signum * prod(U_ii) in index order) is > 0.
+// Compiled with -ffp-contract=off so the elimination rounds like GSL's x86-64 build.
+static double lu_det_gsl25(vector<double> a /*row-major copy*/, int n) {
+    int signum = 1;
+    for (int j = 0; j < n - 1; j++) {
+        double mx = std::fabs(a[(size_t)j * n + j]);
+        int ip = j;
+        for (int i = j + 1; i < n; i++) {
+            double v = std::fabs(a[(size_t)i * n + j]);
+            if (v > mx) { mx = v; ip = i; }
+        }
+        if (ip != j) {
+            for (int k = 0; k < n; k++) std::swap(a[(size_t)j * n + k], a[(size_t)ip * n + k]);
+            signum = -signum;
+        }
+        double ajj = a[(size_t)j * n + j];
+        if (ajj != 0.0) {
+            for (int i = j + 1; i < n; i++) {
+                double aij = a[(size_t)i * n + j] / ajj;
+                a[(size_t)i * n + j] = aij;
+                for (int k = j + 1; k < n; k++) {
+                    double aik = a[(size_t)i * n + k];
+                    double ajk = a[(size_t)j * n + k];
+                    a[(size_t)i * n + k] = aik - aij * ajk;
+                }
+            }
+        }
+    }
+    double det = signum;
+    for (int i = 0; i < n; i++) det *= a[(size_t)i * n + i];
+    return det;
+}
+
+static double make_psd(vector<double>& sig /*row-major n x n*/, int n) {
+    double add = 0;
+    for (;;) {
+        vector<double> t(sig);
+        for (int i = 0; i < n; i++) t[(size_t)i * n + i] = sig[(size_t)i * n + i] + add;
+        double det = lu_det_gsl25(t, n);
+        if (det > 0) break;
+        add += 0.01;
+    }
+    for (int i = 0; i < n; i++) sig[(size_t)i * n + i] += add;
+    return add;
+}
+
+// util.cpp:228-263  eigen_decomp (GSL symmv).  Restated with cyclic Jacobi:
+// eigenvector order/sign differ from GSL but B^T B = Q|W|Q^T and B^T S' are
+// invariant to both, and those are all the path consumes.
+static void jacobi_eigen(const vector<double>& a_in, int n, vector<double>& w,
+                         vector<double>& q /*row-major, columns are eigenvectors*/) {
+    vector<double> a(a_in);
+    q.assign((size_t)n * n, 0.0);
+    for (int i = 0; i < n; i++) q[(size_t)i * n + i] = 1.0;
+    for (int sweep = 0; sweep < 100; sweep++) {
+        double off = 0, tot = 0;
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) {
+                double v = a[(size_t)i * n + j] * a[(size_t)i * n + j];
+                tot += v;
+                if (i != j) off += v;
+            }
+        if (off <= 1e-30 * tot || off == 0) break;
+        for (int p = 0; p < n - 1; p++)
+            for (int r = p + 1; r < n; r++) {
+                double apr = a[(size_t)p * n + r];
+                if (apr == 0.0) continue;
+                double app = a[(size_t)p * n + p], arr = a[(size_t)r * n + r];
+                double theta = (arr - app) / (2.0 * apr);
+                double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+                double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < n; k++) {  // columns p, r
+                    double akp = a[(size_t)k * n + p], akr = a[(size_t)k * n + r];
+                    a[(size_t)k * n + p] = c * akp - s * akr;
+                    a[(size_t)k * n + r] = s * akp + c * akr;
+                }
+                for (int k = 0; k < n; k++) {  // rows p, r
+                    double apk = a[(size_t)p * n + k], ark = a[(size_t)r * n + k];
+                    a[(size_t)p * n + k] = c * apk - s * ark;
+                    a[(size_t)r * n + k] = s * apk + c * ark;
+                }
+                for (int k = 0; k < n; k++) {
+                    double qkp = q[(size_t)k * n + p], qkr = q[(size_t)k * n + r];
+                    q[(size_t)k * n + p] = c * qkp - s * qkr;
+                    q[(size_t)k * n + r] = s * qkp + c * qkr;
+                }
+            }
+    }
+    w.resize(n);
+    for (int i = 0; i < n; i++) w[i] = a[(size_t)i * n + i];
+}
+
+// ---------------------------------------------------------------------------
+// Problem at the PostCal seam (postcal.h:118): what Model hands to PostCal.
+// ---------------------------------------------------------------------------
+struct Problem {
+    int S = 2;                       // num_of_studies
+    vector<int> m;                   // num_snps_all
+    int N = 0;                       // totalSnpCount
+    vector<vector<double>> B;        // per-study B_s, column-major M_s x M_s (Armadillo layout)
+    vector<double> sp;               // S_LONG_VEC (S'), length N
+    int U = 0;                       // unionSnpCount
+    vector<vector<int>> u2l;         // idx_to_snp_map[s][u]
+    vector<vector<int>> l2u;         // idx_to_union_pos_map[s][j]
+    int maxc = 3;
+    vector<int> n;                   // sample sizes
+    double p = 0.75, gamma = 0.01, t2 = 0.52, s2 = 5.2;
+};
+
+// model.h:86-264 Model constructor up to the PostCal construction.
+struct Inputs {
+    vector<vector<string>> names;
+    vector<string> all_snp_pos;
+    double psd_add[8] = {0};
+};
+
+static int model_setup(const vector<string>& ld, const vector<string>& zf, const string& mapf,
+                       Problem& P, Inputs& in) {
+    P.S = (int)ld.size();
+    vector<vector<double>> sig(P.S);
+    vector<vector<double>> z(P.S);
+    for (int i = 0; i < P.S; i++) {
+        vector<double> L;
+        if (!import_data(ld[i], L)) return 1;
+        vector<string> nm;
+        vector<double> zz;
+        import_columns(zf[i], nm, zz);
+        int M = (int)std::sqrt((double)L.size());  // model.h:98
+        if (M != (int)nm.size()) {
+            printf("ERROR: LD matrix is size %d x %d but zscores has %lu snps\n. Check LD file for nans.\n",
+                   M, M, (unsigned long)nm.size());
+            return 1;
+        }
+        P.m.push_back(M);
+        sig[i].assign((size_t)M * M, 0.0);
+        for (int r = 0; r < M; r++)
+            for (int c = 0; c < M; c++) sig[i][(size_t)r * M + c] = L[(size_t)r * M + c];  // model.h:107-111
+        in.names.push_back(nm);
+        z[i] = zz;
+    }
+    P.u2l.assign(P.S, {});
+    if (!import_snp_map(mapf, P.S + 1, in.all_snp_pos, P.u2l)) return 1;  // model.h:132
+    P.U = (int)in.all_snp_pos.size();
+    P.l2u.assign(P.S, {});
+    for (int i = 0; i < P.S; i++) {  // model.h:134-144
+        for (int u = 0; u < (int)P.u2l[i].size(); u++)
+            if (P.u2l[i][u] >= 0) P.l2u[i].push_back(u);
+        if ((int)P.l2u[i].size() != P.m[i]) { printf("Invariant does not hold\n"); return 1; }
+    }
+    P.N = std::accumulate(P.m.begin(), P.m.end(), 0);
+    P.sp.clear();
+    for (int i = 0; i < P.S; i++) P.sp.insert(P.sp.end(), z[i].begin(), z[i].end());  // model.h:154-158
+    for (int i = 0; i < P.S; i++) in.psd_add[i] = make_psd(sig[i], P.m[i]);      // model.h:171-197
+    // model.h:213-264: low-rank transform (haslowrank is always true, model.h:190)
+    P.B.assign(P.S, {});
+    int off = 0;
+    for (int i = 0; i < P.S; i++) {
+        int M = P.m[i];
+        vector<double> w, q;
+        jacobi_eigen(sig[i], M, w, q);
+        vector<double>& B = P.B[i];
+        B.assign((size_t)M * M, 0.0);
+        for (int r = 0; r < M; r++) {
+            double so = std::sqrt(std::fabs(w[r]));  // |Omega|^(1/2)   model.h:227,231
+            for (int c = 0; c < M; c++) B[(size_t)c * M + r] = so * q[(size_t)c * M + r];  // B = sqrtW * Q^T (col-major)
+        }
+        vector<double> low(M, 0.0);  // S' = inv(sqrtW) * Q^T * z   model.h:249-255
+        for (int r = 0; r < M; r++) {
+            double acc = 0;
+            for (int c = 0; c < M; c++) acc += q[(size_t)c * M + r] * P.sp[off + c];
+            low[r] = acc / std::sqrt(std::fabs(w[r]));
+        }
+        for (int r = 0; r < M; r++) P.sp[off + r] = low[r];
+        off += M;
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// PostCal restatement (postcal.h / postcal.cpp / sss_postcal.cpp)
+// ---------------------------------------------------------------------------
+struct Accum {
+    vector<double> post, noc, shared, sll, nsll;
+    double total = 0;
+    long n_eval = 0;
+};
+
+class PostCal {
+  public:
+    const Problem& P;
+    Accum A;
+    bool literal;
+    // derived (the "reduced" mode needs G = B^T B and y = B^T S'; literal uses B directly)
+    vector<vector<double>> G;   // per study M_s x M_s row-major  (B_s^T B_s)
+    vector<vector<double>> y;   // per study B_s^T S'_s
+    vector<int> off;            // study offsets into N
+    double spsq = 0;            // S'^T S'
+    double lrl0 = 0;            // null-config log likelihood + prior
+    double sss_sum = 0;
+    std::unordered_map<vector<int>, double, struct VH> *dummy = nullptr;
+
+    explicit PostCal(const Problem& p, bool lit) : P(p), literal(lit) {
+        A.post.assign(P.N, 0.0);  // postcal.h:129-131
+        A.noc.assign(P.S, 0.0);
+        A.shared.assign(P.U, 0.0);
+        A.sll.assign(P.U, 0.0);
+        A.nsll.assign(P.U, 0.0);
+        off.assign(P.S, 0);
+        for (int s = 1; s < P.S; s++) off[s] = off[s - 1] + P.m[s - 1];
+        G.resize(P.S);
+        y.resize(P.S);
+        for (int s = 0; s < P.S; s++) {
+            int M = P.m[s];
+            const vector<double>& B = P.B[s];
+            G[s].assign((size_t)M * M, 0.0);
+            for (int i = 0; i < M; i++)
+                for (int j = 0; j <= i; j++) {
+                    double acc = 0;
+                    for (int r = 0; r < M; r++) acc += B[(size_t)i * M + r] * B[(size_t)j * M + r];
+                    G[s][(size_t)i * M + j] = G[s][(size_t)j * M + i] = acc;
+                }
+            y[s].assign(M, 0.0);
+            for (int i = 0; i < M; i++) {
+                double acc = 0;
+                for (int r = 0; r < M; r++) acc += B[(size_t)i * M + r] * P.sp[off[s] + r];
+                y[s][i] = acc;
+            }
+        }
+        spsq = 0;
+        for (double v : P.sp) spsq += v * v;
+        // postcal.cpp:797-803: res = S'^T S', matDet = 1, lrl = -res/2 - sqrt(|1|)
+        lrl0 = (-spsq / 2 - std::sqrt(std::fabs(1.0))) + P.U * std::log(1 - P.gamma);
+    }
+
+    // postcal.h:102-112 addlogSpace (0 is the "empty" sentinel, >700 gap drops)
+    static double addlog(double a, double b) {
+        if (a == 0) return b;
+        if (b == 0) return a;
+        double base = std::max(a, b);
+        if (base - std::min(a, b) > 700) return base;
+        return base + std::log(1 + std::exp(std::min(a, b) - base));
+    }
+
+    // postcal.cpp:19-59 log_prior (two studies only)
+    double log_prior(int k, const vector<int>& b0, const vector<int>& b1) const {
+        double pc = 0;
+        if (P.p != 0) {
+            for (int i = 0; i < k; i++) {
+                if (b0[i] == b1[i]) {
+                    if (b0[i] == 1) pc += std::log(P.p);
+                    else { std::cout << "This case in prior should not happen\n"; exit(1); }
+                } else {
+                    pc += std::log((1 - P.p) * 0.5);
+                }
+            }
+        }
+        int n1 = 0;
+        for (int i = 0; i < k; i++)
+            if (b0[i] == 1 || b1[i] == 1) { pc += std::log(P.gamma); n1++; }
+        pc += (P.U - n1) * std::log(1 - P.gamma);
+        return pc;
+    }
+
+    // postcal.cpp:63-121 construct_diagC — only its main diagonal is consumed on the
+    // live path (postcal.cpp:250), so it is restated as the value d_s per study.
+    double dval(int s) const {
+        int mn = *std::min_element(P.n.begin(), P.n.end());
+        return P.s2 * (double(P.n[s]) / mn) + P.t2;
+    }
+
+    // small dense helpers for the k x k system
+    static double det_lu(vector<double> a, int k) {  // partial-pivot LU determinant
+        double det = 1;
+        for (int j = 0; j < k; j++) {
+            int ip = j;
+            for (int i = j + 1; i < k; i++)
+                if (std::fabs(a[i * k + j]) > std::fabs(a[ip * k + j])) ip = i;
+            if (a[ip * k + j] == 0) return 0;
+            if (ip != j) { for (int c = 0; c < k; c++) std::swap(a[j * k + c], a[ip * k + c]); det = -det; }
+            det *= a[j * k + j];
+            for (int i = j + 1; i < k; i++) {
+                double f = a[i * k + j] / a[j * k + j];
+                for (int c = j; c < k; c++) a[i * k + c] -= f * a[j * k + c];
+            }
+        }
+        return det;
+    }
+    static bool inverse(vector<double> a, int k, vector<double>& inv) {  // Gauss-Jordan
+        inv.assign((size_t)k * k, 0.0);
+        for (int i = 0; i < k; i++) inv[i * k + i] = 1;
+        for (int j = 0; j < k; j++) {
+            int ip = j;
+            for (int i = j + 1; i < k; i++)
+                if (std::fabs(a[i * k + j]) > std::fabs(a[ip * k + j])) ip = i;
+            if (a[ip * k + j] == 0) return false;
+            for (int c = 0; c < k; c++) { std::swap(a[j * k + c], a[ip * k + c]); std::swap(inv[j * k + c], inv[ip * k + c]); }
+            double piv = a[j * k + j];
+            for (int c = 0; c < k; c++) { a[j * k + c] /= piv; inv[j * k + c] /= piv; }
+            for (int i = 0; i < k; i++) {
+                if (i == j) continue;
+                double f = a[i * k + j];
+                if (f == 0) continue;
+                for (int c = 0; c < k; c++) { a[i * k + c] -= f * a[j * k + c]; inv[i * k + c] -= f * inv[j * k + c]; }
+            }
+        }
+        return true;
+    }
+
+    // postcal.cpp:214-304 lowrank_likelihood for causal set C (global indices, ascending,
+    // exactly the order of the i-loop at postcal.cpp:245-253).
+    //   U = (B_C D)^T, V = B_C, tmp_CC = I + U V = I + D B_C^T B_C,
+    //   res = S'^T (I - V pinv(tmp_CC) U) S' = S'^T S' - y_C^T pinv(tmp_CC) D y_C,  y_C = B_C^T S'
+    //   ll  = -res/2 - log(sqrt(|det(tmp_CC)|))
+    // The "reduced" form below evaluates exactly these k x k quantities; "literal" builds
+    // the N x N matrices as the reference does.
+    double lowrank_ll(const vector<int>& C, const vector<double>& dC) const {
+        int k = (int)C.size();
+        if (literal) return lowrank_ll_literal(C, dC);
+        vector<double> GC((size_t)k * k, 0.0), yC(k, 0.0);
+        for (int a = 0; a < k; a++) {
+            int sa = study_of(C[a]);
+            yC[a] = y[sa][C[a] - off[sa]];
+            for (int b = 0; b < k; b++) {
+                int sb = study_of(C[b]);
+                GC[a * k + b] = (sa == sb) ? G[sa][(size_t)(C[a] - off[sa]) * P.m[sa] + (C[b] - off[sb])] : 0.0;
+            }
+        }
+        vector<double> T((size_t)k * k);
+        for (int a = 0; a < k; a++)
+            for (int b = 0; b < k; b++) T[a * k + b] = (a == b ? 1.0 : 0.0) + dC[a] * GC[a * k + b];
+        double det = det_lu(T, k);
+        vector<double> inv;
+        if (!inverse(T, k, inv) || det == 0) {
+            std::cout << "Error the matrix is singular and we fail to fix it (low rank lkl)." << std::endl;
+            exit(0);  // postcal.cpp:291-294 exits with status 0
+        }
+        double quad = 0;
+        for (int a = 0; a < k; a++) {
+            double acc = 0;
+            for (int b = 0; b < k; b++) acc += inv[a * k + b] * dC[b] * yC[b];
+            quad += yC[a] * acc;
+        }
+        double res = spsq - quad;
+        return -res / 2 - std::log(std::sqrt(std::fabs(det)));
+    }
+
+    double lowrank_ll_literal(const vector<int>& C, const vector<double>& dC) const {
+        int N = P.N, k = (int)C.size();
+        // sigmaMatrix = BIG_SIGMA (block diagonal B), column-major
+        auto Bel = [&](int r, int c) -> double {
+            int sr = study_of(r), sc = study_of(c);
+            if (sr != sc) return 0.0;
+            int M = P.m[sr];
+            return P.B[sr][(size_t)(c - off[sc]) * M + (r - off[sr])];
+        };
+        vector<double> small_sigma((size_t)N * k);  // N x k
+        for (int j = 0; j < k; j++)
+            for (int r = 0; r < N; r++) small_sigma[(size_t)r * k + j] = Bel(r, C[j]);
+        vector<double> Um((size_t)k * N);  // U = (small_sigma * diag(d))^T
+        for (int j = 0; j < k; j++)
+            for (int r = 0; r < N; r++) Um[(size_t)j * N + r] = small_sigma[(size_t)r * k + j] * dC[j];
+        vector<double> UV((size_t)k * k, 0.0);  // U * V, V = small_sigma
+        for (int a = 0; a < k; a++)
+            for (int b = 0; b < k; b++) {
+                double acc = 0;
+                for (int r = 0; r < N; r++) acc += Um[(size_t)a * N + r] * small_sigma[(size_t)r * k + b];
+                UV[a * k + b] = acc;
+            }
+        vector<double> T((size_t)k * k);
+        for (int a = 0; a < k; a++)
+            for (int b = 0; b < k; b++) T[a * k + b] = (a == b ? 1.0 : 0.0) + UV[a * k + b];
+        double det = det_lu(T, k);
+        vector<double> inv;
+        if (!inverse(T, k, inv) || det == 0) {
+            std::cout << "Error the matrix is singular and we fail to fix it (low rank lkl)." << std::endl;
+            exit(0);
+        }
+        vector<double> temp2((size_t)N * k, 0.0);  // V * pinv(tmp_CC)
+        for (int r = 0; r < N; r++)
+            for (int b = 0; b < k; b++) {
+                double acc = 0;
+                for (int a = 0; a < k; a++) acc += small_sigma[(size_t)r * k + a] * inv[a * k + b];
+                temp2[(size_t)r * k + b] = acc;
+            }
+        // tmp_AA = I - temp2 * U  (N x N), then res = S'^T tmp_AA S'
+        vector<double> AA((size_t)N * N);
+        for (int r = 0; r < N; r++)
+            for (int c = 0; c < N; c++) {
+                double acc = 0;
+                for (int b = 0; b < k; b++) acc += temp2[(size_t)r * k + b] * Um[(size_t)b * N + c];
+                AA[(size_t)r * N + c] = (r == c ? 1.0 : 0.0) - acc;
+            }
+        double res = 0;
+        for (int c = 0; c < N; c++) {
+            double acc = 0;
+            for (int r = 0; r < N; r++) acc += P.sp[r] * AA[(size_t)r * N + c];
+            res += acc * P.sp[c];
+        }
+        return -res / 2 - std::log(std::sqrt(std::fabs(det)));
+    }
+
+    int study_of(int g) const {
+        int s = 0;
+        while (s + 1 < P.S && g >= off[s + 1]) s++;
+        return s;
+    }
+
+    // postcal.cpp:1111-1126 checkOR
+    static bool checkOR(const vector<int>& b0, const vector<int>& b1, int k) {
+        for (int i = 0; i < k; i++)
+            if (b0[i] + b1[i] == 0) return false;
+        return true;
+    }
+
+    // Accumulation block shared by all enumerators (postcal.cpp:981-1030,
+    // postcal.cpp:632-681, sss_postcal.cpp:628-668).
+    void accumulate(double L, double ll, const vector<int>& locs, const vector<int>& b0,
+                    const vector<int>& b1, const vector<int>& cfg /*global bools*/, double* total) {
+        int k = (int)locs.size();
+        *total = addlog(*total, L);
+        for (int w = 0; w < P.S; w++) {
+            const vector<int>& bw = (w == 0) ? b0 : b1;
+            bool allZero = true;
+            for (int v = 0; v < k; v++) if (bw[v] == 1) { allZero = false; break; }
+            if (allZero) A.noc[w] = addlog(A.noc[w], L);
+        }
+        for (int g = 0; g < k; g++) {
+            bool sh = (b0[g] == 1 && b1[g] == 1);
+            if (sh) {
+                A.shared[locs[g]] = addlog(A.shared[locs[g]], L);
+                A.sll[locs[g]] = addlog(A.sll[locs[g]], ll);
+            } else {
+                A.nsll[locs[g]] = addlog(A.nsll[locs[g]], ll);
+            }
+        }
+        for (int f = 0; f < P.N; f++) A.post[f] = addlog(A.post[f], L * cfg[f]);
+    }
+
+    // Evaluate one (union set, per-study assignment) pattern: returns {L, ll}.
+    void eval_pattern(const vector<int>& locs, const vector<int>& b0, const vector<int>& b1,
+                      vector<int>& cfg, double& L, double& ll) const {
+        int k = (int)locs.size();
+        std::fill(cfg.begin(), cfg.end(), 0);
+        for (int j = 0; j < k; j++) {
+            if (b0[j]) cfg[off[0] + P.u2l[0][locs[j]]] = 1;
+            if (b1[j]) cfg[off[1] + P.u2l[1][locs[j]]] = 1;
+        }
+        vector<int> C;
+        vector<double> dC;
+        double d0 = dval(0), d1 = dval(1);
+        for (int i = 0; i < P.N; i++)
+            if (cfg[i]) { C.push_back(i); dC.push_back(study_of(i) == 0 ? d0 : d1); }
+        ll = lowrank_ll(C, dC);
+        L = ll + log_prior(k, b0, b1);
+    }
+
+    // Expand a union set into all per-study assignments (postcal.cpp:856-955 and
+    // sss_postcal.cpp:518-597): bits assigned in (union SNP j, study s) order, masks
+    // 1..2^b-1, patterns failing checkOR skipped.  Returns the sss score
+    // (the pattern L with the largest |L|, sss_postcal.cpp:560,624-626).
+    double expand(const vector<int>& locs, bool updates, double* total, long* nexp) {
+        int k = (int)locs.size();
+        vector<int> cfg(P.N, 0);
+        if (k == 0) {  // null configuration: postcal.cpp:793-822 / sss_postcal.cpp:463-499
+            if (updates) {
+                for (int s = 0; s < P.S; s++) A.noc[s] = addlog(A.noc[s], lrl0);
+                *total = addlog(*total, lrl0);
+                (*nexp)++;
+            }
+            return lrl0;
+        }
+        vector<int> idx0(k), idx1(k), has0(k), has1(k);
+        int nb = 0;
+        for (int j = 0; j < k; j++) {
+            int l0 = P.u2l[0][locs[j]], l1 = P.u2l[1][locs[j]];
+            has0[j] = l0 >= 0;
+            has1[j] = l1 >= 0;
+            nb += has0[j] + has1[j];
+        }
+        int total_masks = (int)(std::pow(2, nb) - 1);
+        double maxl = 0.0;
+        vector<int> b0(k), b1(k);
+        for (int i = 0; i < total_masks; i++) {
+            int bmask = i + 1;
+            for (int j = 0; j < k; j++) {
+                b0[j] = b1[j] = 0;
+                if (has0[j]) { b0[j] = bmask & 1; bmask >>= 1; }
+                if (has1[j]) { b1[j] = bmask & 1; bmask >>= 1; }
+            }
+            if (!checkOR(b0, b1, k)) continue;
+            double L, ll;
+            eval_pattern(locs, b0, b1, cfg, L, ll);
+            if (std::fabs(L) > std::fabs(maxl)) maxl = L;
+            if (updates) { accumulate(L, ll, locs, b0, b1, cfg, total); (*nexp)++; }
+        }
+        return maxl;
+    }
+
+    // postcal.cpp:307-362 nextBinary
+    static int nextBinary(vector<int>& data, int size) {
+        int i = 0, total_one = 0, index = size - 1, ones = 0;
+        while (index >= 0 && data[index] == 1) { index--; ones++; }
+        if (index >= 0)
+            while (index >= 0 && data[index] == 0) index--;
+        if (index == -1) {
+            while (i < ones + 1 && i < size) { data[i] = 1; i++; }
+            i = 0;
+            while (i < size - ones - 1) { data[i + ones + 1] = 0; i++; }
+        } else if (ones == 0) {
+            data[index] = 0;
+            data[index + 1] = 1;
+        } else {
+            data[index] = 0;
+            while (i < ones + 1) { data[i + index + 1] = 1; i++; }
+            i = 0;
+            while (i < size - index - ones - 2) { data[i + index + ones + 2] = 0; i++; }
+        }
+        for (i = 0; i < size; i++) if (data[i] == 1) total_one++;
+        return total_one;
+    }
+
+    // postcal.cpp:716-1092 computeTotalLikelihood (serial order of the omp loop)
+    double exhaustive() {
+        double sum = 0;
+        long total_iteration = 0;
+        for (long i = 0; i <= P.maxc; i++) total_iteration += nCr(P.U, (int)i);
+        vector<int> conf(P.U, 0);
+        for (long it = 0; it < total_iteration; it++) {
+            if (it > 0) nextBinary(conf, P.U);
+            vector<int> locs;
+            for (int i = 0; i < P.U; i++) if (conf[i] == 1) locs.push_back(i);
+            expand(locs, true, &sum, &A.n_eval);
+        }
+        return sum;
+    }
+
+    // postcal.cpp:400-714 computeTotalLikelihoodGivenConfigs (rows of int16 global indices)
+    double given_configs(const int16_t* rows, long nconf, int ngroups) {
+        double sum = 0;
+        vector<int> cfg(P.N, 0);
+        for (long cidx = 0; cidx < nconf; cidx++) {
+            const int16_t* in = rows + cidx * ngroups;
+            int numCausal = 0;
+            for (int i = 0; i < ngroups; i++) if (in[i] >= 0) numCausal++;
+            if (numCausal == 0) {  // postcal.cpp:459-488
+                for (int s = 0; s < P.S; s++) A.noc[s] = addlog(A.noc[s], lrl0);
+                sum = addlog(sum, lrl0);
+                A.n_eval++;
+                continue;
+            }
+            vector<int> locs;  // postcal.cpp:492-512
+            int cs = 0, cum = P.m[0];
+            for (int i = 0; i < ngroups; i++) {
+                int g = in[i];
+                if (g < 0) continue;
+                while (g >= cum) { cs++; cum += P.m[cs]; }
+                locs.push_back(P.l2u[cs][g - (cum - P.m[cs])]);
+            }
+            std::sort(locs.begin(), locs.end());
+            locs.erase(std::unique(locs.begin(), locs.end()), locs.end());
+            int k = (int)locs.size();
+            vector<int> b0(k, 0), b1(k, 0);
+            // postcal.cpp:546-590 walk: entries must appear study-major, union-ordered
+            int aux = 0;
+            while (aux < ngroups && in[aux] < 0) aux++;
+            cum = 0;
+            for (int i = 0; i < P.S; i++) {
+                cum += P.m[i];
+                for (int j = 0; j < k; j++) {
+                    int loc = P.u2l[i][locs[j]];
+                    if (loc >= 0) {
+                        int gidx = off[i] + loc;
+                        if (gidx >= cum) break;
+                        else if (aux < ngroups && in[aux] == gidx) {
+                            aux++;
+                            (i == 0 ? b0 : b1)[j] = 1;
+                            while (aux < ngroups && in[aux] < 0) aux++;
+                        }
+                    }
+                }
+                if (aux == ngroups) break;
+            }
+            if (aux != ngroups) { printf("This did not work as expected\n"); exit(1); }
+            double L, ll;
+            eval_pattern(locs, b0, b1, cfg, L, ll);
+            accumulate(L, ll, locs, b0, b1, cfg, &sum);
+            A.n_eval++;
+        }
+        return sum;
+    }
+
+    // sss_postcal.cpp:20-99 neighbourhoods
+    vector<vector<int>> nbd_plus(const vector<int>& cur) const {
+        vector<vector<int>> out;
+        if ((int)cur.size() >= P.maxc) return out;
+        vector<int> c(P.U, 0);
+        for (int v : cur) c[v] = 1;
+        for (int i = 0; i < P.U; i++)
+            if (!c[i]) {
+                vector<int> nc{i};
+                nc.insert(nc.end(), cur.begin(), cur.end());
+                std::sort(nc.begin(), nc.end());
+                out.push_back(nc);
+            }
+        return out;
+    }
+    static vector<vector<int>> nbd_minus(const vector<int>& cur) {
+        vector<vector<int>> out;
+        for (size_t i = 0; i < cur.size(); i++) {
+            vector<int> nc;
+            for (size_t j = 0; j < cur.size(); j++) if (i != j) nc.push_back(cur[j]);
+            out.push_back(nc);
+        }
+        return out;
+    }
+    vector<vector<int>> nbd_zero(const vector<int>& cur) const {
+        vector<vector<int>> out;
+        vector<int> c(P.U, 0);
+        for (int v : cur) c[v] = 1;
+        vector<vector<int>> mn = nbd_minus(cur);
+        for (int i = 0; i < P.U; i++)
+            if (!c[i])
+                for (const auto& v : mn) {
+                    vector<int> nc{i};
+                    nc.insert(nc.end(), v.begin(), v.end());
+                    std::sort(nc.begin(), nc.end());
+                    out.push_back(nc);
+                }
+        return out;
+    }
+
+    struct VecHash {  // postcal.h:43-56 (hash choice does not affect results)
+        size_t operator()(const vector<int>& v) const noexcept {
+            size_t seed = 0xCBF29CE484222325ULL;
+            for (int x : v) seed ^= (size_t)x + 0x9e3779b97f4a7c15ULL + (seed << 6) + (seed >> 2);
+            return seed;
+        }
+    };
+
+    // sss_postcal.cpp:102-380 sss_computeTotalLikelihood
+    double sss(int* iters_out) {
+        std::unordered_map<vector<int>, double, VecHash> hm;
+        std::mt19937 gen(12345);
+        vector<int> cur;
+        double old_sum = 0;
+        sss_sum = 0;
+        int iter;
+        for (iter = 0; iter < 1000; iter++) {
+            vector<vector<int>> nz = nbd_zero(cur), nm = nbd_minus(cur), np = nbd_plus(cur);
+            int num_zero = (int)nz.size(), num_minus = (int)nm.size(), num_plus = (int)np.size();
+            vector<vector<int>> nbd;
+            nbd.insert(nbd.end(), nz.begin(), nz.end());
+            nbd.insert(nbd.end(), nm.begin(), nm.end());
+            nbd.insert(nbd.end(), np.begin(), np.end());
+            bool mk = hm.find(cur) == hm.end();
+            expand(cur, mk, &sss_sum, &A.n_eval);
+            vector<double> lk(nbd.size(), 0);
+            vector<int> not_done;
+            for (size_t i = 0; i < nbd.size(); i++) {
+                auto it = hm.find(nbd[i]);
+                if (it != hm.end()) lk[i] = it->second;
+                else { lk[i] = expand(nbd[i], true, &sss_sum, &A.n_eval); not_done.push_back((int)i); }
+            }
+            if (not_done.empty()) { printf("hit break condition\n"); break; }
+            if (iter >= 100 && (1 - std::exp(old_sum - sss_sum)) <= 0.001) { printf("hit convergence condition\n"); break; }
+            for (int i : not_done) hm[nbd[i]] = lk[i];
+            double wz = 0, wm = 0, wp = 0;
+            size_t zs = nbd.size(), ms = nbd.size(), ps = nbd.size();
+            auto group = [&](int b, int e, double& wsum, size_t& smp) {
+                vector<double> pr;
+                double mx = *std::max_element(lk.begin() + b, lk.begin() + e);
+                for (int ii = b; ii < e; ii++) pr.push_back(std::exp(lk[ii] - mx));
+                std::discrete_distribution<size_t> dist(pr.begin(), pr.end());
+                smp = dist(gen);
+                wsum = std::accumulate(pr.begin(), pr.end(), 0.0);
+            };
+            if (num_zero != 0) group(0, num_zero, wz, zs);
+            if (num_minus != 0) group(num_zero, num_zero + num_minus, wm, ms);
+            if (num_plus != 0) group(num_zero + num_minus, (int)lk.size(), wp, ps);
+            std::discrete_distribution<size_t> dist({wz, wm, wp});
+            size_t idx = dist(gen), fin = 0;
+            switch (idx) {
+                case 0: fin = zs; break;
+                case 1: fin = ms + num_zero; break;
+                case 2: fin = ps + num_zero + num_minus; break;
+            }
+            cur = nbd[fin];
+            old_sum = sss_sum;
+        }
+        if (iters_out) *iters_out = iter;
+        return sss_sum;
+    }
+};
+
+// postcal.h:277-283 special_exp
+static double special_exp(double post, double total) { return post == 0 ? 0 : std::exp(post - total); }
+
+// postcal.cpp:1128-1164 (finalisation that affects files), model.h:282-310 and
+// postcal.h:288-336 (file writers)
+static void write_outputs(const Problem& P, const Inputs& in, const Accum& A, double totalLog,
+                          const string& out) {
+    {
+        std::ofstream lf((out + "_log.txt").c_str(), std::ios::out | std::ios::app);  // util.cpp:183-187
+        lf << std::exp(totalLog) << std::endl;
+    }
+    vector<char> set(P.N, '0');
+    for (int i = 0; i < P.N; i++)
+        if (special_exp(A.post[i], totalLog) > 0.05) set[i] = '1';
+    int so = 0;
+    for (int s = 0; s < P.S; s++) {
+        std::ofstream f((out + "_study" + std::to_string(s) + "_set.txt").c_str());
+        for (int j = 0; j < P.m[s]; j++)
+            if (set[so + j] == '1') f << in.names[s][j] << std::endl;
+        so += P.m[s];
+    }
+    so = 0;
+    for (int s = 0; s < P.S; s++) {
+        std::ofstream f((out + "_study" + std::to_string(s) + "_post.txt").c_str());
+        f << "SNP_ID\tProb_in_pCausalSet" << std::endl;
+        for (int j = 0; j < P.m[s]; j++) f << in.names[s][j] << "\t" << special_exp(A.post[so + j], totalLog) << std::endl;
+        so += P.m[s];
+    }
+    {
+        std::ofstream f((out + "_nocausal.txt").c_str());
+        for (int s = 0; s < P.S; s++) f << special_exp(A.noc[s], totalLog) << std::endl;
+    }
+    {
+        std::ofstream f((out + "_shared_pips.txt").c_str());
+        f << "SNP_ID\tshared_pip\tshared_ll\tnotshared_ll" << std::endl;
+        for (int u = 0; u < P.U; u++)
+            f << in.all_snp_pos[u] << "\t" << special_exp(A.shared[u], totalLog) << "\t" << A.sll[u] << "\t"
+              << A.nsll[u] << std::endl;
+    }
+}
+
+}  // namespace orc
+
+// ---------------------------------------------------------------------------
+// C API for ctypes (tests) — all accumulators in the reference's log-space
+// convention (0 = empty), full precision.
+// ---------------------------------------------------------------------------
+extern "C" {
+
+// mode: 0 exhaustive, 1 sss, 2 configs-file rows.  literal: 0 reduced k x k, 1 N x N.
+int oracle_postcal(int n_studies, const int* m, const double* B, const double* s_prime, int n_union,
+                   const int* union_to_local, int max_causal, const int* sample_sizes, double p,
+                   double gamma, double t2, double s2, int mode, const int16_t* rows, long n_rows,
+                   int n_groups, int literal, double* post, double* no_causal, double* shared,
+                   double* shared_ll, double* notshared_ll, double* total, long* n_eval) {
+    if (n_studies != 2) return -1;
+    orc::Problem P;
+    P.S = n_studies;
+    P.m.assign(m, m + n_studies);
+    P.N = m[0] + m[1];
+    size_t bo = 0;
+    P.B.resize(2);
+    for (int s = 0; s < 2; s++) {
+        P.B[s].assign(B + bo, B + bo + (size_t)m[s] * m[s]);
+        bo += (size_t)m[s] * m[s];
+    }
+    P.sp.assign(s_prime, s_prime + P.N);
+    P.U = n_union;
+    P.u2l.assign(2, vector<int>(n_union));
+    P.l2u.assign(2, {});
+    for (int s = 0; s < 2; s++)
+        for (int u = 0; u < n_union; u++) {
+            P.u2l[s][u] = union_to_local[s * n_union + u];
+            if (P.u2l[s][u] >= 0) P.l2u[s].push_back(u);
+        }
+    P.maxc = max_causal;
+    P.n.assign(sample_sizes, sample_sizes + 2);
+    P.p = p; P.gamma = gamma; P.t2 = t2; P.s2 = s2;
+    orc::PostCal pc(P, literal != 0);
+    double tot = 0;
+    if (mode == 0) tot = pc.exhaustive();
+    else if (mode == 1) tot = pc.sss(nullptr);
+    else tot = pc.given_configs(rows, n_rows, n_groups);
+    std::copy(pc.A.post.begin(), pc.A.post.end(), post);
+    std::copy(pc.A.noc.begin(), pc.A.noc.end(), no_causal);
+    std::copy(pc.A.shared.begin(), pc.A.shared.end(), shared);
+    std::copy(pc.A.sll.begin(), pc.A.sll.end(), shared_ll);
+    std::copy(pc.A.nsll.begin(), pc.A.nsll.end(), notshared_ll);
+    *total = tot;
+    *n_eval = pc.A.n_eval;
+    return 0;
+}
+
+// Evaluate (L, ll) of single patterns (tests of the per-configuration kernel).
+// sets: [n_sets][k] union indices (ascending); b: [n_sets][2][k] per-study bits.
+int oracle_eval_patterns(int n_studies, const int* m, const double* B, const double* s_prime, int n_union,
+                         const int* union_to_local, const int* sample_sizes, double p, double gamma,
+                         double t2, double s2, int k, int n_sets, const int* sets, const int* bits,
+                         int literal, double* L_out, double* ll_out) {
+    if (n_studies != 2) return -1;
+    orc::Problem P;
+    P.m.assign(m, m + 2);
+    P.N = m[0] + m[1];
+    size_t bo = 0;
+    P.B.resize(2);
+    for (int s = 0; s < 2; s++) { P.B[s].assign(B + bo, B + bo + (size_t)m[s] * m[s]); bo += (size_t)m[s] * m[s]; }
+    P.sp.assign(s_prime, s_prime + P.N);
+    P.U = n_union;
+    P.u2l.assign(2, vector<int>(n_union));
+    for (int s = 0; s < 2; s++) for (int u = 0; u < n_union; u++) P.u2l[s][u] = union_to_local[s * n_union + u];
+    P.n.assign(sample_sizes, sample_sizes + 2);
+    P.p = p; P.gamma = gamma; P.t2 = t2; P.s2 = s2;
+    orc::PostCal pc(P, literal != 0);
+    vector<int> cfg(P.N, 0);
+    for (int i = 0; i < n_sets; i++) {
+        vector<int> locs(sets + (size_t)i * k, sets + (size_t)(i + 1) * k);
+        vector<int> b0(bits + (size_t)i * 2 * k, bits + (size_t)i * 2 * k + k);
+        vector<int> b1(bits + (size_t)i * 2 * k + k, bits + (size_t)(i + 1) * 2 * k);
+        pc.eval_pattern(locs, b0, b1, cfg, L_out[i], ll_out[i]);
+    }
+    return 0;
+}
+
+// Setup restatement (model.h:60-264): files -> PostCal seam inputs.
+// Buffers must be sized by the caller (query with oracle_setup_dims first).
+int oracle_setup_dims(const char* ld0, const char* ld1, const char* z0, const char* z1, const char* map,
+                      int* m_out, int* n_union_out) {
+    orc::Problem P;
+    orc::Inputs in;
+    vector<string> ld{ld0, ld1}, zf{z0, z1};
+    // cheap path: sizes only
+    for (int i = 0; i < 2; i++) {
+        vector<double> L;
+        if (!orc::import_data(ld[i], L)) return 1;
+        m_out[i] = (int)std::sqrt((double)L.size());
+    }
+    vector<string> first;
+    vector<vector<int>> rest(2);
+    if (!orc::import_snp_map(map, 3, first, rest)) return 1;
+    *n_union_out = (int)first.size();
+    return 0;
+}
+
+int oracle_setup(const char* ld0, const char* ld1, const char* z0, const char* z1, const char* map,
+                 double* B_out, double* sp_out, int* u2l_out, double* psd_add_out) {
+    orc::Problem P;
+    orc::Inputs in;
+    vector<string> ld{ld0, ld1}, zf{z0, z1};
+    int rc = orc::model_setup(ld, zf, map, P, in);
+    if (rc) return rc;
+    size_t bo = 0;
+    for (int s = 0; s < 2; s++) {
+        std::copy(P.B[s].begin(), P.B[s].end(), B_out + bo);
+        bo += P.B[s].size();
+        psd_add_out[s] = in.psd_add[s];
+    }
+    std::copy(P.sp.begin(), P.sp.end(), sp_out);
+    for (int s = 0; s < 2; s++)
+        for (int u = 0; u < P.U; u++) u2l_out[s * P.U + u] = P.u2l[s][u];
+    return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// CLI mirroring pipsort.cpp:68-228 (for end-to-end golden-file comparison)
+// ---------------------------------------------------------------------------
+#ifdef ORACLE_MAIN
+static vector<string> read_dir(const string& fn) {  // pipsort.cpp:28-44
+    vector<string> d;
+    std::ifstream fin(fn.c_str());
+    if (!fin) { std::cout << "Error: unable to open " << fn << std::endl; exit(1); }
+    string s;
+    while (fin.good()) { std::getline(fin, s); if (s != "") d.push_back(s); }
+    return d;
+}
+static vector<int> read_sigma(const string& ss) {  // pipsort.cpp:46-66
+    vector<int> sizes;
+    string cur = "";
+    for (char ch : ss) {
+        if (ch == ',') { sizes.push_back((int)std::stod(cur)); cur = ""; }
+        else if (isdigit((unsigned char)ch)) cur += ch;
+        else { std::cout << "Error: sample size is not in the right format" << std::endl; exit(1); }
+    }
+    if (cur != "") sizes.push_back((int)std::stod(cur));
+    return sizes;
+}
+
+int main(int argc, char** argv) {
+    int maxc = 3, oc, sss_flag = 0, num_groups = 0, num_configs = 0, literal = 0;
+    double gamma = 0.01, p = 0.75, t2 = 0.52, s2 = 5.2;
+    string ldf, zf, mapf, out, ss, configs;
+    while ((oc = getopt(argc, argv, "vhl:o:z:m:p:r:c:k:g:f:t:s:n:a:b:d:e:q:xL:")) != -1) {
+        if (optarg == NULL || *optarg == '\0') { printf("optarg is NULL\n"); exit(1); }
+        switch (oc) {
+            case 'l': ldf = optarg; break;
+            case 'o': out = optarg; break;
+            case 'z': zf = optarg; break;
+            case 'm': mapf = optarg; /* fallthrough: pipsort.cpp:128-131 */
+            case 'n': ss = optarg; break;
+            case 'b': configs = optarg; break;
+            case 'd': num_configs = atoi(optarg); break;
+            case 'e': num_groups = atoi(optarg); break;
+            case 'p': p = atof(optarg); break;
+            case 'c': maxc = atoi(optarg); break;
+            case 'g': gamma = atof(optarg); break;
+            case 't': t2 = atof(optarg); break;
+            case 's': s2 = atof(optarg); break;
+            case 'q': sss_flag = std::stoi(optarg); break;
+            case 'L': literal = atoi(optarg); break;
+            default: break;
+        }
+    }
+    if (ldf == "" || zf == "" || mapf == "" || out == "" || ss == "") {
+        std::cout << "Error: -l, -z, -o, and -n are required" << std::endl;
+        exit(1);
+    }
+    vector<string> ld = read_dir(ldf), z = read_dir(zf);
+    vector<int> n = read_sigma(ss);
+    orc::Problem P;
+    orc::Inputs in;
+    if (orc::model_setup(ld, z, mapf, P, in)) return 1;
+    P.maxc = maxc; P.n = n; P.p = p; P.gamma = gamma; P.t2 = t2; P.s2 = s2;
+    orc::PostCal pc(P, literal != 0);
+    auto t0 = std::chrono::steady_clock::now();
+    double tot;
+    int iters = 0;
+    if (configs != "") {
+        int fd = open(configs.c_str(), O_RDONLY);
+        if (fd < 0) { printf("mmap did not succeed\n"); exit(1); }
+        struct stat st; fstat(fd, &st);
+        if ((size_t)num_configs * num_groups * sizeof(int16_t) != (size_t)st.st_size) {
+            printf("config file is not the expected size\n"); exit(1);
+        }
+        vector<int16_t> rows((size_t)num_configs * num_groups);
+        if (read(fd, rows.data(), st.st_size) != st.st_size) exit(1);
+        close(fd);
+        tot = pc.given_configs(rows.data(), num_configs, num_groups);
+    } else if (sss_flag == 1) {
+        tot = pc.sss(&iters);
+    } else {
+        tot = pc.exhaustive();
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    std::cout << "Time to eval all= " << std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count()
+              << "[µs]" << std::endl;
+    printf("configs evaluated = %ld\n", pc.A.n_eval);
+    orc::write_outputs(P, in, pc.A, tot, out);
+    return 0;
+}
+#endif
