@@ -1,0 +1,140 @@
+/*
+ * pipsort_engine.h — C ABI of the MI355X posterior-calculation engine.
+ *
+ * Drop-in boundary for the reference's PostCal class (CAST-genomics/pipsort).
+ * The reference has no FFI; its seam is the PostCal object that Model builds and
+ * drives (model.h:265 constructs it, model.h:274 runs it, model.h:304 prints it).
+ * Each entry point below names the reference interface it replaces.  Inputs are
+ * exactly PostCal's constructor inputs (postcal.h:118); outputs are PostCal's
+ * accumulator arrays in the same log-space convention (0 == "empty",
+ * postcal.h:102-112) plus totalLikeLihoodLOG.
+ *
+ * Plain C types only: host pointers and sizes; no torch/HIP types.  Every
+ * function returns 0 on success and a negative PSX_E* code on failure (message
+ * via psx_last_error()).  The engine is single-host-thread per handle, not
+ * reentrant per handle; one handle drives one GPU.  There is no CPU fallback:
+ * psx_create fails with PSX_ENODEV when no HIP device is present.
+ */
+#ifndef PIPSORT_ENGINE_H
+#define PIPSORT_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSX_ABI_VERSION 1
+
+#define PSX_OK 0
+#define PSX_EINVAL (-1)    /* bad argument / unsupported problem shape        */
+#define PSX_ENODEV (-2)    /* no HIP device (no silent CPU fallback)          */
+#define PSX_EHIP (-3)      /* HIP runtime error                               */
+#define PSX_ESINGULAR (-4) /* postcal.cpp:291-294 "matrix is singular" (ref exits 0) */
+#define PSX_EORDER (-5)    /* postcal.cpp:587-590 "This did not work as expected" */
+#define PSX_ERANGE (-6)    /* sweep too large to index / unsupported c        */
+
+typedef struct psx_engine psx_engine;
+
+/* PostCal constructor inputs (postcal.h:118; built by Model at model.h:213-265). */
+typedef struct {
+    int32_t n_studies;              /* num_of_studies; must be 2 (postcal.cpp:20-23, model.h:125) */
+    const int32_t *m;               /* [n_studies] num_snps_all                                  */
+    const double *B;                /* BIG_SIGMA diagonal blocks B_s, column-major M_s x M_s,
+                                       concatenated (model.h:239,262)                            */
+    const double *s_prime;          /* [N = sum m] S_LONG_VEC after the low-rank transform       */
+    int32_t n_union;                /* unionSnpCount = rows of the snp map                       */
+    const int32_t *union_to_local;  /* [n_studies][n_union] idx_to_snp_map, -1 = absent          */
+    int32_t max_causal;             /* MAX_causal (-c)                                           */
+    const int32_t *sample_sizes;    /* [n_studies] (-n)                                          */
+    double sharing_param;           /* -p */
+    double gamma;                   /* -g */
+    double t_squared;               /* -t */
+    double s_squared;               /* -s */
+} psx_problem;
+
+/* PostCal accumulators (postcal.h:62-78), caller-owned host arrays. */
+typedef struct {
+    double *post;         /* [N]          postValues                    */
+    double *no_causal;    /* [n_studies]  noCausal                      */
+    double *shared;       /* [n_union]    sharedPips                    */
+    double *shared_ll;    /* [n_union]    sharedLL                      */
+    double *notshared_ll; /* [n_union]    notSharedLL                   */
+    double total;         /* totalLikeLihoodLOG (sum over all configs)  */
+    uint64_t n_configs;   /* configurations evaluated (incl. null)      */
+} psx_accum;
+
+typedef struct {
+    double sweep_ms;        /* wall time of the last psx_run_* (HIP events, engine stream) */
+    double kernel_ms;       /* summed device time of the dominant sweep kernel             */
+    int32_t kernel_launches;/* launches of that kernel in the last run                     */
+    double merge_ms;        /* device time of the record-merge kernels                     */
+    uint64_t configs;       /* configurations evaluated by this handle in the last run     */
+    uint64_t union_sets;    /* union subsets evaluated by the dominant kernel              */
+    double alg_bytes;       /* algorithmic bytes of the dominant kernel      */
+    double flops;           /* FP64 operation estimate of the dominant kernel              */
+} psx_timing;
+
+int32_t psx_abi_version(void);
+const char *psx_last_error(void);
+
+/* Number of HIP devices visible (0 on a host without a GPU; never initialises a context). */
+int psx_device_count(int *count);
+
+/* PostCal::PostCal (postcal.h:118-195).  Copies the problem to device `device`,
+ * forms Sigma~_s = B_s^T B_s, y_s = B_s^T S'_s and ||S'||^2 on the GPU. */
+int psx_create(const psx_problem *prob, int device, psx_engine **out);
+void psx_destroy(psx_engine *e);
+
+/* Multi-GPU sharding of the exhaustive sweep (one process per GPU): this handle
+ * evaluates shard `rank` of `world` equal slices of every causal-set level; the
+ * null configuration belongs to rank 0.  Default (0, 1). */
+int psx_set_shard(psx_engine *e, int rank, int world);
+
+/* PostCal::computeTotalLikelihood (postcal.cpp:716-1092): exhaustive sweep over
+ * all union subsets of size <= max_causal and all per-study assignments passing
+ * checkOR (postcal.cpp:1111-1126).  Resets and fills the accumulators. */
+int psx_run_exhaustive(psx_engine *e);
+
+/* PostCal::computeTotalLikelihoodGivenConfigs (postcal.cpp:400-714): rows of
+ * int16 global SNP indices (-1 = none), [n_rows][n_groups] (the -b file). */
+int psx_run_configs(psx_engine *e, const int16_t *rows, int64_t n_rows, int32_t n_groups);
+
+/* PostCal::sss_computeTotalLikelihood (sss_postcal.cpp:102-380): stochastic
+ * shotgun search, host random walk (mt19937(12345)) + GPU neighbour batches. */
+int psx_run_sss(psx_engine *e, int32_t *iterations_out);
+
+/* PostCal::expand_and_compute_lkl (sss_postcal.cpp:447-685), batched: evaluate
+ * n_sets union sets (ascending union indices, -1 padded to `stride`), return the
+ * SSS score (pattern L with largest |L|, sss_postcal.cpp:624-626) per set and,
+ * if accumulate != 0, add every pattern into the accumulators. */
+int psx_eval_union_batch(psx_engine *e, const int32_t *sets, int32_t stride, int32_t n_sets,
+                         int accumulate, double *score_out);
+
+/* Zero the accumulators (PostCal constructor state, postcal.h:129-160). */
+int psx_reset(psx_engine *e);
+
+/* Read PostCal's accumulators (postValues, noCausal, sharedPips, sharedLL,
+ * notSharedLL, totalLikeLihoodLOG) in the reference's log-space convention. */
+int psx_get_accum(psx_engine *e, psx_accum *out);
+
+/* Multi-process reduction of the accumulators (the single exchange step of the
+ * sharded sweep).  Partials are opaque device bytes: export this handle's
+ * partial into a caller device buffer of psx_partials_bytes() bytes, gather
+ * them from all ranks (e.g. one RCCL all-gather), then merge `count`
+ * concatenated partials (rank order) into this handle's accumulators. */
+int64_t psx_partials_bytes(psx_engine *e);
+int psx_export_partials(psx_engine *e, void *device_dst);
+int psx_merge_partials(psx_engine *e, const void *device_src, int32_t count);
+
+/* Timing of the last psx_run_* on this handle. */
+int psx_get_timing(psx_engine *e, psx_timing *t);
+
+/* Number of configurations an exhaustive sweep evaluates (null included):
+ * sum_{k<=c} e_k(w), w_u = 2^{#studies containing u} - 1. */
+uint64_t psx_count_configs(const psx_problem *prob);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PIPSORT_ENGINE_H */

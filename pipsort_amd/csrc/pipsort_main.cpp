@@ -1,0 +1,378 @@
+// pipsort_main.cpp — the PIPSORT command line, drop-in for the reference
+// driver (pipsort.cpp:68-228 + Model, model.h:60-310), with PostCal replaced
+// by the MI355X engine behind include/pipsort_engine.h.
+//
+// Same options (optstring of pipsort.cpp:90, including its quirks: -m falls
+// through into -n, options without an argument abort with "optarg is NULL"),
+// same input formats and the same output files.
+#include <fcntl.h>
+#include <getopt.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/pipsort_engine.h"
+#include "../../include/pipsort_model.h"
+
+using std::string;
+using std::vector;
+
+namespace {
+
+// pipsort.cpp:28-44
+vector<string> read_dir(const string& fn) {
+    vector<string> dirs;
+    std::ifstream fin(fn.c_str());
+    if (!fin) {
+        std::cout << "Error: unable to open " << fn << std::endl;
+        exit(1);
+    }
+    string line;
+    while (fin.good()) {
+        std::getline(fin, line);
+        if (line != "") dirs.push_back(line);
+    }
+    return dirs;
+}
+
+// pipsort.cpp:46-66
+vector<int> read_sigma(const string& s) {
+    vector<int> sizes;
+    string cur = "";
+    for (char ch : s) {
+        if (ch == ',') {
+            sizes.push_back((int)std::stod(cur));
+            cur = "";
+        } else if (isdigit((unsigned char)ch)) {
+            cur += ch;
+        } else {
+            std::cout << "Error: sample size is not in the right format" << std::endl;
+            exit(1);
+        }
+    }
+    if (cur != "") sizes.push_back((int)std::stod(cur));
+    return sizes;
+}
+
+// util.cpp:86-96 importData: doubles separated by whitespace, stopping at the
+// first token `istream >> double` would reject.  mmap + strtod for speed.
+bool import_data(const string& fn, vector<double>& out) {
+    int fd = open(fn.c_str(), O_RDONLY);
+    if (fd < 0) {
+        std::cout << "Unable to open file; This is why";
+        return false;
+    }
+    struct stat st;
+    fstat(fd, &st);
+    size_t len = (size_t)st.st_size;
+    if (len == 0) { close(fd); return true; }
+    char* p = (char*)mmap(nullptr, len + 1, PROT_READ, MAP_PRIVATE, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) return false;
+    string buf(p, len);  // NUL-terminated copy for strtod
+    munmap(p, len + 1);
+    const char* s = buf.c_str();
+    const char* end = s + len;
+    out.reserve(len / 8);
+    while (s < end) {
+        while (s < end && isspace((unsigned char)*s)) s++;
+        if (s >= end) break;
+        char c = *s;
+        if (!(isdigit((unsigned char)c) || c == '-' || c == '+' || c == '.')) break;
+        char* e = nullptr;
+        double v = strtod(s, &e);
+        if (e == s) break;
+        out.push_back(v);
+        s = e;
+    }
+    return true;
+}
+
+// util.cpp:132-159 (first column names, second column z)
+void import_z(const string& fn, vector<string>& names, vector<double>& z) {
+    std::ifstream fin(fn.c_str());
+    string line, first = "", second;
+    double d = 0.0;
+    while (std::getline(fin, line)) {
+        std::istringstream a(line);
+        a >> first;
+        names.push_back(first);
+        std::istringstream b(line);
+        b >> second;
+        b >> d;
+        z.push_back(d);
+    }
+}
+
+// util.cpp:99-126
+bool import_snp_map(const string& fn, int ncols, vector<string>& first, vector<vector<int>>& rest) {
+    std::ifstream f(fn.c_str());
+    if (!f.is_open()) {
+        std::cout << "Could not open file\n";
+        return false;
+    }
+    string line, word;
+    while (std::getline(f, line)) {
+        std::stringstream s(line);
+        for (int i = 0; i < ncols; i++) {
+            std::getline(s, word, ',');
+            if (i == 0) first.push_back(word);
+            else rest[i - 1].push_back(std::stoi(word));
+        }
+    }
+    return true;
+}
+
+double special_exp(double post, double total) { return post == 0 ? 0 : std::exp(post - total); }  // postcal.h:277-283
+
+int die_engine(int rc) {
+    std::cout << "engine error (" << rc << "): " << psx_last_error() << std::endl;
+    if (rc == PSX_ESINGULAR) {
+        std::cout << "Error the matrix is singular and we fail to fix it (low rank lkl)." << std::endl;
+        exit(0);  // postcal.cpp:291-294
+    }
+    if (rc == PSX_EORDER) {
+        printf("This did not work as expected\n");
+        exit(1);
+    }
+    exit(1);
+}
+
+}  // namespace
+
+int main(int argc, char* argv[]) {
+    int totalCausalSNP = 3;  // pipsort.cpp:69-77
+    double gamma = 0.01, sharing_param = 0.75, rho = 0.95, tau_sqr = 0.52, sigma_g_squared = 5.2;
+    double cutoff_threshold = 0;
+    string ldFile = "", zFile = "", snpMapFile = "", outputFileName = "", sample_s = "", num_causal_s = "";
+    string configsFile = "";
+    int num_groups = 0, num_configs = 0, sss_flag = 0, oc = 0;
+    while ((oc = getopt(argc, argv, "vhl:o:z:m:p:r:c:k:g:f:t:s:n:a:b:d:e:q:x")) != -1) {
+        if (optarg == NULL || *optarg == '\0') {  // pipsort.cpp:92-95
+            printf("optarg is NULL\n");
+            exit(1);
+        }
+        switch (oc) {
+            case 'l': ldFile = optarg; break;
+            case 'o': outputFileName = optarg; break;
+            case 'z': zFile = optarg; break;
+            case 'm': snpMapFile = optarg; /* falls through, pipsort.cpp:128-131 */
+            case 'n': sample_s = optarg; break;
+            case 'b': configsFile = optarg; break;
+            case 'd': num_configs = atoi(optarg); break;
+            case 'e': num_groups = atoi(optarg); break;
+            case 'p': sharing_param = atof(optarg); break;
+            case 'r': rho = atof(optarg); break;
+            case 'c': totalCausalSNP = atoi(optarg); break;
+            case 'k': num_causal_s = optarg; break;
+            case 'g': gamma = atof(optarg); break;
+            case 'f': break;
+            case 't': tau_sqr = atof(optarg); break;
+            case 's': sigma_g_squared = atof(optarg); break;
+            case 'q': sss_flag = std::stoi(optarg); break;
+            case ':':
+            case '?':
+            case 'a': cutoff_threshold = atof(optarg); break;
+            case 'x': printf("Hello world flag x\n"); break;
+            default: break;
+        }
+    }
+    if (ldFile == "" || zFile == "" || snpMapFile == "" || outputFileName == "" || sample_s == "") {
+        std::cout << "Error: -l, -z, -o, and -n are required" << std::endl;
+        exit(1);
+    }
+    if (configsFile != "") {
+        if (num_configs <= 0) {
+            std::cout << "Number of configs must be greater than 0" << std::endl;
+            exit(1);
+        }
+        if (num_groups <= 0) std::cout << "Number of groups must be greater than 0" << std::endl;
+    }
+    vector<string> ldDir = read_dir(ldFile), zDir = read_dir(zFile);
+    vector<int> sample_sizes = read_sigma(sample_s);
+    if (ldDir.size() != zDir.size() || ldDir.size() != sample_sizes.size()) {
+        std::cout << "Error: LD files, Z files, and sample sizes do not match in number" << std::endl;
+        exit(1);
+    }
+    const int S = (int)ldDir.size();
+    if (S != 2) {
+        std::cout << "This prior does not work for more than 2 studies yet\n";
+        exit(1);
+    }
+    auto t_setup0 = std::chrono::steady_clock::now();
+    // ---- Model (model.h:86-264) ----
+    vector<vector<double>> sig(S), zs(S);
+    vector<vector<string>> names(S);
+    vector<int> m(S);
+    for (int i = 0; i < S; i++) {
+        vector<double> L;
+        if (!import_data(ldDir[i], L)) exit(1);
+        import_z(zDir[i], names[i], zs[i]);
+        int M = (int)std::sqrt((double)L.size());  // model.h:98
+        m[i] = M;
+        if (M != (int)names[i].size()) {
+            printf("ERROR: LD matrix is size %d x %d but zscores has %lu snps\n. Check LD file for nans.\n", M, M,
+                   (unsigned long)names[i].size());
+            exit(1);
+        }
+        printf("pushing back num snps %d for study %d\n", i, M);
+        L.resize((size_t)M * M);
+        sig[i] = std::move(L);
+    }
+    vector<string> all_snp_pos;
+    vector<vector<int>> u2l(S);
+    if (!import_snp_map(snpMapFile, S + 1, all_snp_pos, u2l)) exit(1);
+    const int U = (int)all_snp_pos.size();
+    for (int i = 0; i < S; i++) {  // model.h:134-144
+        int cnt = 0;
+        if ((int)u2l[i].size() != U) { printf("Invariant does not hold\n"); exit(1); }
+        for (int u = 0; u < U; u++) cnt += u2l[i][u] >= 0;
+        if (cnt != m[i]) { printf("Invariant does not hold\n"); exit(1); }
+    }
+    const int N = m[0] + m[1];
+    vector<double> B, sp(N);
+    size_t boff = 0;
+    int off = 0;
+    B.resize((size_t)m[0] * m[0] + (size_t)m[1] * m[1]);
+    for (int i = 0; i < S; i++) {
+        auto b0 = std::chrono::steady_clock::now();
+        double add = 0;
+        psx_psd_shift(sig[i].data(), m[i], &add);  // model.h:194
+        auto b1 = std::chrono::steady_clock::now();
+        std::cout << "Time to make psd = " << std::chrono::duration_cast<std::chrono::microseconds>(b1 - b0).count()
+                  << "[µs]" << std::endl;
+        psx_lowrank_study(sig[i].data(), zs[i].data(), m[i], B.data() + boff, sp.data() + off);  // model.h:213-259
+        auto b2 = std::chrono::steady_clock::now();
+        std::cout << "Time for eigen decomp = "
+                  << std::chrono::duration_cast<std::chrono::microseconds>(b2 - b1).count() << "[µs]" << std::endl;
+        boff += (size_t)m[i] * m[i];
+        off += m[i];
+    }
+    vector<int32_t> u2l_flat(2 * U);
+    for (int s = 0; s < 2; s++)
+        for (int u = 0; u < U; u++) u2l_flat[s * U + u] = u2l[s][u];
+    psx_problem prob;
+    prob.n_studies = 2;
+    prob.m = m.data();
+    prob.B = B.data();
+    prob.s_prime = sp.data();
+    prob.n_union = U;
+    prob.union_to_local = u2l_flat.data();
+    prob.max_causal = totalCausalSNP;
+    prob.sample_sizes = sample_sizes.data();
+    prob.sharing_param = sharing_param;
+    prob.gamma = gamma;
+    prob.t_squared = tau_sqr;
+    prob.s_squared = sigma_g_squared;
+    int device = 0;
+    if (const char* d = getenv("PSX_DEVICE")) device = atoi(d);
+    psx_engine* eng = nullptr;
+    int rc = psx_create(&prob, device, &eng);  // model.h:265
+    if (rc) die_engine(rc);
+    auto t_setup1 = std::chrono::steady_clock::now();
+    std::cout << "Time for setup = " << std::chrono::duration_cast<std::chrono::microseconds>(t_setup1 - t_setup0).count()
+              << "[µs]" << std::endl;
+    // ---- findOptimalSetGreedy (postcal.cpp:1128-1244) ----
+    std::cout << "Max Causal = " << totalCausalSNP << std::endl;
+    std::cout << "Union Snp Count = " << U << std::endl;
+    auto t0 = std::chrono::steady_clock::now();
+    if (configsFile != "") {
+        int fd = open(configsFile.c_str(), O_RDONLY);  // util.cpp:26-49
+        if (fd < 0) {
+            printf("Could not open %s\n", configsFile.c_str());
+            printf("mmap did not succeed\n");
+            exit(1);
+        }
+        struct stat st;
+        fstat(fd, &st);
+        size_t sz = (size_t)st.st_size;
+        if ((size_t)num_configs * num_groups * sizeof(int16_t) != sz) {  // postcal.cpp:434-437
+            printf("config file is not the expected size\n");
+            exit(1);
+        }
+        void* p = sz ? mmap(nullptr, sz, PROT_READ, MAP_SHARED, fd, 0) : nullptr;
+        close(fd);
+        rc = psx_run_configs(eng, (const int16_t*)p, num_configs, num_groups);
+        if (p) munmap(p, sz);
+    } else if (sss_flag == 1) {
+        int32_t iters = 0;
+        rc = psx_run_sss(eng, &iters);
+        printf("sss iterations = %d\n", iters);
+    } else {
+        rc = psx_run_exhaustive(eng);
+    }
+    if (rc) die_engine(rc);
+    auto t1 = std::chrono::steady_clock::now();
+    std::cout << "Time to eval all= " << std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count()
+              << "[µs]" << std::endl;
+    vector<double> post(N), noc(2), shared(U), sll(U), nsll(U);
+    psx_accum acc;
+    acc.post = post.data();
+    acc.no_causal = noc.data();
+    acc.shared = shared.data();
+    acc.shared_ll = sll.data();
+    acc.notshared_ll = nsll.data();
+    if ((rc = psx_get_accum(eng, &acc))) die_engine(rc);
+    psx_timing tm;
+    psx_get_timing(eng, &tm);
+    printf("num total configs = %llu\n", (unsigned long long)acc.n_configs);
+    printf("sweep device time = %.3f ms (kernel %.3f ms, merge %.3f ms)\n", tm.sweep_ms, tm.kernel_ms, tm.merge_ms);
+    const double total = acc.total;
+    {
+        std::ofstream lf((outputFileName + "_log.txt").c_str(), std::ios::out | std::ios::app);  // util.cpp:183-187
+        lf << std::exp(total) << std::endl;
+    }
+    double total_post = 0;
+    printf("\nTotal Likelihood = %e SNP=%d \n", total_post, N);
+    printf("total post as total likelihood log = %f\n", total);
+    for (int i = 0; i < 2; i++) {
+        printf("no causal just value %f\n", noc[i]);
+        printf("Prob of no causal for study %d is %f\n", i, std::exp(noc[i] - total));
+    }
+    vector<char> causalSet(N, '0');
+    for (int i = 0; i < N; i++)
+        if (special_exp(post[i], total) > 0.05) causalSet[i] = '1';  // postcal.cpp:1158-1164
+    // ---- finishUp (model.h:282-310) + printPost2File (postcal.h:288-336) ----
+    int so = 0;
+    for (int s = 0; s < 2; s++) {
+        std::ofstream f((outputFileName + "_study" + std::to_string(s) + "_set.txt").c_str());
+        for (int j = 0; j < m[s]; j++)
+            if (causalSet[so + j] == '1') f << names[s][j] << std::endl;
+        so += m[s];
+    }
+    so = 0;
+    for (int s = 0; s < 2; s++) {
+        std::ofstream f((outputFileName + "_study" + std::to_string(s) + "_post.txt").c_str());
+        f << "SNP_ID\tProb_in_pCausalSet" << std::endl;
+        for (int j = 0; j < m[s]; j++) f << names[s][j] << "\t" << special_exp(post[so + j], total) << std::endl;
+        so += m[s];
+    }
+    {
+        std::ofstream f((outputFileName + "_nocausal.txt").c_str());
+        for (int s = 0; s < 2; s++) f << special_exp(noc[s], total) << std::endl;
+    }
+    {
+        std::ofstream f((outputFileName + "_shared_pips.txt").c_str());
+        f << "SNP_ID\tshared_pip\tshared_ll\tnotshared_ll" << std::endl;
+        for (int u = 0; u < U; u++)
+            f << all_snp_pos[u] << "\t" << special_exp(shared[u], total) << "\t" << sll[u] << "\t" << nsll[u]
+              << std::endl;
+    }
+    psx_destroy(eng);
+    (void)rho;
+    (void)cutoff_threshold;
+    (void)num_causal_s;
+    return 0;
+}

@@ -1,0 +1,1041 @@
+// psx_engine.hip — MI355X (gfx950) posterior-calculation engine for PIPSORT.
+//
+// Replaces PostCal's configuration sweep (postcal.cpp:400-1092,
+// sss_postcal.cpp:102-685) with HIP kernels.  See DESIGN.md for the data layout
+// and the kernel inventory; psx_math.h for the accumulator representation.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <random>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pipsort_engine.h"
+#include "psx_math.h"
+#include "psx_sweep.h"
+
+using psx::Acc5;
+using psx::SetRec;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess)                                                                 \
+            return fail(PSX_EHIP, std::string("HIP error ") + hipGetErrorString(_e) + " at " + \
+                                      __FILE__ + ":" + std::to_string(__LINE__) + ": " #expr); \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// Device problem description (union-indexed, see DESIGN.md "HBM layout")
+// ---------------------------------------------------------------------------
+struct DevProb {
+    int U, ldg;                   // union SNPs, padded leading dimension (multiple of 64)
+    const double* G[2];           // Sigma~_s in union coordinates, ldg x ldg, 0 where absent
+    const double* Ad[2];          // 1/d_s + Sigma~_s[u,u]  (1/d_s where absent / padding)
+    const double* y[2];           // y_s = B_s^T S'_s in union coordinates (0 where absent)
+    const unsigned char* pres;    // bit s set when union SNP u is in study s
+    double dval[2];               // d_s = s^2 n_s / min(n) + t^2   (postcal.cpp:89)
+    int Ck[PSX_KMAX + 1];         // integer prior shift per causal-set size
+    double pit[PSX_KMAX + 1][PSX_KMAX + 1];    // 2^{prior(k,nsh) log2e - Ck[k]}
+    double prior[PSX_KMAX + 1][PSX_KMAX + 1];  // prior(k, nsh) in nats (postcal.cpp:19-59)
+};
+
+__device__ inline double wave_sum(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ inline double wave_min(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// Setup kernels: Sigma~_s = B_s^T B_s (FP64, LDS tiled), y_s = B_s^T S'_s
+// ---------------------------------------------------------------------------
+// B column-major M x M: Sigma~[i][j] = sum_r B[i*M + r] * B[j*M + r]
+__global__ __launch_bounds__(256) void k_btb(const double* __restrict__ B, int M, double* __restrict__ out) {
+    __shared__ double ti[16][17], tj[16][17];
+    int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
+    double acc = 0.0;
+    for (int r0 = 0; r0 < M; r0 += 16) {
+        int r = r0 + tx;
+        int ci = i0 + ty, cj = j0 + ty;
+        ti[ty][tx] = (ci < M && r < M) ? B[(size_t)ci * M + r] : 0.0;
+        tj[ty][tx] = (cj < M && r < M) ? B[(size_t)cj * M + r] : 0.0;
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < 16; kk++) acc = fma(ti[ty][kk], tj[tx][kk], acc);
+        __syncthreads();
+    }
+    int i = i0 + ty, j = j0 + tx;
+    if (i < M && j < M) out[(size_t)i * M + j] = acc;
+}
+
+__global__ void k_bts(const double* __restrict__ B, const double* __restrict__ sp, int M, double* __restrict__ y) {
+    int i = blockIdx.x;
+    double acc = 0.0;
+    for (int r = threadIdx.x; r < M; r += 64) acc = fma(B[(size_t)i * M + r], sp[r], acc);
+    acc = wave_sum(acc);
+    if (threadIdx.x == 0) y[i] = acc;
+}
+
+// scatter study-local Sigma~ into union coordinates
+__global__ void k_to_union(const double* __restrict__ S, int M, const int* __restrict__ u2l, int U, int ldg,
+                           double* __restrict__ G) {
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    int u = blockIdx.y;
+    if (v >= ldg) return;
+    double val = 0.0;
+    if (u < U && v < U) {
+        int lu = u2l[u], lv = u2l[v];
+        if (lu >= 0 && lv >= 0) val = S[(size_t)lu * M + lv];
+    }
+    G[(size_t)u * ldg + v] = val;
+}
+
+// ---------------------------------------------------------------------------
+// Generic evaluator: one wave per union set (any k <= PSX_KMAX).  Lanes first
+// factor the 2^k per-study subsets (LDL^T), then stride over the 3^k study
+// assignments (x_j in {1: study0 only, 2: study1 only, 3: both}), i.e. exactly
+// the masks of postcal.cpp:907-955 that pass checkOR.  Used for SSS neighbour
+// batches, the -b configs path, levels the tiled sweep does not cover.
+// forced[set] = (C0 mask, C1 mask) restricts a set to one pattern (configs rows).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restrict__ sets, int stride,
+                                                  const int* __restrict__ forced, SetRec* __restrict__ srec,
+                                                  Acc5* __restrict__ mrec) {
+    __shared__ double s_mu[2][64];
+    __shared__ double s_f[2][64];
+    __shared__ int s_n[2][64];
+    const int set = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int* S = sets + (size_t)set * stride;
+    int mem[PSX_KMAX];
+    int k = 0;
+    for (int i = 0; i < stride && i < PSX_KMAX; i++) {
+        int v = S[i];
+        if (v >= 0) mem[k++] = v;
+    }
+    int pmask[2] = {0, 0};
+    for (int j = 0; j < k; j++) {
+        unsigned char pr = P.pres[mem[j]];
+        if (pr & 1) pmask[0] |= 1 << j;
+        if (pr & 2) pmask[1] |= 1 << j;
+    }
+    const int nsub = 1 << k;
+    if (lane < nsub) {
+        for (int s = 0; s < 2; s++) {
+            int idx[PSX_KMAX];
+            int t = 0;
+            for (int j = 0; j < k; j++)
+                if (lane & (1 << j)) idx[t++] = mem[j];
+            double q, Pd;
+            psx::ldlt_terms(P.G[s], P.ldg, P.Ad[s], P.y[s], P.dval[s], idx, t, q, Pd);
+            int n;
+            double mu;
+            psx::split_exp(0.5 * q * PSX_LOG2E, 1.0 / sqrt(Pd), n, mu);
+            s_mu[s][lane] = mu;
+            s_n[s][lane] = n;
+            s_f[s][lane] = 0.5 * q - 0.5 * log(Pd);
+        }
+    }
+    __syncthreads();
+    const int S0 = pmask[0], S1 = pmask[1];
+    const int Gll = s_n[0][S0] + s_n[1][S1] + 2;
+    int GN[PSX_KMAX];
+    for (int j = 0; j < k; j++) {
+        int bj = 1 << j;
+        int g1 = s_n[0][S0] + s_n[1][S1 & ~bj];
+        int g2 = s_n[0][S0 & ~bj] + s_n[1][S1];
+        GN[j] = psx::imax(g1, g2) + 2;
+    }
+    const int GS = Gll + P.Ck[k];
+    int npat = 1;
+    for (int j = 0; j < k; j++) npat *= 3;
+    int fc0 = -1, fc1 = -1;
+    if (forced) {
+        fc0 = forced[2 * set];
+        fc1 = forced[2 * set + 1];
+    }
+    double tot = 0, nc0 = 0, nc1 = 0, smin = 1e300, npatv = 0;
+    double p0[PSX_KMAX], p1[PSX_KMAX], sh[PSX_KMAX], sl[PSX_KMAX], ns[PSX_KMAX];
+    for (int j = 0; j < PSX_KMAX; j++) p0[j] = p1[j] = sh[j] = sl[j] = ns[j] = 0.0;
+    for (int p = lane; p < npat; p += 64) {
+        int c0 = 0, c1 = 0, x[PSX_KMAX];
+        int r = p;
+        for (int j = 0; j < k; j++) {
+            x[j] = r % 3 + 1;
+            r /= 3;
+            if (x[j] & 1) c0 |= 1 << j;
+            if (x[j] & 2) c1 |= 1 << j;
+        }
+        if ((c0 & ~S0) || (c1 & ~S1)) continue;  // (study, SNP) pair not present: no mask bit
+        if (fc0 >= 0 && (c0 != fc0 || c1 != fc1)) continue;
+        int nsh = __popc(c0 & c1);
+        double mup = s_mu[0][c0] * s_mu[1][c1];
+        int np = s_n[0][c0] + s_n[1][c1];
+        double wll = ldexp(mup, np - Gll);
+        double w = wll * P.pit[k][nsh];
+        npatv += 1.0;
+        tot += w;
+        if (c0 == 0) nc0 += w;
+        if (c1 == 0) nc1 += w;
+        smin = fmin(smin, s_f[0][c0] + s_f[1][c1] + P.prior[k][nsh]);
+        for (int j = 0; j < k; j++) {
+            if (x[j] & 1) p0[j] += w;
+            if (x[j] & 2) p1[j] += w;
+            if (x[j] == 3) {
+                sh[j] += w;
+                sl[j] += wll;
+            } else {
+                ns[j] += ldexp(mup, np - GN[j]);
+            }
+        }
+    }
+    tot = wave_sum(tot);
+    nc0 = wave_sum(nc0);
+    nc1 = wave_sum(nc1);
+    npatv = wave_sum(npatv);
+    smin = wave_min(smin);
+    for (int j = 0; j < k; j++) {
+        p0[j] = wave_sum(p0[j]);
+        p1[j] = wave_sum(p1[j]);
+        sh[j] = wave_sum(sh[j]);
+        sl[j] = wave_sum(sl[j]);
+        ns[j] = wave_sum(ns[j]);
+    }
+    if (lane == 0) {
+        SetRec r;
+        r.m = GS;
+        r.pad = 0;
+        r.tot = tot;
+        r.nc0 = nc0;
+        r.nc1 = nc1;
+        r.score = smin;
+        r.npat = npatv;
+        srec[set] = r;
+    }
+    if (lane < k && mrec) {
+        Acc5 a;
+        a.mP = GS;
+        a.mS = Gll;
+        a.mN = GN[lane];
+        a.pad = 0;
+        // dynamic index into the per-lane arrays happens once; keep it simple
+        double vp0 = 0, vp1 = 0, vsh = 0, vsl = 0, vns = 0;
+        for (int j = 0; j < k; j++)
+            if (j == lane) { vp0 = p0[j]; vp1 = p1[j]; vsh = sh[j]; vsl = sl[j]; vns = ns[j]; }
+        a.post0 = vp0;
+        a.post1 = vp1;
+        a.shared = vsh;
+        a.sll = vsl;
+        a.nsll = vns;
+        mrec[(size_t)set * stride + lane] = a;
+    }
+}
+
+// merge `count` concatenated partial images (rank order) into acc / sacc.
+// Image layout: Acc5[ldg] followed by one Acc5-sized slot holding the SetRec.
+__global__ void k_merge_partials(const Acc5* __restrict__ parts, int U, int ldg, int count, Acc5* __restrict__ acc,
+                                 SetRec* __restrict__ sacc) {
+    const size_t stride = (size_t)ldg + 1;
+    int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u < U) {
+        Acc5 a = {0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        for (int r = 0; r < count; r++) psx::fold_acc(a, parts[(size_t)r * stride + u]);
+        acc[u] = a;
+    }
+    if (u == 0) {
+        SetRec s = {0, 0, 0.0, 0.0, 0.0, 1e300, 0.0};
+        for (int r = 0; r < count; r++)
+            psx::fold_set(s, *reinterpret_cast<const SetRec*>(parts + (size_t)r * stride + ldg));
+        *sacc = s;
+    }
+}
+
+}  // namespace
+
+// ===========================================================================
+// Host engine
+// ===========================================================================
+struct psx_engine {
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    int S = 2;
+    int m[2] = {0, 0};
+    int N = 0, U = 0, ldg = 0, maxc = 0;
+    int rank = 0, world = 1;
+    std::vector<int> u2l;     // [2][U]
+    std::vector<unsigned char> pres;
+    double K = 0;             // -||S'||^2/2
+    double L0 = 0;            // null configuration L' (K excluded), postcal.cpp:797-803
+    double dval[2] = {0, 0};
+    DevProb dp;
+    // device buffers
+    double* dG[2] = {nullptr, nullptr};
+    double* dAd[2] = {nullptr, nullptr};
+    double* dy[2] = {nullptr, nullptr};
+    unsigned char* dpres = nullptr;
+    Acc5* dacc = nullptr;
+    SetRec* dsacc = nullptr;
+    // sweep workspace (tiled kernel)
+    psx::SweepPlanCache plans;
+    // generic workspace
+    int* dsets = nullptr;
+    size_t cap_sets = 0;
+    int* dforced = nullptr;
+    size_t cap_forced = 0;
+    SetRec* dsrec = nullptr;
+    size_t cap_srec = 0;
+    Acc5* dmrec = nullptr;
+    size_t cap_mrec = 0;
+    int* dcsr = nullptr;
+    size_t cap_csr = 0;
+    // timing
+    hipEvent_t ev[4];
+    psx_timing timing;
+    uint64_t n_configs = 0;
+
+    ~psx_engine();
+};
+
+psx_engine::~psx_engine() {
+    hipSetDevice(dev);
+    for (int s = 0; s < 2; s++) { hipFree(dG[s]); hipFree(dAd[s]); hipFree(dy[s]); }
+    hipFree(dpres); hipFree(dacc); hipFree(dsacc);
+    hipFree(dsets); hipFree(dforced); hipFree(dsrec); hipFree(dmrec); hipFree(dcsr);
+    psx::sweep_free(plans);
+    for (int i = 0; i < 4; i++) hipEventDestroy(ev[i]);
+    if (stream) hipStreamDestroy(stream);
+}
+
+namespace {
+
+template <typename T>
+int ensure(T*& p, size_t& cap, size_t n) {
+    if (n <= cap) return 0;
+    hipFree(p);
+    p = nullptr;
+    size_t nc = std::max(n, cap * 2);
+    HIPCHK(hipMalloc(&p, nc * sizeof(T)));
+    cap = nc;
+    return 0;
+}
+
+double logval(const psx_engine* e, int32_t m, double s) {
+    if (!(s > 0)) return 0.0;  // reference "empty" sentinel
+    return e->K + ((double)m + std::log2(s)) * PSX_LN2;
+}
+
+// prior(k, nsh) in nats exactly as postcal.cpp:19-59 accumulates it
+double prior_nats(const psx_problem* p, int U, int k, int nsh) {
+    double pc = 0;
+    if (p->sharing_param != 0) pc += nsh * std::log(p->sharing_param) + (k - nsh) * std::log((1 - p->sharing_param) * 0.5);
+    pc += k * std::log(p->gamma);
+    pc += (U - k) * std::log(1 - p->gamma);
+    return pc;
+}
+
+// Build a CSR (SNP -> record indices) for records laid out as [set][stride]
+// with member SNPs `sets`; records in set order, so folds are deterministic.
+void build_csr(const std::vector<int>& sets, int stride, size_t nsets, int U, std::vector<int>& ptr,
+               std::vector<int>& idx, std::vector<int>& rows) {
+    std::vector<int> cnt(U + 1, 0);
+    for (size_t i = 0; i < nsets * stride; i++)
+        if (sets[i] >= 0) cnt[sets[i]]++;
+    rows.clear();
+    ptr.assign(1, 0);
+    std::vector<int> start(U, -1);
+    int acc = 0;
+    for (int u = 0; u < U; u++)
+        if (cnt[u]) {
+            start[u] = acc;
+            rows.push_back(u);
+            acc += cnt[u];
+            ptr.push_back(acc);
+        }
+    idx.assign(acc, 0);
+    std::vector<int> fill(U, 0);
+    for (size_t i = 0; i < nsets * stride; i++) {
+        int u = sets[i];
+        if (u >= 0) idx[start[u] + fill[u]++] = (int)i;
+    }
+}
+
+// Evaluate a batch of union sets with the generic kernel; optionally fold all
+// patterns into the accumulators and/or return SSS scores.
+int eval_generic(psx_engine* e, const std::vector<int>& sets, int stride, size_t nsets, const int* forced,
+                 bool accumulate, double* scores, double* kernel_ms) {
+    if (nsets == 0) return 0;
+    if (stride > PSX_KMAX) return fail(PSX_ERANGE, "union set larger than PSX_KMAX");
+    int rc;
+    if ((rc = ensure(e->dsets, e->cap_sets, nsets * stride))) return rc;
+    if ((rc = ensure(e->dsrec, e->cap_srec, nsets))) return rc;
+    if ((rc = ensure(e->dmrec, e->cap_mrec, nsets * stride))) return rc;
+    HIPCHK(hipMemcpyAsync(e->dsets, sets.data(), nsets * stride * sizeof(int), hipMemcpyHostToDevice, e->stream));
+    int* dforced = nullptr;
+    if (forced) {
+        if ((rc = ensure(e->dforced, e->cap_forced, nsets * 2))) return rc;
+        HIPCHK(hipMemcpyAsync(e->dforced, forced, nsets * 2 * sizeof(int), hipMemcpyHostToDevice, e->stream));
+        dforced = e->dforced;
+    }
+    if (kernel_ms) HIPCHK(hipEventRecord(e->ev[2], e->stream));
+    hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)nsets), dim3(64), 0, e->stream, e->dp, e->dsets, stride, dforced,
+                       e->dsrec, e->dmrec);
+    HIPCHK(hipGetLastError());
+    if (kernel_ms) HIPCHK(hipEventRecord(e->ev[3], e->stream));
+    if (accumulate) {
+        std::vector<int> ptr, idx, rows;
+        build_csr(sets, stride, nsets, e->U, ptr, idx, rows);
+        size_t need = ptr.size() + idx.size() + rows.size();
+        if ((rc = ensure(e->dcsr, e->cap_csr, need))) return rc;
+        std::vector<int> packed;
+        packed.reserve(need);
+        packed.insert(packed.end(), ptr.begin(), ptr.end());
+        packed.insert(packed.end(), idx.begin(), idx.end());
+        packed.insert(packed.end(), rows.begin(), rows.end());
+        HIPCHK(hipMemcpyAsync(e->dcsr, packed.data(), need * sizeof(int), hipMemcpyHostToDevice, e->stream));
+        if (psx::launch_merge_members(e->dmrec, e->dcsr, e->dcsr + ptr.size(), e->dcsr + ptr.size() + idx.size(),
+                                      (int)rows.size(), e->dacc, e->stream))
+            return fail(PSX_EHIP, psx::sweep_error());
+        SetRec none = {0, 0, 0.0, 0.0, 0.0, 1e300, 0.0};
+        if (psx::launch_merge_sets(e->dsrec, (long)nsets, none, e->dsacc, e->stream))
+            return fail(PSX_EHIP, psx::sweep_error());
+    }
+    if (scores) {
+        std::vector<SetRec> sr(nsets);
+        HIPCHK(hipMemcpyAsync(sr.data(), e->dsrec, nsets * sizeof(SetRec), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        for (size_t i = 0; i < nsets; i++) scores[i] = e->K + sr[i].score;
+    }
+    if (kernel_ms) {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+        *kernel_ms += ms;
+    }
+    return 0;
+}
+
+// fold `count` null configurations (postcal.cpp:793-822) into the scalars
+int fold_null(psx_engine* e, double count) {
+    if (count <= 0) return 0;
+    double h = e->L0 * PSX_LOG2E;
+    double fl = std::floor(h);
+    SetRec x = {(int32_t)fl, 0, 0.0, 0.0, 0.0, e->L0, count};
+    double v = std::exp2(h - fl) * count;
+    x.tot = x.nc0 = x.nc1 = v;
+    if (psx::launch_merge_sets(nullptr, 0L, x, e->dsacc, e->stream)) return fail(PSX_EHIP, psx::sweep_error());
+    return 0;
+}
+
+// lexicographic k-subset enumeration over [0, U)
+long double choose_ld(int n, int k) {
+    if (k < 0 || k > n) return 0;
+    long double r = 1;
+    for (int i = 1; i <= k; i++) r = r * (n - k + i) / i;
+    return r;
+}
+uint64_t choose_u64(int n, int k) {
+    if (k < 0 || k > n) return 0;
+    unsigned __int128 r = 1;
+    for (int i = 1; i <= k; i++) r = r * (unsigned)(n - k + i) / (unsigned)i;
+    return (uint64_t)r;
+}
+void unrank_lex(uint64_t r, int U, int k, int* out) {
+    int x = 0;
+    for (int i = 0; i < k; i++) {
+        for (;;) {
+            uint64_t c = choose_u64(U - x - 1, k - i - 1);
+            if (r < c) break;
+            r -= c;
+            x++;
+        }
+        out[i] = x++;
+    }
+}
+bool next_lex(int* c, int U, int k) {
+    int i = k - 1;
+    while (i >= 0 && c[i] == U - k + i) i--;
+    if (i < 0) return false;
+    c[i]++;
+    for (int j = i + 1; j < k; j++) c[j] = c[j - 1] + 1;
+    return true;
+}
+
+// exhaustive level k through the generic evaluator, shard-restricted
+int run_level_generic(psx_engine* e, int k, double* kms) {
+    uint64_t total = choose_u64(e->U, k);
+    uint64_t lo = total * (uint64_t)e->rank / e->world;
+    uint64_t hi = total * (uint64_t)(e->rank + 1) / e->world;
+    if (lo >= hi) return 0;
+    const uint64_t CH = 1u << 20;
+    std::vector<int> c(k);
+    unrank_lex(lo, e->U, k, c.data());
+    uint64_t r = lo;
+    std::vector<int> sets;
+    while (r < hi) {
+        uint64_t n = std::min<uint64_t>(CH, hi - r);
+        sets.resize(n * k);
+        for (uint64_t i = 0; i < n; i++) {
+            std::copy(c.begin(), c.end(), sets.begin() + i * k);
+            next_lex(c.data(), e->U, k);
+        }
+        int rc = eval_generic(e, sets, k, n, nullptr, true, nullptr, kms);
+        if (rc) return rc;
+        r += n;
+    }
+    return 0;
+}
+
+int reset_acc(psx_engine* e) {
+    HIPCHK(hipMemsetAsync(e->dacc, 0, sizeof(Acc5) * e->ldg, e->stream));
+    SetRec z = {0, 0, 0.0, 0.0, 0.0, 1e300, 0.0};
+    HIPCHK(hipMemcpyAsync(e->dsacc, &z, sizeof(SetRec), hipMemcpyHostToDevice, e->stream));
+    return 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int32_t psx_abi_version(void) { return PSX_ABI_VERSION; }
+const char* psx_last_error(void) { return g_err.c_str(); }
+
+int psx_device_count(int* count) {
+    int c = 0;
+    hipError_t err = hipGetDeviceCount(&c);
+    if (err != hipSuccess) c = 0;
+    *count = c;
+    return 0;
+}
+
+uint64_t psx_count_configs(const psx_problem* p) {
+    // e_k of weights w_u = 2^{b_u} - 1 (postcal.cpp:903 masks minus checkOR failures = prod (2^b - 1))
+    int U = p->n_union, c = p->max_causal;
+    std::vector<long double> e(c + 1, 0.0L);
+    e[0] = 1;
+    for (int u = 0; u < U; u++) {
+        int b = 0;
+        for (int s = 0; s < p->n_studies; s++) b += p->union_to_local[s * U + u] >= 0;
+        long double w = (long double)((1 << b) - 1);
+        for (int k = c; k >= 1; k--) e[k] += e[k - 1] * w;
+    }
+    long double t = 0;
+    for (int k = 0; k <= c; k++) t += e[k];
+    return (uint64_t)(t + 0.5L);
+}
+
+int psx_create(const psx_problem* p, int device, psx_engine** out) {
+    *out = nullptr;
+    if (!p || p->n_studies != 2) return fail(PSX_EINVAL, "only two studies are supported (postcal.cpp:20-23)");
+    if (p->max_causal < 0 || p->max_causal > PSX_KMAX) return fail(PSX_ERANGE, "max_causal outside [0, 6]");
+    if (p->n_union <= 0 || p->m[0] <= 0 || p->m[1] <= 0) return fail(PSX_EINVAL, "empty problem");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(PSX_ENODEV, "no HIP device: the engine has no CPU fallback");
+    if (device < 0 || device >= ndev) return fail(PSX_EINVAL, "device index out of range");
+    HIPCHK(hipSetDevice(device));
+    psx_engine* e = new psx_engine();
+    e->dev = device;
+    auto bail = [&](int rc) { delete e; return rc; };
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(fail(PSX_EHIP, "stream"));
+    for (int i = 0; i < 4; i++)
+        if (hipEventCreate(&e->ev[i]) != hipSuccess) return bail(fail(PSX_EHIP, "event"));
+    e->m[0] = p->m[0];
+    e->m[1] = p->m[1];
+    e->N = p->m[0] + p->m[1];
+    e->U = p->n_union;
+    e->ldg = (e->U + 63) / 64 * 64;
+    e->maxc = p->max_causal;
+    e->u2l.assign(p->union_to_local, p->union_to_local + 2 * e->U);
+    e->pres.assign(e->ldg, 0);
+    for (int s = 0; s < 2; s++) {
+        int cnt = 0;
+        for (int u = 0; u < e->U; u++) {
+            int l = e->u2l[s * e->U + u];
+            if (l >= p->m[s]) return bail(fail(PSX_EINVAL, "snp map index outside the study"));
+            if (l >= 0) { e->pres[u] |= (unsigned char)(1 << s); cnt++; }
+        }
+        if (cnt != p->m[s]) return bail(fail(PSX_EINVAL, "Invariant does not hold (model.h:140-143)"));
+    }
+    // d_s (postcal.cpp:66,89): s^2 * (n_s / min n) + t^2 with integer sample sizes
+    int mn = std::min(p->sample_sizes[0], p->sample_sizes[1]);
+    for (int s = 0; s < 2; s++) e->dval[s] = p->s_squared * (double(p->sample_sizes[s]) / mn) + p->t_squared;
+    double spsq = 0;
+    for (int i = 0; i < e->N; i++) spsq += p->s_prime[i] * p->s_prime[i];
+    e->K = -spsq / 2;
+    // null configuration (postcal.cpp:799-803): -res/2 - sqrt(|1|) + U log(1-gamma); K factored out
+    e->L0 = -std::sqrt(std::fabs(1.0)) + e->U * std::log(1 - p->gamma);
+
+    // prior tables
+    DevProb& dp = e->dp;
+    std::memset(&dp, 0, sizeof(dp));
+    dp.U = e->U;
+    dp.ldg = e->ldg;
+    dp.dval[0] = e->dval[0];
+    dp.dval[1] = e->dval[1];
+    for (int k = 0; k <= PSX_KMAX; k++) {
+        double mx = -INFINITY;
+        for (int n = 0; n <= k; n++) {
+            double pr = prior_nats(p, e->U, k, n);
+            dp.prior[k][n] = pr;
+            if (std::isfinite(pr)) mx = std::max(mx, pr * PSX_LOG2E);
+        }
+        dp.Ck[k] = std::isfinite(mx) ? (int)std::ceil(mx) : 0;
+        for (int n = 0; n <= k; n++) {
+            double v = dp.prior[k][n] * PSX_LOG2E - dp.Ck[k];
+            dp.pit[k][n] = std::isfinite(v) ? std::exp2(v) : 0.0;
+        }
+    }
+
+    // device data: Sigma~ = B^T B, y = B^T S' per study, in union coordinates
+    size_t gsz = (size_t)e->ldg * e->ldg;
+    double *dB = nullptr, *dS = nullptr, *dsp = nullptr, *dyl = nullptr;
+    int* du2l = nullptr;
+    int Mx = std::max(p->m[0], p->m[1]);
+    if (hipMalloc(&dB, (size_t)Mx * Mx * sizeof(double)) != hipSuccess ||
+        hipMalloc(&dS, (size_t)Mx * Mx * sizeof(double)) != hipSuccess ||
+        hipMalloc(&dsp, (size_t)Mx * sizeof(double)) != hipSuccess ||
+        hipMalloc(&dyl, (size_t)Mx * sizeof(double)) != hipSuccess ||
+        hipMalloc(&du2l, (size_t)e->U * sizeof(int)) != hipSuccess)
+        return bail(fail(PSX_EHIP, "out of device memory (setup)"));
+    auto cleanup = [&]() { hipFree(dB); hipFree(dS); hipFree(dsp); hipFree(dyl); hipFree(du2l); };
+    size_t boff = 0;
+    int soff = 0;
+    std::vector<double> ad(e->ldg), yu(e->ldg);
+    for (int s = 0; s < 2; s++) {
+        int M = p->m[s];
+        if (hipMalloc(&e->dG[s], gsz * sizeof(double)) != hipSuccess ||
+            hipMalloc(&e->dAd[s], e->ldg * sizeof(double)) != hipSuccess ||
+            hipMalloc(&e->dy[s], e->ldg * sizeof(double)) != hipSuccess) {
+            cleanup();
+            return bail(fail(PSX_EHIP, "out of device memory"));
+        }
+        hipMemcpyAsync(dB, p->B + boff, (size_t)M * M * sizeof(double), hipMemcpyHostToDevice, e->stream);
+        hipMemcpyAsync(dsp, p->s_prime + soff, (size_t)M * sizeof(double), hipMemcpyHostToDevice, e->stream);
+        hipMemcpyAsync(du2l, p->union_to_local + s * e->U, e->U * sizeof(int), hipMemcpyHostToDevice, e->stream);
+        dim3 g((M + 15) / 16, (M + 15) / 16);
+        hipLaunchKernelGGL(k_btb, g, dim3(256), 0, e->stream, dB, M, dS);
+        hipLaunchKernelGGL(k_bts, dim3(M), dim3(64), 0, e->stream, dB, dsp, M, dyl);
+        hipLaunchKernelGGL(k_to_union, dim3((e->ldg + 255) / 256, e->ldg), dim3(256), 0, e->stream, dS, M, du2l,
+                           e->U, e->ldg, e->dG[s]);
+        if (hipGetLastError() != hipSuccess) { cleanup(); return bail(fail(PSX_EHIP, "setup kernel launch")); }
+        std::vector<double> Sd((size_t)M), yl(M);
+        // diagonal of Sigma~ and y (small D2H copies)
+        for (int i = 0; i < M; i++)
+            hipMemcpyAsync(&Sd[i], dS + (size_t)i * M + i, sizeof(double), hipMemcpyDeviceToHost, e->stream);
+        hipMemcpyAsync(yl.data(), dyl, M * sizeof(double), hipMemcpyDeviceToHost, e->stream);
+        if (hipStreamSynchronize(e->stream) != hipSuccess) { cleanup(); return bail(fail(PSX_EHIP, "setup sync")); }
+        for (int u = 0; u < e->ldg; u++) {
+            int l = (u < e->U) ? e->u2l[s * e->U + u] : -1;
+            ad[u] = 1.0 / e->dval[s] + (l >= 0 ? Sd[l] : 0.0);
+            yu[u] = (l >= 0) ? yl[l] : 0.0;
+        }
+        hipMemcpyAsync(e->dAd[s], ad.data(), e->ldg * sizeof(double), hipMemcpyHostToDevice, e->stream);
+        hipMemcpyAsync(e->dy[s], yu.data(), e->ldg * sizeof(double), hipMemcpyHostToDevice, e->stream);
+        if (hipStreamSynchronize(e->stream) != hipSuccess) { cleanup(); return bail(fail(PSX_EHIP, "setup copy")); }
+        boff += (size_t)M * M;
+        soff += M;
+    }
+    cleanup();
+    if (hipMalloc(&e->dpres, e->ldg) != hipSuccess || hipMalloc(&e->dacc, sizeof(Acc5) * e->ldg) != hipSuccess ||
+        hipMalloc(&e->dsacc, sizeof(SetRec)) != hipSuccess)
+        return bail(fail(PSX_EHIP, "out of device memory"));
+    hipMemcpyAsync(e->dpres, e->pres.data(), e->ldg, hipMemcpyHostToDevice, e->stream);
+    for (int s = 0; s < 2; s++) {
+        dp.G[s] = e->dG[s];
+        dp.Ad[s] = e->dAd[s];
+        dp.y[s] = e->dy[s];
+    }
+    dp.pres = e->dpres;
+    if (reset_acc(e)) return bail(PSX_EHIP);
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(fail(PSX_EHIP, "create sync"));
+    std::memset(&e->timing, 0, sizeof(e->timing));
+    *out = e;
+    return 0;
+}
+
+void psx_destroy(psx_engine* e) { delete e; }
+
+int psx_set_shard(psx_engine* e, int rank, int world) {
+    if (!e || world < 1 || rank < 0 || rank >= world) return fail(PSX_EINVAL, "bad shard");
+    e->rank = rank;
+    e->world = world;
+    return 0;
+}
+
+int psx_reset(psx_engine* e) {
+    HIPCHK(hipSetDevice(e->dev));
+    int rc = reset_acc(e);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int psx_run_exhaustive(psx_engine* e) {
+    HIPCHK(hipSetDevice(e->dev));
+    int rc;
+    if ((rc = reset_acc(e))) return rc;
+    std::memset(&e->timing, 0, sizeof(e->timing));
+    HIPCHK(hipEventRecord(e->ev[0], e->stream));
+    if (e->rank == 0 && (rc = fold_null(e, 1.0))) return rc;
+    double kms = 0;
+    psx::SweepStats st;
+    std::memset(&st, 0, sizeof(st));
+    int top_tiled = 0;
+    for (int k = 1; k <= e->maxc; k++) {
+        if (psx::sweep_supports(k, e->U)) {
+            psx::SweepArgs sa{e->dG[0], e->dG[1], e->dAd[0], e->dAd[1], e->dy[0], e->dy[1], e->dpres,
+                              e->dval[0], e->dval[1], e->dp.Ck, &e->dp.pit[0][0], PSX_KMAX + 1};
+            rc = psx::sweep_level(e->plans, k, e->U, e->ldg, e->rank, e->world, e->stream, sa, e->dacc, e->dsacc, &st);
+            if (rc) return fail(PSX_EHIP, std::string("sweep level ") + std::to_string(k) + ": " + psx::sweep_error());
+            top_tiled = k;
+        } else {
+            if ((rc = run_level_generic(e, k, &kms))) return rc;
+        }
+    }
+    HIPCHK(hipEventRecord(e->ev[1], e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
+    e->timing.sweep_ms = ms;
+    if (top_tiled) {
+        e->timing.kernel_ms = st.kernel_ms[top_tiled];
+        e->timing.kernel_launches = st.launches[top_tiled];
+        e->timing.union_sets = st.union_sets[top_tiled];
+        e->timing.alg_bytes = st.alg_bytes[top_tiled];
+        e->timing.flops = st.flops[top_tiled];
+    } else {
+        e->timing.kernel_ms = kms;
+    }
+    e->timing.merge_ms = st.merge_ms;
+    SetRec s;
+    HIPCHK(hipMemcpy(&s, e->dsacc, sizeof(SetRec), hipMemcpyDeviceToHost));
+    e->timing.configs = (uint64_t)(s.npat + 0.5);
+    return 0;
+}
+
+int psx_eval_union_batch(psx_engine* e, const int32_t* sets, int32_t stride, int32_t n_sets, int accumulate,
+                         double* score_out) {
+    HIPCHK(hipSetDevice(e->dev));
+    if (stride < 1 || stride > PSX_KMAX) return fail(PSX_ERANGE, "stride outside [1, 6]");
+    // the empty set is the null configuration (sss_postcal.cpp:463-499): host side
+    std::vector<int> v;
+    std::vector<size_t> where;
+    v.reserve((size_t)n_sets * stride);
+    double nulls = 0;
+    for (int i = 0; i < n_sets; i++) {
+        const int* s = sets + (size_t)i * stride;
+        int prev = -1, k = 0;
+        for (int j = 0; j < stride; j++) {
+            if (s[j] < 0) continue;
+            if (s[j] <= prev || s[j] >= e->U) return fail(PSX_EINVAL, "sets must be ascending union indices");
+            prev = s[j];
+            k++;
+        }
+        if (k == 0) {
+            nulls += 1;
+            if (score_out) score_out[i] = e->K + e->L0;
+            continue;
+        }
+        where.push_back(i);
+        v.insert(v.end(), s, s + stride);
+    }
+    std::vector<double> sc(where.size());
+    int rc = eval_generic(e, v, stride, where.size(), nullptr, accumulate != 0, score_out ? sc.data() : nullptr, nullptr);
+    if (rc) return rc;
+    if (score_out)
+        for (size_t i = 0; i < where.size(); i++) score_out[where[i]] = sc[i];
+    if (accumulate && nulls > 0 && (rc = fold_null(e, nulls))) return rc;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int psx_run_configs(psx_engine* e, const int16_t* rows, int64_t n_rows, int32_t n_groups) {
+    HIPCHK(hipSetDevice(e->dev));
+    int rc;
+    if ((rc = reset_acc(e))) return rc;
+    std::memset(&e->timing, 0, sizeof(e->timing));
+    const int stride = PSX_KMAX;
+    std::vector<int> sets;
+    std::vector<int> forced;
+    double nulls = 0;
+    int off1 = e->m[0];
+    // idx_to_union_pos_map (model.h:134-139)
+    std::vector<int> l2u[2];
+    for (int s = 0; s < 2; s++)
+        for (int u = 0; u < e->U; u++)
+            if (e->u2l[s * e->U + u] >= 0) l2u[s].push_back(u);
+    HIPCHK(hipEventRecord(e->ev[0], e->stream));
+    for (int64_t r = 0; r < n_rows; r++) {
+        const int16_t* in = rows + r * n_groups;
+        std::vector<int> locs;
+        int numc = 0;
+        for (int i = 0; i < n_groups; i++) {
+            int g = in[i];
+            if (g < 0) continue;
+            if (g >= e->N) return fail(PSX_EINVAL, "configs row index outside the SNP range");
+            numc++;
+            int st = g >= off1 ? 1 : 0;  // postcal.cpp:500-504
+            locs.push_back(l2u[st][g - (st ? off1 : 0)]);
+        }
+        if (numc == 0) { nulls += 1; continue; }  // postcal.cpp:459-488
+        std::sort(locs.begin(), locs.end());
+        locs.erase(std::unique(locs.begin(), locs.end()), locs.end());
+        int k = (int)locs.size();
+        if (k > PSX_KMAX) return fail(PSX_ERANGE, "configs row has more than 6 union SNPs");
+        // postcal.cpp:546-590: walk the row in (study, union position) order
+        int b[2] = {0, 0};
+        int aux = 0;
+        while (aux < n_groups && in[aux] < 0) aux++;
+        int cum = 0;
+        for (int i = 0; i < 2; i++) {
+            cum += e->m[i];
+            int offi = i ? off1 : 0;
+            for (int j = 0; j < k; j++) {
+                int loc = e->u2l[i * e->U + locs[j]];
+                if (loc >= 0) {
+                    int gidx = offi + loc;
+                    if (gidx >= cum) break;
+                    if (aux < n_groups && in[aux] == gidx) {
+                        aux++;
+                        b[i] |= 1 << j;
+                        while (aux < n_groups && in[aux] < 0) aux++;
+                    }
+                }
+            }
+            if (aux == n_groups) break;
+        }
+        if (aux != n_groups) return fail(PSX_EORDER, "This did not work as expected (postcal.cpp:587-590)");
+        for (int j = 0; j < stride; j++) sets.push_back(j < k ? locs[j] : -1);
+        forced.push_back(b[0]);
+        forced.push_back(b[1]);
+    }
+    size_t ns = forced.size() / 2;
+    double kms = 0;
+    if ((rc = eval_generic(e, sets, stride, ns, forced.data(), true, nullptr, &kms))) return rc;
+    if ((rc = fold_null(e, nulls))) return rc;
+    HIPCHK(hipEventRecord(e->ev[1], e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
+    e->timing.sweep_ms = ms;
+    e->timing.kernel_ms = kms;
+    e->timing.kernel_launches = 1;
+    e->timing.configs = (uint64_t)n_rows;
+    return 0;
+}
+
+// sss_postcal.cpp:102-380.  The random walk, neighbourhoods, hash map and
+// sampling run on the host exactly as the reference orders them; every
+// iteration's unseen neighbours are one GPU batch.
+namespace {
+struct VecHash {  // postcal.h:43-56
+    size_t operator()(const std::vector<int>& v) const noexcept {
+        size_t seed = 0xCBF29CE484222325ULL;
+        for (int x : v) seed ^= (size_t)x + 0x9e3779b97f4a7c15ULL + (seed << 6) + (seed >> 2);
+        return seed;
+    }
+};
+}  // namespace
+
+int psx_run_sss(psx_engine* e, int32_t* iterations_out) {
+    HIPCHK(hipSetDevice(e->dev));
+    int rc;
+    if ((rc = reset_acc(e))) return rc;
+    std::memset(&e->timing, 0, sizeof(e->timing));
+    const int U = e->U, C = e->maxc;
+    if (C > PSX_KMAX) return fail(PSX_ERANGE, "SSS max_causal > 6");
+    std::unordered_map<std::vector<int>, double, VecHash> hm;
+    std::mt19937 gen(12345);
+    std::vector<int> cur;
+    double old_sum = 0;
+    int iter;
+    const int stride = std::max(C, 1);
+    double kms = 0;
+    auto t0 = std::chrono::steady_clock::now();
+    auto sss_total = [&](double& out) -> int {
+        SetRec s;
+        HIPCHK(hipMemcpy(&s, e->dsacc, sizeof(SetRec), hipMemcpyDeviceToHost));
+        out = logval(e, s.m, s.tot);
+        return 0;
+    };
+    std::vector<char> in_cur(U, 0);
+    for (iter = 0; iter < 1000; iter++) {
+        // sss_postcal.cpp:166-186 nbd = zero ++ minus ++ plus
+        std::vector<std::vector<int>> nbd;
+        int k = (int)cur.size();
+        std::fill(in_cur.begin(), in_cur.end(), 0);
+        for (int v : cur) in_cur[v] = 1;
+        std::vector<std::vector<int>> minus;
+        for (int i = 0; i < k; i++) {
+            std::vector<int> nc;
+            for (int j = 0; j < k; j++) if (i != j) nc.push_back(cur[j]);
+            minus.push_back(nc);
+        }
+        for (int i = 0; i < U; i++)
+            if (!in_cur[i])
+                for (const auto& v : minus) {
+                    std::vector<int> nc;
+                    nc.reserve(k);
+                    nc.push_back(i);
+                    nc.insert(nc.end(), v.begin(), v.end());
+                    std::sort(nc.begin(), nc.end());
+                    nbd.push_back(std::move(nc));
+                }
+        int num_zero = (int)nbd.size();
+        for (auto& v : minus) nbd.push_back(v);
+        int num_minus = k;
+        if (k < C)
+            for (int i = 0; i < U; i++)
+                if (!in_cur[i]) {
+                    std::vector<int> nc{i};
+                    nc.insert(nc.end(), cur.begin(), cur.end());
+                    std::sort(nc.begin(), nc.end());
+                    nbd.push_back(std::move(nc));
+                }
+        int num_plus = (int)nbd.size() - num_zero - num_minus;
+        // current configuration (sss_postcal.cpp:195-202): updates only if unseen
+        std::vector<std::vector<int>> batch;
+        std::vector<int> batch_pos;  // -1 == cur
+        if (hm.find(cur) == hm.end()) { batch.push_back(cur); batch_pos.push_back(-1); }
+        std::vector<double> lk(nbd.size(), 0.0);
+        std::vector<int> not_done;
+        for (size_t i = 0; i < nbd.size(); i++) {
+            auto it = hm.find(nbd[i]);
+            if (it != hm.end()) lk[i] = it->second;
+            else { not_done.push_back((int)i); batch.push_back(nbd[i]); batch_pos.push_back((int)i); }
+        }
+        // evaluate the batch on the GPU (null sets folded host side)
+        std::vector<int> flat;
+        flat.reserve(batch.size() * stride);
+        for (auto& v : batch) for (int j = 0; j < stride; j++) flat.push_back(j < (int)v.size() ? v[j] : -1);
+        std::vector<double> sc(batch.size());
+        {
+            std::vector<int> vv;
+            std::vector<size_t> wh;
+            double nulls = 0;
+            for (size_t i = 0; i < batch.size(); i++) {
+                if (batch[i].empty()) { nulls += 1; sc[i] = e->K + e->L0; continue; }
+                wh.push_back(i);
+                vv.insert(vv.end(), flat.begin() + i * stride, flat.begin() + (i + 1) * stride);
+            }
+            std::vector<double> s2(wh.size());
+            if ((rc = eval_generic(e, vv, stride, wh.size(), nullptr, true, s2.data(), &kms))) return rc;
+            for (size_t i = 0; i < wh.size(); i++) sc[wh[i]] = s2[i];
+            if (nulls > 0 && (rc = fold_null(e, nulls))) return rc;
+        }
+        for (size_t i = 0; i < batch.size(); i++)
+            if (batch_pos[i] >= 0) lk[batch_pos[i]] = sc[i];
+        double sss_sum;
+        if ((rc = sss_total(sss_sum))) return rc;
+        if (not_done.empty()) break;                                                       // :260-263
+        if (iter >= 100 && (1 - std::exp(old_sum - sss_sum)) <= 0.001) break;             // :265-270
+        for (int i : not_done) hm[nbd[i]] = lk[i];                                         // :280-284
+        double wz = 0, wm = 0, wp = 0;
+        size_t zs = nbd.size(), ms = nbd.size(), ps = nbd.size();
+        auto group = [&](int b, int en, double& wsum, size_t& smp) {
+            std::vector<double> pr;
+            double mx = *std::max_element(lk.begin() + b, lk.begin() + en);
+            for (int ii = b; ii < en; ii++) pr.push_back(std::exp(lk[ii] - mx));
+            std::discrete_distribution<size_t> dist(pr.begin(), pr.end());
+            smp = dist(gen);
+            wsum = std::accumulate(pr.begin(), pr.end(), 0.0);
+        };
+        if (num_zero != 0) group(0, num_zero, wz, zs);                                     // :296-306
+        if (num_minus != 0) group(num_zero, num_zero + num_minus, wm, ms);                 // :307-317
+        if (num_plus != 0) group(num_zero + num_minus, (int)lk.size(), wp, ps);            // :318-328
+        std::discrete_distribution<size_t> dist({wz, wm, wp});                             // :330-343
+        size_t idx = dist(gen), fin = 0;
+        switch (idx) {
+            case 0: fin = zs; break;
+            case 1: fin = ms + num_zero; break;
+            case 2: fin = ps + num_zero + num_minus; break;
+        }
+        cur = nbd[fin];
+        old_sum = sss_sum;
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    if (iterations_out) *iterations_out = iter;
+    e->timing.sweep_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    e->timing.kernel_ms = kms;
+    SetRec s;
+    HIPCHK(hipMemcpy(&s, e->dsacc, sizeof(SetRec), hipMemcpyDeviceToHost));
+    e->timing.configs = (uint64_t)(s.npat + 0.5);
+    return 0;
+}
+
+int psx_get_accum(psx_engine* e, psx_accum* out) {
+    HIPCHK(hipSetDevice(e->dev));
+    std::vector<Acc5> a(e->U);
+    SetRec s;
+    HIPCHK(hipMemcpyAsync(a.data(), e->dacc, sizeof(Acc5) * e->U, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&s, e->dsacc, sizeof(SetRec), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    for (int u = 0; u < e->U; u++) {
+        for (int st = 0; st < 2; st++) {
+            int l = e->u2l[st * e->U + u];
+            if (l < 0) continue;
+            double v = st == 0 ? logval(e, a[u].mP, a[u].post0) : logval(e, a[u].mP, a[u].post1);
+            if (out->post) out->post[(st ? e->m[0] : 0) + l] = v;
+        }
+        if (out->shared) out->shared[u] = logval(e, a[u].mP, a[u].shared);
+        if (out->shared_ll) out->shared_ll[u] = logval(e, a[u].mS, a[u].sll);
+        if (out->notshared_ll) out->notshared_ll[u] = logval(e, a[u].mN, a[u].nsll);
+    }
+    if (out->no_causal) {
+        out->no_causal[0] = logval(e, s.m, s.nc0);
+        out->no_causal[1] = logval(e, s.m, s.nc1);
+    }
+    out->total = logval(e, s.m, s.tot);
+    out->n_configs = (uint64_t)(s.npat + 0.5);
+    return 0;
+}
+
+int64_t psx_partials_bytes(psx_engine* e) { return (int64_t)(sizeof(Acc5) * ((size_t)e->ldg + 1)); }
+
+int psx_export_partials(psx_engine* e, void* dst) {
+    HIPCHK(hipSetDevice(e->dev));
+    char* d = (char*)dst;
+    HIPCHK(hipMemcpyAsync(d, e->dacc, sizeof(Acc5) * e->ldg, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(d + sizeof(Acc5) * e->ldg, e->dsacc, sizeof(SetRec), hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int psx_merge_partials(psx_engine* e, const void* src, int32_t count) {
+    HIPCHK(hipSetDevice(e->dev));
+    if (count < 1) return fail(PSX_EINVAL, "count < 1");
+    hipLaunchKernelGGL(k_merge_partials, dim3((e->U + 255) / 256), dim3(256), 0, e->stream, (const Acc5*)src, e->U,
+                       e->ldg, count, e->dacc, e->dsacc);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int psx_get_timing(psx_engine* e, psx_timing* t) {
+    *t = e->timing;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+// psx_sweep.h — tiled exhaustive sweep over union subsets of size k in {2, 3}
+// (the dominant levels of PostCal::computeTotalLikelihood, postcal.cpp:716-1092).
+#ifndef PSX_SWEEP_H
+#define PSX_SWEEP_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <map>
+#include <tuple>
+#include <vector>
+
+#include "psx_math.h"
+
+namespace psx {
+
+struct SweepArgs {
+    const double* G0;
+    const double* G1;
+    const double* Ad0;
+    const double* Ad1;
+    const double* y0;
+    const double* y1;
+    const unsigned char* pres;
+    double d0, d1;
+    const int* Ck;      // host array [PSX_KMAX+1]
+    const double* pit;  // host array [PSX_KMAX+1][pit_ld]
+    int pit_ld;
+};
+
+struct SweepStats {           // indexed by causal-set level k
+    double kernel_ms[8];      // device time of the sweep kernel
+    int launches[8];
+    uint64_t union_sets[8];   // union subsets covered
+    double alg_bytes[8];      // 8 * sum_s (|C_s|^2 + |C_s|) over configurations
+    double flops[8];          // FP64 operation estimate
+    double merge_ms;          // device time of the record merges (all levels)
+};
+
+// One decomposition of a level into wave units, with its record CSR.
+struct SweepPlan {
+    int k = 0, U = 0, ldg = 0, rank = 0, world = 1, ca = 0;
+    int n_units = 0, rec_stride = 0, n_rows = 0;
+    uint64_t union_sets = 0;
+    double alg_bytes = 0, flops = 0;
+    int4* d_units = nullptr;     // {a0, a1, B, T}
+    Acc5* d_rec = nullptr;       // [n_units][rec_stride]
+    SetRec* d_srec = nullptr;    // [n_units]
+    int* d_csr = nullptr;        // ptr[n_rows+1], idx[...], row_snp[n_rows]
+    int csr_ptr_len = 0, csr_idx_len = 0;
+};
+
+struct SweepPlanCache {
+    std::map<std::tuple<int, int, int, int>, SweepPlan> plans;  // (k, U, rank, world)
+    double* d_skew[2] = {nullptr, nullptr};  // skewed Sigma~ tiles (B <= T)
+    int skew_ldg = 0;
+    const double* skew_src[2] = {nullptr, nullptr};
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+
+bool sweep_supports(int k, int U);
+int sweep_level(SweepPlanCache& cache, int k, int U, int ldg, int rank, int world, hipStream_t stream,
+                const SweepArgs& a, Acc5* acc, SetRec* sacc, SweepStats* st);
+void sweep_free(SweepPlanCache& cache);
+int launch_merge_members(const Acc5* rec, const int* ptr, const int* idx, const int* rows, int n_rows, Acc5* acc,
+                         hipStream_t st);
+int launch_merge_sets(const SetRec* rec, long n, const SetRec& extra, SetRec* acc, hipStream_t st);
+const char* sweep_error();
+
+}  // namespace psx
+#endif

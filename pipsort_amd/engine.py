@@ -1,0 +1,339 @@
+"""ctypes binding of the MI355X PostCal engine (include/pipsort_engine.h).
+
+`PostCal` mirrors the reference class's seam (postcal.h:118 constructor inputs,
+postcal.cpp:1128 run, postcal.h:62-78 accumulators) so parity tests read like
+the reference's own usage.  There is no CPU fallback: constructing a PostCal
+without a HIP device raises EngineError (PSX_ENODEV).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libpipsort_engine.so")
+PIPSORT_BIN = os.path.join(_HERE, "bin", "PIPSORT")
+
+PSX_OK = 0
+PSX_EINVAL = -1
+PSX_ENODEV = -2
+PSX_EHIP = -3
+PSX_ESINGULAR = -4
+PSX_EORDER = -5
+PSX_ERANGE = -6
+
+# Every symbol declared in include/pipsort_engine.h and include/pipsort_model.h
+EXPORTED = [
+    "psx_abi_version", "psx_last_error", "psx_device_count", "psx_create", "psx_destroy",
+    "psx_set_shard", "psx_run_exhaustive", "psx_run_configs", "psx_run_sss",
+    "psx_eval_union_batch", "psx_reset", "psx_get_accum", "psx_partials_bytes",
+    "psx_export_partials", "psx_merge_partials", "psx_get_timing", "psx_count_configs",
+    "psx_psd_shift", "psx_lowrank_study", "psx_sym_eigen",
+]
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"psx error {code}: {msg}")
+        self.code = code
+
+
+class _Problem(ctypes.Structure):
+    _fields_ = [
+        ("n_studies", ctypes.c_int32),
+        ("m", ctypes.POINTER(ctypes.c_int32)),
+        ("B", ctypes.POINTER(ctypes.c_double)),
+        ("s_prime", ctypes.POINTER(ctypes.c_double)),
+        ("n_union", ctypes.c_int32),
+        ("union_to_local", ctypes.POINTER(ctypes.c_int32)),
+        ("max_causal", ctypes.c_int32),
+        ("sample_sizes", ctypes.POINTER(ctypes.c_int32)),
+        ("sharing_param", ctypes.c_double),
+        ("gamma", ctypes.c_double),
+        ("t_squared", ctypes.c_double),
+        ("s_squared", ctypes.c_double),
+    ]
+
+
+class _Accum(ctypes.Structure):
+    _fields_ = [
+        ("post", ctypes.POINTER(ctypes.c_double)),
+        ("no_causal", ctypes.POINTER(ctypes.c_double)),
+        ("shared", ctypes.POINTER(ctypes.c_double)),
+        ("shared_ll", ctypes.POINTER(ctypes.c_double)),
+        ("notshared_ll", ctypes.POINTER(ctypes.c_double)),
+        ("total", ctypes.c_double),
+        ("n_configs", ctypes.c_uint64),
+    ]
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [
+        ("sweep_ms", ctypes.c_double),
+        ("kernel_ms", ctypes.c_double),
+        ("kernel_launches", ctypes.c_int32),
+        ("merge_ms", ctypes.c_double),
+        ("configs", ctypes.c_uint64),
+        ("union_sets", ctypes.c_uint64),
+        ("alg_bytes", ctypes.c_double),
+        ("flops", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load the in-tree engine library (fails loudly if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise EngineError(PSX_ENODEV, f"engine library missing: {path} (run __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    c_int, c_i32, c_i64, c_u64 = ctypes.c_int, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+    P = ctypes.POINTER
+    dbl = ctypes.c_double
+    vp = ctypes.c_void_p
+    sig = {
+        "psx_abi_version": (c_i32, []),
+        "psx_last_error": (ctypes.c_char_p, []),
+        "psx_device_count": (c_int, [P(c_int)]),
+        "psx_create": (c_int, [P(_Problem), c_int, P(vp)]),
+        "psx_destroy": (None, [vp]),
+        "psx_set_shard": (c_int, [vp, c_int, c_int]),
+        "psx_run_exhaustive": (c_int, [vp]),
+        "psx_run_configs": (c_int, [vp, P(ctypes.c_int16), c_i64, c_i32]),
+        "psx_run_sss": (c_int, [vp, P(c_i32)]),
+        "psx_eval_union_batch": (c_int, [vp, P(c_i32), c_i32, c_i32, c_int, P(dbl)]),
+        "psx_reset": (c_int, [vp]),
+        "psx_get_accum": (c_int, [vp, P(_Accum)]),
+        "psx_partials_bytes": (c_i64, [vp]),
+        "psx_export_partials": (c_int, [vp, vp]),
+        "psx_merge_partials": (c_int, [vp, vp, c_i32]),
+        "psx_get_timing": (c_int, [vp, P(Timing)]),
+        "psx_count_configs": (c_u64, [P(_Problem)]),
+        "psx_psd_shift": (c_int, [P(dbl), c_i32, P(dbl)]),
+        "psx_lowrank_study": (c_int, [P(dbl), P(dbl), c_i32, P(dbl), P(dbl)]),
+        "psx_sym_eigen": (c_int, [P(dbl), c_i32, P(dbl), P(dbl)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _ptr(a, ctype):
+    return a.ctypes.data_as(ctypes.POINTER(ctype))
+
+
+def _check(rc: int):
+    if rc != PSX_OK:
+        raise EngineError(rc, load_library().psx_last_error().decode())
+
+
+def device_count() -> int:
+    c = ctypes.c_int(0)
+    load_library().psx_device_count(ctypes.byref(c))
+    return c.value
+
+
+# ---------------------------------------------------------------------------
+# Model setup (model.h:171-264) through the host C++ in the same library
+# ---------------------------------------------------------------------------
+def psd_shift(sigma: np.ndarray):
+    """util.cpp:195-226: returns (sigma + a I, a)."""
+    s = np.ascontiguousarray(sigma, dtype=np.float64).copy()
+    add = ctypes.c_double(0.0)
+    _check(load_library().psx_psd_shift(_ptr(s, ctypes.c_double), s.shape[0], ctypes.byref(add)))
+    return s, add.value
+
+
+def lowrank_study(sigma: np.ndarray, z: np.ndarray):
+    """model.h:213-259: (B column-major flattened, S')."""
+    m = sigma.shape[0]
+    s = np.ascontiguousarray(sigma, dtype=np.float64)
+    zz = np.ascontiguousarray(z, dtype=np.float64)
+    B = np.empty(m * m, dtype=np.float64)
+    sp = np.empty(m, dtype=np.float64)
+    _check(load_library().psx_lowrank_study(_ptr(s, ctypes.c_double), _ptr(zz, ctypes.c_double), m,
+                                             _ptr(B, ctypes.c_double), _ptr(sp, ctypes.c_double)))
+    return B, sp
+
+
+def sym_eigen(a: np.ndarray):
+    m = a.shape[0]
+    aa = np.ascontiguousarray(a, dtype=np.float64)
+    w = np.empty(m)
+    q = np.empty((m, m))
+    _check(load_library().psx_sym_eigen(_ptr(aa, ctypes.c_double), m, _ptr(w, ctypes.c_double),
+                                        _ptr(q, ctypes.c_double)))
+    return w, q
+
+
+@dataclass
+class Seam:
+    """PostCal constructor inputs (postcal.h:118) for two studies."""
+    m: np.ndarray            # int32[2]
+    B: np.ndarray            # float64, per-study column-major blocks concatenated
+    s_prime: np.ndarray      # float64[N]
+    union_to_local: np.ndarray  # int32[2, U]
+    sample_sizes: np.ndarray    # int32[2]
+    max_causal: int = 3
+    sharing_param: float = 0.75
+    gamma: float = 0.01
+    t_squared: float = 0.52
+    s_squared: float = 5.2
+
+    @property
+    def n_union(self):
+        return int(self.union_to_local.shape[1])
+
+    @property
+    def N(self):
+        return int(self.m.sum())
+
+    def _struct(self):
+        self._keep = [np.ascontiguousarray(self.m, dtype=np.int32),
+                      np.ascontiguousarray(self.B, dtype=np.float64),
+                      np.ascontiguousarray(self.s_prime, dtype=np.float64),
+                      np.ascontiguousarray(self.union_to_local, dtype=np.int32),
+                      np.ascontiguousarray(self.sample_sizes, dtype=np.int32)]
+        m, B, sp, u2l, n = self._keep
+        p = _Problem()
+        p.n_studies = 2
+        p.m = _ptr(m, ctypes.c_int32)
+        p.B = _ptr(B, ctypes.c_double)
+        p.s_prime = _ptr(sp, ctypes.c_double)
+        p.n_union = u2l.shape[1]
+        p.union_to_local = _ptr(u2l, ctypes.c_int32)
+        p.max_causal = int(self.max_causal)
+        p.sample_sizes = _ptr(n, ctypes.c_int32)
+        p.sharing_param = float(self.sharing_param)
+        p.gamma = float(self.gamma)
+        p.t_squared = float(self.t_squared)
+        p.s_squared = float(self.s_squared)
+        return p
+
+    def count_configs(self) -> int:
+        p = self._struct()
+        return int(load_library().psx_count_configs(ctypes.byref(p)))
+
+
+def seam_from_arrays(ld, z, union_to_local, sample_sizes, **params) -> Seam:
+    """Model setup (model.h:171-264): PSD shift + eigen low-rank transform per study."""
+    Bs, sps, ms = [], [], []
+    for s in range(2):
+        sig, _ = psd_shift(np.asarray(ld[s], dtype=np.float64))
+        B, sp = lowrank_study(sig, np.asarray(z[s], dtype=np.float64))
+        Bs.append(B)
+        sps.append(sp)
+        ms.append(sig.shape[0])
+    return Seam(m=np.array(ms, dtype=np.int32), B=np.concatenate(Bs), s_prime=np.concatenate(sps),
+                union_to_local=np.asarray(union_to_local, dtype=np.int32),
+                sample_sizes=np.asarray(sample_sizes, dtype=np.int32), **params)
+
+
+@dataclass
+class Accumulators:
+    """PostCal accumulators in the reference's log-space convention (0 = empty)."""
+    post: np.ndarray
+    no_causal: np.ndarray
+    shared: np.ndarray
+    shared_ll: np.ndarray
+    notshared_ll: np.ndarray
+    total: float
+    n_configs: int
+
+    def pips(self):
+        """special_exp(post, total) (postcal.h:277-283)."""
+        def se(v):
+            out = np.exp(v - self.total)
+            out[v == 0] = 0.0
+            return out
+        return se(self.post), se(self.no_causal), se(self.shared)
+
+
+class PostCal:
+    """The engine handle: one per GPU (postcal.h:118 PostCal::PostCal)."""
+
+    def __init__(self, seam: Seam, device: int = 0):
+        self.lib = load_library()
+        self.seam = seam
+        self._p = seam._struct()
+        h = ctypes.c_void_p()
+        _check(self.lib.psx_create(ctypes.byref(self._p), int(device), ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.psx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_shard(self, rank: int, world: int):
+        _check(self.lib.psx_set_shard(self.h, rank, world))
+
+    def run_exhaustive(self):
+        """postcal.cpp:716 computeTotalLikelihood."""
+        _check(self.lib.psx_run_exhaustive(self.h))
+
+    def run_configs(self, rows: np.ndarray):
+        """postcal.cpp:400 computeTotalLikelihoodGivenConfigs; rows int16 [n, groups]."""
+        r = np.ascontiguousarray(rows, dtype=np.int16)
+        _check(self.lib.psx_run_configs(self.h, _ptr(r, ctypes.c_int16), r.shape[0], r.shape[1]))
+
+    def run_sss(self) -> int:
+        """sss_postcal.cpp:102 sss_computeTotalLikelihood; returns iterations."""
+        it = ctypes.c_int32(0)
+        _check(self.lib.psx_run_sss(self.h, ctypes.byref(it)))
+        return it.value
+
+    def eval_union_batch(self, sets: np.ndarray, accumulate: bool = False) -> np.ndarray:
+        """sss_postcal.cpp:447 expand_and_compute_lkl over a batch; returns scores."""
+        s = np.ascontiguousarray(sets, dtype=np.int32)
+        out = np.empty(s.shape[0], dtype=np.float64)
+        _check(self.lib.psx_eval_union_batch(self.h, _ptr(s, ctypes.c_int32), s.shape[1], s.shape[0],
+                                             1 if accumulate else 0, _ptr(out, ctypes.c_double)))
+        return out
+
+    def reset(self):
+        _check(self.lib.psx_reset(self.h))
+
+    def accum(self) -> Accumulators:
+        N, U = self.seam.N, self.seam.n_union
+        post, noc = np.zeros(N), np.zeros(2)
+        sh, sll, nsll = np.zeros(U), np.zeros(U), np.zeros(U)
+        a = _Accum()
+        a.post, a.no_causal = _ptr(post, ctypes.c_double), _ptr(noc, ctypes.c_double)
+        a.shared, a.shared_ll = _ptr(sh, ctypes.c_double), _ptr(sll, ctypes.c_double)
+        a.notshared_ll = _ptr(nsll, ctypes.c_double)
+        _check(self.lib.psx_get_accum(self.h, ctypes.byref(a)))
+        return Accumulators(post, noc, sh, sll, nsll, a.total, int(a.n_configs))
+
+    def timing(self) -> dict:
+        t = Timing()
+        _check(self.lib.psx_get_timing(self.h, ctypes.byref(t)))
+        return t.as_dict()
+
+    def partials_bytes(self) -> int:
+        return int(self.lib.psx_partials_bytes(self.h))
+
+    def export_partials(self, device_ptr: int):
+        _check(self.lib.psx_export_partials(self.h, ctypes.c_void_p(device_ptr)))
+
+    def merge_partials(self, device_ptr: int, count: int):
+        _check(self.lib.psx_merge_partials(self.h, ctypes.c_void_p(device_ptr), int(count)))
