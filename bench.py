@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""bench.py — PostCal exhaustive sweep on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload syn1000c3]
+
+A step is one full exhaustive sweep of the locus (every causal configuration,
+postcal.cpp:716-1092) plus, for N > 1, the single RCCL all-gather + merge of
+the per-GPU accumulators.  The locus is sharded across ranks (one process per
+GPU under torch.distributed.run); the total work per step is fixed, so the
+scaling is "strong".  Inputs are resident in HBM before the timed region.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), including
+`roofline` for the dominant kernel (k_sweep<3>) and `cpu_baseline` (the
+oracle's literal N x N restatement of the reference algorithm timed on the host
+cores on a bounded sample of the same workload, rank 0 at N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+
+# torch first: its bundled HIP runtime then also serves the engine library
+# (same SONAME), so device pointers from torch and from the engine are one space.
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import numpy as np  # noqa: E402
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+from pipsort_amd import engine as E  # noqa: E402
+from pipsort_amd import synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (spec)
+
+WORKLOADS = {
+    # name: (M, c, p, n, description)
+    "syn1000c3": (1000, 3, 0.25, (10000, 8000), "SYN-v1 2-study locus, M=1000 SNPs, -c 3 -p 0.25 -n 10000,8000"),
+    "syn500c3": (500, 3, 0.25, (10000, 8000), "SYN-v1 2-study locus, M=500 SNPs, -c 3 -p 0.25 -n 10000,8000"),
+    "syn200c2": (200, 2, 0.25, (10000, 8000), "SYN-v1 2-study locus, M=200 SNPs, -c 2 -p 0.25 -n 10000,8000"),
+    "example": (None, 2, 0.25, (334324, 6771), "reference tests/example locus, -c 2 -p 0.25 -n 334324,6771"),
+}
+
+
+def build_seam(name):
+    M, c, p, n, _ = WORKLOADS[name]
+    if M is None:
+        import loci
+        L = loci.read_locus("example")
+        return E.seam_from_arrays(L["ld"], L["z"], L["u2l"], n, max_causal=c, sharing_param=p)
+    ld, z, _, _, u2l = synth.syn_v1(M)
+    return E.seam_from_arrays(ld, z, u2l, n, max_causal=c, sharing_param=p)
+
+
+def cpu_baseline(seam, budget_s=15.0, threads=None):
+    """Oracle literal (N x N, postcal.cpp:214-304) per-configuration cost on the
+    host cores, on a random sample of this workload's configurations."""
+    from oracle import oracle as O
+    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    U = seam.n_union
+    k = int(seam.max_causal)
+    rng = np.random.default_rng(0)
+    both = (seam.union_to_local[0] >= 0) & (seam.union_to_local[1] >= 0)
+
+    def sample(n):
+        sets = np.sort(np.stack([rng.choice(U, k, replace=False) for _ in range(n)]), axis=1).astype(np.int32)
+        bits = np.zeros((n, 2, k), dtype=np.int32)
+        for i in range(n):
+            for j in range(k):
+                u = sets[i, j]
+                if both[u]:
+                    x = rng.integers(1, 4)
+                else:
+                    x = 1 if seam.union_to_local[0, u] >= 0 else 2
+                bits[i, 0, j] = x & 1
+                bits[i, 1, j] = (x >> 1) & 1
+        return sets, bits
+
+    O.load()
+    done = [0] * threads
+    stop = time.time() + budget_s
+    work = [sample(4) for _ in range(threads)]
+
+    def run(t):
+        s, b = work[t]
+        while time.time() < stop:
+            O.eval_patterns(seam, s, b, literal=True)
+            done[t] += s.shape[0]
+
+    t0 = time.time()
+    th = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    dt = time.time() - t0
+    n = sum(done)
+    return {"value": n / dt, "unit": "configs/s", "cores": threads, "kind": "port",
+            "sample": f"{n} random {k}-SNP configurations of this workload, oracle literal N x N "
+                      f"restatement of lowrank_likelihood (postcal.cpp:214-304), {threads} host threads, "
+                      f"{dt:.1f} s"}
+
+
+def example_wall():
+    """Wall-clock of the drop-in PIPSORT CLI on tests/example (-c 2 -p 0.25)."""
+    import loci
+    src = os.path.join(loci.GOLDEN, "example")
+    with tempfile.TemporaryDirectory() as d:
+        for f in os.listdir(src):
+            if not f.startswith("expected_"):
+                os.symlink(os.path.join(src, f), os.path.join(d, f))
+        t0 = time.time()
+        r = subprocess.run([E.PIPSORT_BIN, "-c", "2", "-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "snp_map",
+                            "-n", "334324,6771", "-p", "0.25", "-o", "out"], cwd=d, capture_output=True, text=True)
+        wall = time.time() - t0
+        same = all(open(os.path.join(d, f"out_{f}.txt")).read() ==
+                   open(os.path.join(src, f"expected_{f}.txt")).read()
+                   for f in ("study0_post", "study1_post", "study0_set", "study1_set", "nocausal"))
+    return wall if r.returncode == 0 else None, same
+
+
+def load_pmc(workload):
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        if d.get("workload") == workload:
+            return d
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="syn1000c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    t_setup = time.time()
+    seam = build_seam(args.workload)
+    configs_per_step = seam.count_configs()
+    pc = E.PostCal(seam, device=local)
+    pc.set_shard(rank, world)
+    nbytes = pc.partials_bytes()
+    mine = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    gathered = torch.empty(nbytes * world, dtype=torch.uint8, device="cuda")
+    setup_s = time.time() - t_setup
+
+    def step():
+        pc.run_exhaustive()
+        if world > 1:
+            pc.export_partials(mine.data_ptr())
+            dist.all_gather_into_tensor(gathered, mine)  # the one exchange step (RCCL over xGMI)
+            torch.cuda.synchronize()
+            pc.merge_partials(gathered.data_ptr(), world)
+
+    for _ in range(args.warmup):
+        step()
+    kms, launches, sweep_ms = 0.0, 0, 0.0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        t = pc.timing()
+        kms += t["kernel_ms"]
+        launches += t["kernel_launches"]
+        sweep_ms += t["sweep_ms"]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        x = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        elapsed = float(x.item())
+    tm = pc.timing()
+    acc = pc.accum() if (world == 1 or rank == 0) else None
+
+    if rank == 0:
+        value = configs_per_step * args.steps / elapsed
+        avg_kernel_s = (kms / max(launches, 1)) / 1e3
+        alg_bytes = tm["alg_bytes"]  # per launch of the dominant kernel (this rank's shard)
+        achieved = alg_bytes / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
+        pmc = load_pmc(args.workload) if world == 1 else None
+        roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS,
+                    "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+                    "kernel": "k_sweep<3>" if seam.max_causal >= 3 else "k_sweep<2>",
+                    "kernel_ms": avg_kernel_s * 1e3,
+                    "alg_bytes_per_launch": alg_bytes}
+        fp64 = {"achieved": tm["flops"] / avg_kernel_s / 1e12 if avg_kernel_s > 0 else 0.0,
+                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s"}
+        fp64["frac"] = fp64["achieved"] / FP64_PEAK_TFLOPS
+        out = {
+            "metric": "causal configurations evaluated/sec (whole node)",
+            "value": value,
+            "unit": "configs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic" if args.workload != "example" else "reference fixture",
+            "config": {"workload": WORKLOADS[args.workload][4], "union_snps": seam.n_union,
+                       "max_causal": int(seam.max_causal), "configs_per_step": configs_per_step,
+                       "parallelism": f"config-shard x{world} + 1 RCCL all-gather" if world > 1 else "single GPU"},
+            "roofline": roofline,
+            "fp64": fp64,
+            "setup_s": setup_s,
+            "configs_checked": int(acc.n_configs) if acc is not None else None,
+        }
+        if world == 1:
+            w, same = example_wall()
+            out["example_wall_s"] = w
+            out["example_outputs_match_reference"] = same
+            if not args.no_cpu_baseline:
+                out["cpu_baseline"] = cpu_baseline(seam, budget_s=args.cpu_budget)
+        print(json.dumps(out), flush=True)
+    pc.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

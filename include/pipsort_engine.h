@@ -127,6 +127,17 @@ int64_t psx_partials_bytes(psx_engine *e);
 int psx_export_partials(psx_engine *e, void *device_dst);
 int psx_merge_partials(psx_engine *e, const void *device_src, int32_t count);
 
+/* Host-only (no GPU needed): fold `count` partial images of `image_bytes`
+ * bytes each (psx_export_partials layout, rank order) into one image at dst —
+ * the same fold psx_merge_partials runs on the device, for partials gathered
+ * through a host collective. */
+int psx_fold_partials_host(const void *src, int32_t count, int64_t image_bytes, void *dst);
+
+/* Host-only: union subsets and configurations of causal-set level k (1..c)
+ * that shard `rank` of `world` evaluates in psx_run_exhaustive. */
+int psx_shard_stats(const psx_problem *prob, int32_t k, int32_t rank, int32_t world, uint64_t *union_sets,
+                    double *configs);
+
 /* Timing of the last psx_run_* on this handle. */
 int psx_get_timing(psx_engine *e, psx_timing *t);
 

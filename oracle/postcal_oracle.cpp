@@ -314,7 +314,7 @@ class PostCal {
         for (int s = 1; s < P.S; s++) off[s] = off[s - 1] + P.m[s - 1];
         G.resize(P.S);
         y.resize(P.S);
-        for (int s = 0; s < P.S; s++) {
+        for (int s = 0; s < P.S && !literal; s++) {  // literal mode works from B directly
             int M = P.m[s];
             const vector<double>& B = P.B[s];
             G[s].assign((size_t)M * M, 0.0);

@@ -1033,6 +1033,60 @@ int psx_merge_partials(psx_engine* e, const void* src, int32_t count) {
     return 0;
 }
 
+int psx_fold_partials_host(const void* src, int32_t count, int64_t image_bytes, void* dst) {
+    if (count < 1 || image_bytes < (int64_t)(2 * sizeof(Acc5)) || image_bytes % (int64_t)sizeof(Acc5) != 0)
+        return fail(PSX_EINVAL, "bad partial image size");
+    const size_t n = (size_t)image_bytes / sizeof(Acc5);  // ldg Acc5 slots + 1 SetRec slot
+    const Acc5* parts = (const Acc5*)src;
+    std::vector<Acc5> out(n);
+    std::memset(out.data(), 0, n * sizeof(Acc5));
+    for (size_t u = 0; u + 1 < n; u++) {
+        Acc5 a = {0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        for (int r = 0; r < count; r++) psx::fold_acc(a, parts[(size_t)r * n + u]);
+        out[u] = a;
+    }
+    SetRec s = {0, 0, 0.0, 0.0, 0.0, 1e300, 0.0};
+    for (int r = 0; r < count; r++) psx::fold_set(s, *reinterpret_cast<const SetRec*>(parts + (size_t)r * n + n - 1));
+    std::memcpy(&out[n - 1], &s, sizeof(SetRec));
+    std::memcpy(dst, out.data(), n * sizeof(Acc5));
+    return 0;
+}
+
+int psx_shard_stats(const psx_problem* p, int32_t k, int32_t rank, int32_t world, uint64_t* union_sets,
+                    double* configs) {
+    if (!p || p->n_studies != 2 || k < 1 || world < 1 || rank < 0 || rank >= world)
+        return fail(PSX_EINVAL, "bad arguments");
+    const int U = p->n_union;
+    const int ldg = (U + 63) / 64 * 64;
+    std::vector<unsigned char> pres(ldg, 0);
+    for (int s = 0; s < 2; s++)
+        for (int u = 0; u < U; u++)
+            if (p->union_to_local[s * U + u] >= 0) pres[u] |= (unsigned char)(1 << s);
+    double sets = 0, cfg = 0, bytes = 0;
+    if (psx::sweep_supports(k, U)) {
+        std::vector<psx::PlanUnit> mine;
+        int ca = 0;
+        psx::plan_units(k, U, ldg, rank, world, pres.data(), mine, ca, sets, cfg, bytes);
+    } else {
+        uint64_t total = choose_u64(U, k);
+        uint64_t lo = total * (uint64_t)rank / world, hi = total * (uint64_t)(rank + 1) / world;
+        if (lo < hi) {
+            std::vector<int> c(k);
+            unrank_lex(lo, U, k, c.data());
+            for (uint64_t r = lo; r < hi; r++) {
+                double w = 1;
+                for (int j = 0; j < k; j++) w *= (pres[c[j]] == 3) ? 3.0 : 1.0;
+                sets += 1;
+                cfg += w;
+                next_lex(c.data(), U, k);
+            }
+        }
+    }
+    if (union_sets) *union_sets = (uint64_t)(sets + 0.5);
+    if (configs) *configs = cfg;
+    return 0;
+}
+
 int psx_get_timing(psx_engine* e, psx_timing* t) {
     *t = e->timing;
     return 0;

@@ -59,6 +59,9 @@ struct SweepPlanCache {
 };
 
 bool sweep_supports(int k, int U);
+struct PlanUnit { int a0, a1, B, T; double work; };
+int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* pres_host,
+               std::vector<PlanUnit>& mine, int& ca, double& sets, double& configs, double& bytes);
 int sweep_level(SweepPlanCache& cache, int k, int U, int ldg, int rank, int world, hipStream_t stream,
                 const SweepArgs& a, Acc5* acc, SetRec* sacc, SweepStats* st);
 void sweep_free(SweepPlanCache& cache);

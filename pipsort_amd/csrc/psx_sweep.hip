@@ -415,18 +415,18 @@ static double set_alg_bytes(int k, const int* memb /*bit0 study0, bit1 study1*/)
     return tot;
 }
 
-static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, const unsigned char* pres_host) {
+// Host-only decomposition of level k into wave units for shard (rank, world),
+// plus exact union-set / configuration counts and algorithmic bytes.
+int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* pres_host,
+               std::vector<PlanUnit>& mine, int& ca, double& sets, double& configs, double& bytes) {
     const int nblk = ldg / 64;
-    P.k = k; P.U = U; P.ldg = ldg; P.rank = rank; P.world = world;
-    struct Unit { int a0, a1, B, T; double work; };
-    std::vector<Unit> all;
+    std::vector<PlanUnit> all;
     if (k == 3) {
         double total_a = 0;
         for (int T = 0; T < nblk; T++)
             for (int B = 0; B <= T; B++) total_a += std::min(64 * B + 63, U);
-        int ca = (int)std::floor(total_a / (4096.0 * world));
+        ca = (int)std::floor(total_a / (4096.0 * world));
         ca = std::max(1, std::min(64, ca));
-        P.ca = ca;
         for (int T = 0; T < nblk; T++) {
             if (64 * T >= U) break;
             for (int B = 0; B <= T; B++) {
@@ -438,9 +438,8 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
                 }
             }
         }
-        P.rec_stride = 128 + ca;
-    } else {
-        P.ca = 0;
+    } else if (k == 2) {
+        ca = 0;
         for (int T = 0; T < nblk; T++) {
             if (64 * T >= U) break;
             for (int B = 0; B <= T; B++) {
@@ -448,21 +447,20 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
                 all.push_back({0, 1, B, T, 1.0});
             }
         }
-        P.rec_stride = 128;
+    } else {
+        return -1;
     }
     // contiguous shard with ~equal work
     double wsum = 0;
     for (auto& u : all) wsum += u.work;
     double lo = wsum * rank / world, hi = wsum * (rank + 1) / world, run = 0;
-    std::vector<Unit> mine;
+    mine.clear();
     for (auto& u : all) {
         double mid = run + 0.5 * u.work;
         if (mid >= lo && mid < hi) mine.push_back(u);
         run += u.work;
     }
-    P.n_units = (int)mine.size();
-    // exact union-set count and algorithmic bytes of this shard: membership
-    // classes (1 study0, 2 study1, 3 both) with prefix counts over a
+    // exact counts: membership classes (1 study0, 2 study1, 3 both) with prefix counts
     double bytes_cls[4][4][4];
     for (int x = 1; x < 4; x++)
         for (int y = 1; y < 4; y++)
@@ -470,12 +468,13 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
                 int m3[3] = {x, y, z};
                 bytes_cls[x][y][z] = (k == 3) ? set_alg_bytes(3, m3) : set_alg_bytes(2, m3 + 1);
             }
+    const double wcls[4] = {0, 1, 1, 3};
     std::vector<int> pref[4];
     for (int x = 1; x < 4; x++) {
         pref[x].assign(U + 1, 0);
         for (int i = 0; i < U; i++) pref[x][i + 1] = pref[x][i] + (pres_host[i] == x);
     }
-    double sets = 0, bytes = 0;
+    sets = 0; bytes = 0; configs = 0;
     for (auto& u : mine) {
         for (int t = 0; t < 64; t++) {
             int b = 64 * u.B + t;
@@ -484,6 +483,7 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
             int c_hi = std::min(64 * u.T + 64, U);
             if (c_hi <= c_lo) continue;
             int mb = pres_host[b];
+            if (mb == 0) continue;
             if (k == 3) {
                 int ahi = std::min(u.a1, b);
                 if (ahi <= u.a0) continue;
@@ -494,6 +494,7 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
                         double ncz = pref[z][c_hi] - pref[z][c_lo];
                         sets += na * ncz;
                         bytes += na * ncz * bytes_cls[x][mb][z];
+                        configs += na * ncz * wcls[x] * wcls[mb] * wcls[z];
                     }
                 }
             } else {
@@ -501,10 +502,26 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
                     double ncz = pref[z][c_hi] - pref[z][c_lo];
                     sets += ncz;
                     bytes += ncz * bytes_cls[1][mb][z];
+                    configs += ncz * wcls[mb] * wcls[z];
                 }
             }
         }
     }
+    return 0;
+}
+
+static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, const unsigned char* pres_host) {
+    P.k = k; P.U = U; P.ldg = ldg; P.rank = rank; P.world = world;
+    std::vector<PlanUnit> mine;
+    int ca = 0;
+    double sets = 0, configs = 0, bytes = 0;
+    if (plan_units(k, U, ldg, rank, world, pres_host, mine, ca, sets, configs, bytes)) {
+        g_sweep_err = "unsupported sweep level";
+        return -1;
+    }
+    P.ca = ca;
+    P.rec_stride = (k == 3) ? 128 + ca : 128;
+    P.n_units = (int)mine.size();
     P.union_sets = (uint64_t)sets;
     P.alg_bytes = bytes;
     // FP64 operation estimate per union set (prefix, c-row
@@ -522,7 +539,7 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     // CSR: record -> SNP, grouped by SNP in record order (deterministic folds)
     std::vector<int> key((size_t)P.n_units * P.rec_stride, -1);
     for (int i = 0; i < P.n_units; i++) {
-        const Unit& u = mine[i];
+        const PlanUnit& u = mine[i];
         int* kk = key.data() + (size_t)i * P.rec_stride;
         for (int t = 0; t < 64; t++) {
             int c = 64 * u.T + t;

@@ -31,6 +31,7 @@ EXPORTED = [
     "psx_set_shard", "psx_run_exhaustive", "psx_run_configs", "psx_run_sss",
     "psx_eval_union_batch", "psx_reset", "psx_get_accum", "psx_partials_bytes",
     "psx_export_partials", "psx_merge_partials", "psx_get_timing", "psx_count_configs",
+    "psx_fold_partials_host", "psx_shard_stats",
     "psx_psd_shift", "psx_lowrank_study", "psx_sym_eigen",
 ]
 
@@ -119,6 +120,8 @@ def load_library(path: str = LIB_PATH):
         "psx_merge_partials": (c_int, [vp, vp, c_i32]),
         "psx_get_timing": (c_int, [vp, P(Timing)]),
         "psx_count_configs": (c_u64, [P(_Problem)]),
+        "psx_fold_partials_host": (c_int, [vp, c_i32, c_i64, vp]),
+        "psx_shard_stats": (c_int, [P(_Problem), c_i32, c_i32, c_i32, P(c_u64), P(dbl)]),
         "psx_psd_shift": (c_int, [P(dbl), c_i32, P(dbl)]),
         "psx_lowrank_study": (c_int, [P(dbl), P(dbl), c_i32, P(dbl), P(dbl)]),
         "psx_sym_eigen": (c_int, [P(dbl), c_i32, P(dbl), P(dbl)]),
@@ -227,6 +230,15 @@ class Seam:
         p = self._struct()
         return int(load_library().psx_count_configs(ctypes.byref(p)))
 
+    def shard_stats(self, k: int, rank: int, world: int):
+        """(union sets, configurations) of level k evaluated by shard rank/world (host only)."""
+        p = self._struct()
+        sets = ctypes.c_uint64(0)
+        cfg = ctypes.c_double(0)
+        _check(load_library().psx_shard_stats(ctypes.byref(p), k, rank, world, ctypes.byref(sets),
+                                              ctypes.byref(cfg)))
+        return int(sets.value), float(cfg.value)
+
 
 def seam_from_arrays(ld, z, union_to_local, sample_sizes, **params) -> Seam:
     """Model setup (model.h:171-264): PSD shift + eigen low-rank transform per study."""
@@ -240,6 +252,22 @@ def seam_from_arrays(ld, z, union_to_local, sample_sizes, **params) -> Seam:
     return Seam(m=np.array(ms, dtype=np.int32), B=np.concatenate(Bs), s_prime=np.concatenate(sps),
                 union_to_local=np.asarray(union_to_local, dtype=np.int32),
                 sample_sizes=np.asarray(sample_sizes, dtype=np.int32), **params)
+
+
+def fold_partials_host(images: np.ndarray) -> np.ndarray:
+    """Fold partial images (uint8 [count, image_bytes], rank order) on the host."""
+    imgs = np.ascontiguousarray(images, dtype=np.uint8)
+    out = np.empty(imgs.shape[1], dtype=np.uint8)
+    _check(load_library().psx_fold_partials_host(imgs.ctypes.data_as(ctypes.c_void_p), imgs.shape[0],
+                                                 imgs.shape[1], out.ctypes.data_as(ctypes.c_void_p)))
+    return out
+
+
+# partial image record layout (psx_math.h Acc5 / SetRec)
+ACC5_DTYPE = np.dtype([("mP", "<i4"), ("mS", "<i4"), ("mN", "<i4"), ("pad", "<i4"), ("post0", "<f8"),
+                       ("post1", "<f8"), ("shared", "<f8"), ("sll", "<f8"), ("nsll", "<f8")])
+SETREC_DTYPE = np.dtype([("m", "<i4"), ("pad", "<i4"), ("tot", "<f8"), ("nc0", "<f8"), ("nc1", "<f8"),
+                         ("score", "<f8"), ("npat", "<f8")])
 
 
 @dataclass
@@ -256,7 +284,8 @@ class Accumulators:
     def pips(self):
         """special_exp(post, total) (postcal.h:277-283)."""
         def se(v):
-            out = np.exp(v - self.total)
+            with np.errstate(over="ignore"):
+                out = np.exp(v - self.total)
             out[v == 0] = 0.0
             return out
         return se(self.post), se(self.no_causal), se(self.shared)

@@ -56,7 +56,7 @@ def mixed_locus(M0: int, M1: int, n_shared: int, seed: int = 7):
     for s, M in enumerate((M0, M1)):
         x = rng.standard_normal((M, 3 * M))
         x = x + 0.8 * np.roll(x, 1, axis=0)
-        sig = np.corrcoef(x)
+        sig = np.atleast_2d(np.corrcoef(x))
         lam = np.zeros(M)
         lam[rng.integers(0, M)] = 4.0 + s
         zs = sig @ lam + rng.standard_normal(M) * 0.5

@@ -1,0 +1,109 @@
+"""C-ABI library: loads, exports every declared symbol, refuses to run without a
+GPU, and its host-only helpers are exact.  CPU only (no compute calls)."""
+import math
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import loci
+from pipsort_amd import engine as E
+from pipsort_amd import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    names = set()
+    for h in ("pipsort_engine.h", "pipsort_model.h"):
+        txt = open(os.path.join(ROOT, "include", h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        names |= set(re.findall(r"\b(psx_\w+)\s*\(", txt))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = E.load_library()
+    decl = _declared()
+    assert decl == set(E.EXPORTED)
+    dyn = subprocess.run(["nm", "-D", "--defined-only", E.LIB_PATH], capture_output=True, text=True).stdout
+    for name in decl:
+        assert re.search(rf"\bT {name}\b", dyn), name
+        assert getattr(lib, name)
+    assert lib.psx_abi_version() == 1
+
+
+def test_no_cpu_fallback():
+    if E.device_count() > 0:
+        pytest.skip("a HIP device is present")
+    seam, _ = loci.seam_for(loci.SMALL)
+    with pytest.raises(E.EngineError) as ei:
+        E.PostCal(seam)
+    assert ei.value.code == E.PSX_ENODEV
+
+
+def _count_seam(u2l, c):
+    U = u2l.shape[1]
+    m = np.array([(u2l[0] >= 0).sum(), (u2l[1] >= 0).sum()], dtype=np.int32)
+    return E.Seam(m=m, B=np.zeros(1), s_prime=np.zeros(1), union_to_local=u2l,
+                  sample_sizes=np.array([1, 1], dtype=np.int32), max_causal=c)
+
+
+def test_configuration_counts_match_survey():
+    L = loci.read_locus("example")
+    assert _count_seam(L["u2l"], 2).count_configs() == 216_817
+    for M, c, n in ((200, 2, 179_701), (500, 3, 560_253_751), (1000, 3, 4_491_007_501)):
+        u2l = np.stack([np.arange(M), np.arange(M)]).astype(np.int32)
+        assert _count_seam(u2l, c).count_configs() == n
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shards_partition_every_level(world):
+    _, _, _, _, u2l = synth.mixed_locus(150, 170, 120, seed=3)
+    U = u2l.shape[1]
+    w = np.where((u2l[0] >= 0) & (u2l[1] >= 0), 3, 1)
+    seam = _count_seam(u2l, 3)
+    for k in (1, 2, 3):
+        tot_sets, tot_cfg = 0, 0.0
+        for r in range(world):
+            s, c = seam.shard_stats(k, r, world)
+            tot_sets += s
+            tot_cfg += c
+        assert tot_sets == math.comb(U, k)
+        # e_k of the per-SNP pattern weights
+        e = np.zeros(k + 1)
+        e[0] = 1
+        for x in w:
+            e[1:] = e[1:] + e[:-1] * x
+        assert abs(tot_cfg - e[k]) < 0.5
+
+
+def test_partial_fold_is_associative_and_order_fixed():
+    rng = np.random.default_rng(0)
+    ldg = 128
+    imgs = []
+    for r in range(4):
+        a = np.zeros(ldg + 1, dtype=E.ACC5_DTYPE)
+        for f in ("mP", "mS", "mN"):
+            a[f] = rng.integers(-3000, 3000, ldg + 1)
+        for f in ("post0", "post1", "shared", "sll", "nsll"):
+            a[f] = rng.random(ldg + 1) * (rng.random(ldg + 1) > 0.2)
+        s = np.zeros(1, dtype=E.SETREC_DTYPE)
+        s["m"], s["tot"], s["nc0"], s["nc1"], s["score"], s["npat"] = rng.integers(-50, 50), 1.5, 0.5, 0.25, -3.0, 7
+        raw = a.tobytes()
+        raw = raw[: ldg * 56] + s.tobytes() + b"\0" * (56 - s.itemsize)
+        imgs.append(np.frombuffer(raw, dtype=np.uint8))
+    imgs = np.stack(imgs)
+    full = E.fold_partials_host(imgs)
+    left = E.fold_partials_host(np.stack([E.fold_partials_host(imgs[:2]), E.fold_partials_host(imgs[2:])]))
+    A = np.frombuffer(full[: ldg * 56].tobytes(), dtype=E.ACC5_DTYPE)
+    B = np.frombuffer(left[: ldg * 56].tobytes(), dtype=E.ACC5_DTYPE)
+
+    def val(x, m, s):
+        return np.where(x[s] > 0, x[m] + np.log2(np.where(x[s] > 0, x[s], 1)), -np.inf)
+    for m, s in (("mP", "post0"), ("mP", "post1"), ("mS", "sll"), ("mN", "nsll")):
+        np.testing.assert_allclose(val(A, m, s), val(B, m, s), rtol=0, atol=1e-12)
+    sa = np.frombuffer(full[ldg * 56: ldg * 56 + 48].tobytes(), dtype=E.SETREC_DTYPE)[0]
+    assert sa["npat"] == 28 and sa["score"] == -3.0

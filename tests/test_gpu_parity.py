@@ -1,0 +1,256 @@
+"""GPU parity: the HIP engine (through the C ABI) against the oracle restatement
+and the reference's own golden files.  Marked gpu; run on an MI355X."""
+import dataclasses
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import loci
+from oracle import oracle as O
+from pipsort_amd import engine as E
+from pipsort_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+PIP_TOL = 1e-6  # north star: PIPs within 1e-6 of the reference
+
+
+def _sexp(v, t):
+    with np.errstate(over="ignore"):
+        r = np.exp(v - t)
+    r[v == 0] = 0.0
+    return r
+
+
+def assert_parity(got: E.Accumulators, ref: dict, pip_tol=1e-9, ll_rtol=1e-10):
+    assert got.n_configs == ref["n_configs"]
+    assert abs(got.total - ref["total"]) <= 1e-9 * max(1.0, abs(ref["total"]))
+    for name in ("post", "no_causal", "shared"):
+        g, r = getattr(got, name), ref[name]
+        assert np.array_equal(g == 0, r == 0), name  # same "empty" entries
+        d = np.abs(_sexp(g, got.total) - _sexp(r, ref["total"])).max()
+        assert d <= pip_tol, (name, d)
+    for name in ("shared_ll", "notshared_ll"):
+        g, r = getattr(got, name), ref[name]
+        assert np.array_equal(g == 0, r == 0), name
+        np.testing.assert_allclose(g, r, rtol=ll_rtol, atol=0, err_msg=name)
+
+
+@pytest.mark.parametrize("c", [1, 2, 3])
+def test_small_example_exhaustive(gpu, c):
+    seam, _ = loci.seam_for(loci.SMALL, c=c)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    assert_parity(pc.accum(), O.postcal(seam))
+
+
+@pytest.mark.parametrize("p", [0.0, 0.25, 0.75, 0.999])
+def test_sharing_param_edges(gpu, p):
+    """p == 0 skips the sharing prior (postcal.cpp:27).  (p == 1 is degenerate in
+    the reference: -inf * 0 at postcal.cpp:1023 turns postValues into NaN.)"""
+    seam, _ = loci.seam_for(loci.SMALL, c=3, p=p)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    assert_parity(pc.accum(), O.postcal(seam))
+
+
+def test_example_locus_against_oracle(gpu):
+    seam, _ = loci.seam_for(loci.EXAMPLE)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    got = pc.accum()
+    assert got.n_configs == 216_817
+    assert_parity(got, O.postcal(seam), ll_rtol=1e-11)
+
+
+def test_pipsort_cli_reproduces_reference_goldens(gpu, tmp_path):
+    """tests/example/run_example.sh:1 through the drop-in executable: the PIP /
+    set / no-causal files are byte-identical to the reference's expected files."""
+    d = tmp_path / "example"
+    shutil.copytree(os.path.join(loci.GOLDEN, "example"), d)
+    r = subprocess.run([E.PIPSORT_BIN, "-c", "2", "-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "snp_map", "-n",
+                        "334324,6771", "-p", "0.25", "-o", "pipsort_results"], cwd=d, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for f in ("study0_post", "study1_post", "study0_set", "study1_set", "nocausal"):
+        assert open(d / f"pipsort_results_{f}.txt").read() == open(d / f"expected_{f}.txt").read(), f
+    g = [l.split("\t") for l in open(d / "pipsort_results_shared_pips.txt").read().splitlines()]
+    e = [l.split("\t") for l in open(d / "expected_shared_pips.txt").read().splitlines()]
+    assert [x[:2] for x in g] == [x[:2] for x in e]
+    gl = np.array([[float(x[2]), float(x[3])] for x in g[1:]])
+    el = np.array([[float(x[2]), float(x[3])] for x in e[1:]])
+    # LL columns are race-affected in the reference (postcal.cpp:1012-1017)
+    assert (np.abs(gl - el) > 1e-6 * np.abs(el).clip(1)).any(axis=1).sum() <= 1
+    for f in ("study0_post", "study1_post"):
+        a = [float(l.split()[1]) for l in open(d / f"pipsort_results_{f}.txt").read().splitlines()[1:]]
+        b = [float(l.split()[1]) for l in open(d / f"expected_{f}.txt").read().splitlines()[1:]]
+        assert np.abs(np.array(a) - np.array(b)).max() <= PIP_TOL
+
+
+def test_configs_file_path(gpu):
+    seam, L = loci.seam_for(loci.CONFIGS)
+    rows = np.fromfile(os.path.join(L["dir"], "all_configs_int16"), dtype=np.int16).reshape(72, 5)
+    pc = E.PostCal(seam)
+    pc.run_configs(rows)
+    assert_parity(pc.accum(), O.postcal(seam, "configs", rows))
+
+
+def test_configs_row_order_error(gpu):
+    """postcal.cpp:587-590: a row whose entries are not study-major exits 1."""
+    seam, _ = loci.seam_for(loci.CONFIGS)
+    bad = np.array([[9, 0, -1, -1, -1]], dtype=np.int16)  # study-1 index before a study-0 index
+    pc = E.PostCal(seam)
+    with pytest.raises(E.EngineError) as ei:
+        pc.run_configs(bad)
+    assert ei.value.code == E.PSX_EORDER
+
+
+@pytest.mark.parametrize("spec,c", [(loci.SMALL, 3), (loci.EXAMPLE, 2)])
+def test_sss_walk(gpu, spec, c):
+    seam, _ = loci.seam_for(spec, c=c)
+    pc = E.PostCal(seam)
+    pc.run_sss()
+    assert_parity(pc.accum(), O.postcal(seam, "sss"), ll_rtol=1e-11)
+
+
+def test_sss_synthetic_c5(gpu):
+    ld, z, _, _, u2l = synth.syn_v1(60)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=5, sharing_param=0.25)
+    pc = E.PostCal(seam)
+    pc.run_sss()
+    assert_parity(pc.accum(), O.postcal(seam, "sss"), ll_rtol=1e-11)
+
+
+def test_union_batch_scores(gpu):
+    """expand_and_compute_lkl scores (max |L| pattern) for ragged sets incl. the null set."""
+    seam, _ = loci.seam_for(loci.SMALL, c=3)
+    pc = E.PostCal(seam)
+    sets = np.array([[-1, -1, -1], [5, -1, -1], [0, 5, -1], [1, 2, 5], [3, 7, 9], [0, 1, 2]], dtype=np.int32)
+    got = pc.eval_union_batch(sets)
+    # oracle: score = most negative L over the expanded assignments
+    ref = []
+    for row in sets:
+        mem = [x for x in row if x >= 0]
+        if not mem:
+            r = O.postcal(dataclasses.replace(seam, max_causal=0))
+            ref.append(r["total"])
+            continue
+        k = len(mem)
+        best = None
+        for p in range(3 ** k):
+            b = np.zeros((1, 2, k), dtype=np.int32)
+            ok = True
+            for j in range(k):
+                x = (p // 3 ** j) % 3 + 1
+                if (x & 1 and seam.union_to_local[0, mem[j]] < 0) or (x & 2 and seam.union_to_local[1, mem[j]] < 0):
+                    ok = False
+                b[0, 0, j], b[0, 1, j] = x & 1, (x >> 1) & 1
+            if not ok:
+                continue
+            L, _ = O.eval_patterns(seam, np.array([mem], dtype=np.int32), b)
+            best = L[0] if best is None or abs(L[0]) > abs(best) else best
+        ref.append(best)
+    np.testing.assert_allclose(got, ref, rtol=1e-12)
+
+
+@pytest.mark.parametrize("M0,M1,shared,c", [(90, 110, 60, 3), (64, 64, 64, 3), (130, 70, 5, 2), (1, 3, 1, 3)])
+def test_mixed_membership_loci(gpu, M0, M1, shared, c):
+    """Union SNPs present in one study only, U not a multiple of 64, tiny loci."""
+    ld, z, _, _, u2l = synth.mixed_locus(M0, M1, shared, seed=M0 + M1)
+    seam = E.seam_from_arrays(ld, z, u2l, (5000, 9000), max_causal=c, sharing_param=0.5)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    assert_parity(pc.accum(), O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-9)
+
+
+@pytest.mark.parametrize("M,c", [(100, 3), (200, 2), (130, 3)])
+def test_synthetic_vs_oracle(gpu, M, c):
+    ld, z, _, _, u2l = synth.syn_v1(M)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=c, sharing_param=0.25)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    assert_parity(pc.accum(), O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-9)
+
+
+def test_exhaustive_c4_generic_levels(gpu):
+    """c = 4 is undefined behaviour in the reference (3-int thread buffers,
+    postcal.cpp:760-762); the engine's generic evaluator handles it exactly."""
+    seam, _ = loci.seam_for(loci.SMALL, c=4)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    assert_parity(pc.accum(), O.postcal(seam))
+
+
+def test_deterministic_and_reusable(gpu):
+    ld, z, _, _, u2l = synth.syn_v1(300)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    a = pc.accum()
+    pc.run_exhaustive()
+    b = pc.accum()
+    for f in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    assert a.total == b.total
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_shard_merge_equals_single(gpu, world):
+    """Config-shard + merge of partials (the multi-GPU exchange) reproduces the
+    single-device sweep exactly, on one device."""
+    import torch  # noqa: F401  (device buffers for the partial images)
+    ld, z, _, _, u2l = synth.mixed_locus(150, 170, 120, seed=11)
+    seam = E.seam_from_arrays(ld, z, u2l, (5000, 9000), max_causal=3, sharing_param=0.4)
+    ref = E.PostCal(seam)
+    ref.run_exhaustive()
+    r = ref.accum()
+    nb = ref.partials_bytes()
+    buf = torch.empty(nb * world, dtype=torch.uint8, device="cuda")
+    for k in range(world):
+        pc = E.PostCal(seam)
+        pc.set_shard(k, world)
+        pc.run_exhaustive()
+        pc.export_partials(buf.data_ptr() + k * nb)
+        pc.close()
+    torch.cuda.synchronize()
+    m = E.PostCal(seam)
+    m.merge_partials(buf.data_ptr(), world)
+    g = m.accum()
+    assert g.n_configs == r.n_configs
+    for f in ("post", "no_causal", "shared"):
+        d = np.abs(_sexp(getattr(g, f), g.total) - _sexp(getattr(r, f), r.total)).max()
+        assert d <= 1e-12, f
+    for f in ("shared_ll", "notshared_ll"):
+        np.testing.assert_allclose(getattr(g, f), getattr(r, f), rtol=1e-12)
+
+
+def test_full_size_properties(gpu):
+    """BASELINE config 4 size (M = 1000, c = 3, 4.49e9 configurations):
+    size-independent properties (the oracle would take hours here)."""
+    ld, z, _, _, u2l = synth.syn_v1(1000)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    a = pc.accum()
+    assert a.n_configs == 4_491_007_501 == seam.count_configs()
+    post, noc, sh = a.pips()
+    assert np.all(post >= 0) and np.all(post <= 1 + 1e-12)
+    # utils/get_global_pips.py:23,32-33: global = post0 + post1 - shared in [0, 1]
+    gpip = post[:1000] + post[1000:] - sh
+    assert np.all(gpip <= 1 + 1e-6) and np.all(gpip >= -1e-6)
+    # the planted shared causal SNP (M/4) dominates both studies
+    assert post[250] > 0.5 and post[1000 + 250] > 0.5 and sh[250] > 0.5
+    # every accumulator is below the normaliser
+    assert np.all(a.post <= a.total + 1e-9) and np.all(a.no_causal <= a.total + 1e-9)
+    # spot-check single patterns against the oracle's literal N x N formula
+    sets = np.array([[250, 251, 750], [0, 500, 999], [249, 250, 750]], dtype=np.int32)
+    scores = pc.eval_union_batch(sets)
+    xs = [[(p // 3 ** j) % 3 + 1 for j in range(3)] for p in range(27)]
+    bits = np.array([[[v & 1 for v in x], [(v >> 1) & 1 for v in x]] for x in xs], dtype=np.int32)
+    for i, s in enumerate(sets):
+        L, _ = O.eval_patterns(seam, np.repeat(s[None, :], 27, axis=0), bits, literal=True)
+        best = L[np.argmax(np.abs(L))]
+        assert abs(scores[i] - best) <= 1e-9 * abs(best)

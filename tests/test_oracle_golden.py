@@ -1,0 +1,71 @@
+"""The oracle (CPU restatement, oracle/) pinned against the reference's own
+golden vectors: /root/reference/tests/example/expected_* (copied to
+tests/golden/example/).  CPU only."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+
+import loci
+from oracle import oracle as O
+
+FILES = ("study0_post", "study1_post", "study0_set", "study1_set", "nocausal", "shared_pips")
+
+
+def _run_cli(tmp_path, args, src="example"):
+    d = tmp_path / src
+    shutil.copytree(os.path.join(loci.GOLDEN, src), d)
+    r = subprocess.run([O.CLI] + args, cwd=d, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return d
+
+
+def test_example_reproduces_reference_goldens(tmp_path):
+    # tests/example/run_example.sh:1 invocation
+    d = _run_cli(tmp_path, ["-c", "2", "-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "snp_map", "-n",
+                            "334324,6771", "-p", "0.25", "-o", "pipsort_results"])
+    for f in FILES:
+        got = open(d / f"pipsort_results_{f}.txt").read()
+        exp = open(d / f"expected_{f}.txt").read()
+        if f != "shared_pips":
+            assert got == exp, f
+        else:
+            # shared_ll / notshared_ll are updated without a lock in the reference
+            # (postcal.cpp:1012-1017): compare the PIP column exactly, LL columns numerically
+            g = [l.split("\t") for l in got.splitlines()[1:]]
+            e = [l.split("\t") for l in exp.splitlines()[1:]]
+            assert [x[:2] for x in g] == [x[:2] for x in e]
+            gl = np.array([[float(x[2]), float(x[3])] for x in g])
+            el = np.array([[float(x[2]), float(x[3])] for x in e])
+            bad = np.abs(gl - el) > 1e-6 * np.maximum(1.0, np.abs(el))
+            assert bad.any(axis=1).sum() <= 1
+    # _log.txt is appended, never overwritten (util.cpp:183-187)
+    assert len(open(d / "pipsort_results_log.txt").read().splitlines()) == 1
+
+
+def test_literal_nxn_equals_reduced_kxk():
+    """The k x k reduction used by the oracle equals the reference's N x N
+    Woodbury formulation (postcal.cpp:214-304) on the rank-deficient small locus."""
+    for c in (1, 2, 3):
+        seam, _ = loci.seam_for(loci.SMALL, c=c)
+        a = O.postcal(seam)
+        b = O.postcal(seam, literal=True)
+        for k in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+            np.testing.assert_allclose(a[k], b[k], rtol=1e-12, atol=1e-9)
+        assert abs(a["total"] - b["total"]) < 1e-9
+        assert a["n_configs"] == b["n_configs"]
+
+
+def test_configs_file_and_sss_paths():
+    seam, L = loci.seam_for(loci.CONFIGS)
+    rows = np.fromfile(os.path.join(L["dir"], "all_configs_int16"), dtype=np.int16).reshape(72, 5)
+    r = O.postcal(seam, "configs", rows)
+    assert r["n_configs"] == 72
+    pip = np.where(r["post"] == 0, 0.0, np.exp(np.minimum(r["post"] - r["total"], 0)))
+    assert np.all(pip <= 1 + 1e-12) and (r["post"] == 0).sum() == 4
+    seam, _ = loci.seam_for(loci.SMALL)
+    s = O.postcal(seam, "sss")
+    # the walk hits "no new configurations" after 2 iterations and the null
+    # configuration is accumulated twice (sss_postcal.cpp:202 then as a minus-neighbour)
+    assert s["n_configs"] == 25
