@@ -95,6 +95,11 @@ __global__ void k_bts(const double* __restrict__ B, const double* __restrict__ s
     if (threadIdx.x == 0) y[i] = acc;
 }
 
+__global__ void k_diag(const double* __restrict__ S, int M, double* __restrict__ d) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < M) d[i] = S[(size_t)i * M + i];
+}
+
 // scatter study-local Sigma~ into union coordinates
 __global__ void k_to_union(const double* __restrict__ S, int M, const int* __restrict__ u2l, int U, int ldg,
                            double* __restrict__ G) {
@@ -174,6 +179,8 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
         fc1 = forced[2 * set + 1];
     }
     double tot = 0, nc0 = 0, nc1 = 0, smin = 1e300, npatv = 0;
+    // noCausal[s] terms live on their own shifts (C_s empty => the other study is full)
+    const int Gnc0 = s_n[1][S1] + P.Ck[k], Gnc1 = s_n[0][S0] + P.Ck[k];
     double p0[PSX_KMAX], p1[PSX_KMAX], sh[PSX_KMAX], sl[PSX_KMAX], ns[PSX_KMAX];
     for (int j = 0; j < PSX_KMAX; j++) p0[j] = p1[j] = sh[j] = sl[j] = ns[j] = 0.0;
     for (int p = lane; p < npat; p += 64) {
@@ -194,8 +201,8 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
         double w = wll * P.pit[k][nsh];
         npatv += 1.0;
         tot += w;
-        if (c0 == 0) nc0 += w;
-        if (c1 == 0) nc1 += w;
+        if (c0 == 0) nc0 += ldexp(mup * P.pit[k][0], np - Gnc0);
+        if (c1 == 0) nc1 += ldexp(mup * P.pit[k][0], np - Gnc1);
         smin = fmin(smin, s_f[0][c0] + s_f[1][c1] + P.prior[k][nsh]);
         for (int j = 0; j < k; j++) {
             if (x[j] & 1) p0[j] += w;
@@ -221,9 +228,10 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
         ns[j] = wave_sum(ns[j]);
     }
     if (lane == 0) {
-        SetRec r;
+        SetRec r = psx::set_zero();
         r.m = GS;
-        r.pad = 0;
+        r.m0 = Gnc0;
+        r.m1 = Gnc1;
         r.tot = tot;
         r.nc0 = nc0;
         r.nc1 = nc1;
@@ -262,7 +270,7 @@ __global__ void k_merge_partials(const Acc5* __restrict__ parts, int U, int ldg,
         acc[u] = a;
     }
     if (u == 0) {
-        SetRec s = {0, 0, 0.0, 0.0, 0.0, 1e300, 0.0};
+        SetRec s = psx::set_zero();
         for (int r = 0; r < count; r++)
             psx::fold_set(s, *reinterpret_cast<const SetRec*>(parts + (size_t)r * stride + ldg));
         *sacc = s;
@@ -414,7 +422,7 @@ int eval_generic(psx_engine* e, const std::vector<int>& sets, int stride, size_t
         if (psx::launch_merge_members(e->dmrec, e->dcsr, e->dcsr + ptr.size(), e->dcsr + ptr.size() + idx.size(),
                                       (int)rows.size(), e->dacc, e->stream))
             return fail(PSX_EHIP, psx::sweep_error());
-        SetRec none = {0, 0, 0.0, 0.0, 0.0, 1e300, 0.0};
+        SetRec none = psx::set_zero();
         if (psx::launch_merge_sets(e->dsrec, (long)nsets, none, e->dsacc, e->stream))
             return fail(PSX_EHIP, psx::sweep_error());
     }
@@ -438,7 +446,10 @@ int fold_null(psx_engine* e, double count) {
     if (count <= 0) return 0;
     double h = e->L0 * PSX_LOG2E;
     double fl = std::floor(h);
-    SetRec x = {(int32_t)fl, 0, 0.0, 0.0, 0.0, e->L0, count};
+    SetRec x = psx::set_zero();
+    x.m = x.m0 = x.m1 = (int32_t)fl;
+    x.score = e->L0;
+    x.npat = count;
     double v = std::exp2(h - fl) * count;
     x.tot = x.nc0 = x.nc1 = v;
     if (psx::launch_merge_sets(nullptr, 0L, x, e->dsacc, e->stream)) return fail(PSX_EHIP, psx::sweep_error());
@@ -506,7 +517,7 @@ int run_level_generic(psx_engine* e, int k, double* kms) {
 
 int reset_acc(psx_engine* e) {
     HIPCHK(hipMemsetAsync(e->dacc, 0, sizeof(Acc5) * e->ldg, e->stream));
-    SetRec z = {0, 0, 0.0, 0.0, 0.0, 1e300, 0.0};
+    SetRec z = psx::set_zero();
     HIPCHK(hipMemcpyAsync(e->dsacc, &z, sizeof(SetRec), hipMemcpyHostToDevice, e->stream));
     return 0;
 }
@@ -641,9 +652,9 @@ int psx_create(const psx_problem* p, int device, psx_engine** out) {
                            e->U, e->ldg, e->dG[s]);
         if (hipGetLastError() != hipSuccess) { cleanup(); return bail(fail(PSX_EHIP, "setup kernel launch")); }
         std::vector<double> Sd((size_t)M), yl(M);
-        // diagonal of Sigma~ and y (small D2H copies)
-        for (int i = 0; i < M; i++)
-            hipMemcpyAsync(&Sd[i], dS + (size_t)i * M + i, sizeof(double), hipMemcpyDeviceToHost, e->stream);
+        // diagonal of Sigma~ (into the B staging buffer, no longer needed) and y
+        hipLaunchKernelGGL(k_diag, dim3((M + 255) / 256), dim3(256), 0, e->stream, dS, M, dB);
+        hipMemcpyAsync(Sd.data(), dB, M * sizeof(double), hipMemcpyDeviceToHost, e->stream);
         hipMemcpyAsync(yl.data(), dyl, M * sizeof(double), hipMemcpyDeviceToHost, e->stream);
         if (hipStreamSynchronize(e->stream) != hipSuccess) { cleanup(); return bail(fail(PSX_EHIP, "setup sync")); }
         for (int u = 0; u < e->ldg; u++) {
@@ -1004,8 +1015,8 @@ int psx_get_accum(psx_engine* e, psx_accum* out) {
         if (out->notshared_ll) out->notshared_ll[u] = logval(e, a[u].mN, a[u].nsll);
     }
     if (out->no_causal) {
-        out->no_causal[0] = logval(e, s.m, s.nc0);
-        out->no_causal[1] = logval(e, s.m, s.nc1);
+        out->no_causal[0] = logval(e, s.m0, s.nc0);
+        out->no_causal[1] = logval(e, s.m1, s.nc1);
     }
     out->total = logval(e, s.m, s.tot);
     out->n_configs = (uint64_t)(s.npat + 0.5);
@@ -1045,7 +1056,7 @@ int psx_fold_partials_host(const void* src, int32_t count, int64_t image_bytes, 
         for (int r = 0; r < count; r++) psx::fold_acc(a, parts[(size_t)r * n + u]);
         out[u] = a;
     }
-    SetRec s = {0, 0, 0.0, 0.0, 0.0, 1e300, 0.0};
+    SetRec s = psx::set_zero();
     for (int r = 0; r < count; r++) psx::fold_set(s, *reinterpret_cast<const SetRec*>(parts + (size_t)r * n + n - 1));
     std::memcpy(&out[n - 1], &s, sizeof(SetRec));
     std::memcpy(dst, out.data(), n * sizeof(Acc5));

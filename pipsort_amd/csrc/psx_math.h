@@ -43,15 +43,27 @@ struct Acc5 {
     double post0, post1, shared, sll, nsll;
 };
 
-// Per-set (or per-unit) scalar record: total and noCausal[0..1] share one shift.
+// Per-set (or per-unit) scalar record: total, noCausal[0], noCausal[1], each with
+// its own shift (noCausal[s] can sit thousands of nats below the total).
 struct SetRec {
-    int32_t m, pad;
+    int32_t m, m0, m1, pad;
     double tot, nc0, nc1;
     double score;  // min over patterns of L' (nats, K excluded) == SSS max|L| pattern
     double npat;   // configurations folded in (exact integer in a double)
 };
 
+static_assert(sizeof(Acc5) == 56 && sizeof(SetRec) == 56, "partial-image slot layout");
+
 __host__ __device__ inline int imax(int a, int b) { return a > b ? a : b; }
+
+__host__ __device__ inline SetRec set_zero() {
+    SetRec r;
+    r.m = r.m0 = r.m1 = r.pad = 0;
+    r.tot = r.nc0 = r.nc1 = 0.0;
+    r.score = 1e300;
+    r.npat = 0.0;
+    return r;
+}
 
 // fold (m2, s2[0..n)) into (m, s[0..n)) — shared shift within the group
 __host__ __device__ inline void fold_group(int32_t& m, double* s, int n, int32_t m2, const double* s2) {
@@ -86,10 +98,9 @@ __host__ __device__ inline void fold_acc(Acc5& a, const Acc5& b) {
 }
 
 __host__ __device__ inline void fold_set(SetRec& a, const SetRec& b) {
-    double sa[3] = {a.tot, a.nc0, a.nc1};
-    const double sb[3] = {b.tot, b.nc0, b.nc1};
-    fold_group(a.m, sa, 3, b.m, sb);
-    a.tot = sa[0]; a.nc0 = sa[1]; a.nc1 = sa[2];
+    fold1(a.m, a.tot, b.m, b.tot);
+    fold1(a.m0, a.nc0, b.m0, b.nc0);
+    fold1(a.m1, a.nc1, b.m1, b.nc1);
     a.score = fmin(a.score, b.score);
     a.npat += b.npat;
 }

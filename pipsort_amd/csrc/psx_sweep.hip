@@ -74,6 +74,8 @@ __device__ inline Acc5 shfl_acc5(const Acc5& a, int o) {
 __device__ inline SetRec shfl_set(const SetRec& a, int o) {
     SetRec b;
     b.m = __shfl_xor(a.m, o);
+    b.m0 = __shfl_xor(a.m0, o);
+    b.m1 = __shfl_xor(a.m1, o);
     b.pad = 0;
     b.tot = __shfl_xor(a.tot, o);
     b.nc0 = __shfl_xor(a.nc0, o);
@@ -137,8 +139,9 @@ __device__ __forceinline__ void fold_patterns(const double (&mu0)[1 << K], const
         const double w = wll * A.pit[nsh];
         tot += w;
         npat += valid ? 1.0 : 0.0;
-        if (c0 == 0) nc0 += w;
-        if (c1 == 0) nc1 += w;
+        // noCausal[s]: the single assignment with C_s empty, on its own shift
+        if (c0 == 0) nc0 = valid ? mu1[c1] * A.pit[0] : 0.0;
+        if (c1 == 0) nc1 = valid ? mu0[c0] * A.pit[0] : 0.0;
 #pragma unroll
         for (int j = 0; j < K; j++) {
             if (x[j] & 1) p0[j] += w;
@@ -164,6 +167,8 @@ __device__ __forceinline__ void fold_patterns(const double (&mu0)[1 << K], const
         mem[j].nsll = ns[j];
     }
     sr.m = GS;
+    sr.m0 = n1[FULL] + A.Ck;  // C0 empty => C1 = FULL: 2^{n1[FULL]} mu1[FULL] 2^{prior}
+    sr.m1 = n0[FULL] + A.Ck;
     sr.pad = 0;
     sr.tot = tot;
     sr.nc0 = nc0;
@@ -190,8 +195,7 @@ __global__ __launch_bounds__(64) void k_sweep(TileArgs A, const int4* __restrict
     const int ldg = A.ldg;
     slot[t] = acc_zero();
     Acc5 accb = acc_zero();
-    SetRec accs;
-    accs.m = 0; accs.pad = 0; accs.tot = accs.nc0 = accs.nc1 = 0.0; accs.score = 1e300; accs.npat = 0.0;
+    SetRec accs = set_zero();
     const unsigned pb = bvalid ? A.pres[b] : 0u;
     double Abb[2], yb[2], iAbb[2], qb[2], Pb[2];
 #pragma unroll
@@ -358,8 +362,7 @@ __global__ __launch_bounds__(64) void k_merge_members(const Acc5* __restrict__ r
 __global__ __launch_bounds__(256) void k_merge_sets(const SetRec* __restrict__ rec, long n, SetRec extra,
                                                     SetRec* __restrict__ acc) {
     __shared__ SetRec sh[256];
-    SetRec a;
-    a.m = 0; a.pad = 0; a.tot = a.nc0 = a.nc1 = 0.0; a.score = 1e300; a.npat = 0.0;
+    SetRec a = set_zero();
     for (long i = threadIdx.x; i < n; i += 256) fold_set(a, rec[i]);
     sh[threadIdx.x] = a;
     __syncthreads();
@@ -626,8 +629,7 @@ int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, h
     const int* idx = P.d_csr + P.csr_ptr_len;
     const int* rows = P.d_csr + P.csr_ptr_len + P.csr_idx_len;
     if (launch_merge_members(P.d_rec, ptr, idx, rows, P.n_rows, acc, st)) return -1;
-    SetRec none;
-    none.m = 0; none.pad = 0; none.tot = none.nc0 = none.nc1 = 0.0; none.score = 1e300; none.npat = 0.0;
+    SetRec none = set_zero();
     if (launch_merge_sets(P.d_srec, P.n_units, none, sacc, st)) return -1;
     SWCHK(hipEventRecord(C.ev[2], st));
     SWCHK(hipEventSynchronize(C.ev[2]));

@@ -266,8 +266,8 @@ def fold_partials_host(images: np.ndarray) -> np.ndarray:
 # partial image record layout (psx_math.h Acc5 / SetRec)
 ACC5_DTYPE = np.dtype([("mP", "<i4"), ("mS", "<i4"), ("mN", "<i4"), ("pad", "<i4"), ("post0", "<f8"),
                        ("post1", "<f8"), ("shared", "<f8"), ("sll", "<f8"), ("nsll", "<f8")])
-SETREC_DTYPE = np.dtype([("m", "<i4"), ("pad", "<i4"), ("tot", "<f8"), ("nc0", "<f8"), ("nc1", "<f8"),
-                         ("score", "<f8"), ("npat", "<f8")])
+SETREC_DTYPE = np.dtype([("m", "<i4"), ("m0", "<i4"), ("m1", "<i4"), ("pad", "<i4"), ("tot", "<f8"),
+                         ("nc0", "<f8"), ("nc1", "<f8"), ("score", "<f8"), ("npat", "<f8")])
 
 
 @dataclass

@@ -91,9 +91,10 @@ def test_partial_fold_is_associative_and_order_fixed():
         for f in ("post0", "post1", "shared", "sll", "nsll"):
             a[f] = rng.random(ldg + 1) * (rng.random(ldg + 1) > 0.2)
         s = np.zeros(1, dtype=E.SETREC_DTYPE)
-        s["m"], s["tot"], s["nc0"], s["nc1"], s["score"], s["npat"] = rng.integers(-50, 50), 1.5, 0.5, 0.25, -3.0, 7
+        s["m"], s["m0"], s["m1"] = rng.integers(-50, 50), -70, 3
+        s["tot"], s["nc0"], s["nc1"], s["score"], s["npat"] = 1.5, 0.5, 0.25, -3.0, 7
         raw = a.tobytes()
-        raw = raw[: ldg * 56] + s.tobytes() + b"\0" * (56 - s.itemsize)
+        raw = raw[: ldg * 56] + s.tobytes()
         imgs.append(np.frombuffer(raw, dtype=np.uint8))
     imgs = np.stack(imgs)
     full = E.fold_partials_host(imgs)
@@ -105,5 +106,5 @@ def test_partial_fold_is_associative_and_order_fixed():
         return np.where(x[s] > 0, x[m] + np.log2(np.where(x[s] > 0, x[s], 1)), -np.inf)
     for m, s in (("mP", "post0"), ("mP", "post1"), ("mS", "sll"), ("mN", "nsll")):
         np.testing.assert_allclose(val(A, m, s), val(B, m, s), rtol=0, atol=1e-12)
-    sa = np.frombuffer(full[ldg * 56: ldg * 56 + 48].tobytes(), dtype=E.SETREC_DTYPE)[0]
+    sa = np.frombuffer(full[ldg * 56: ldg * 56 + 56].tobytes(), dtype=E.SETREC_DTYPE)[0]
     assert sa["npat"] == 28 and sa["score"] == -3.0

@@ -33,7 +33,8 @@ def _image(rank, ldg=256):
         a[f] = rng.random(ldg + 1) * (rng.random(ldg + 1) > 0.3)
     raw = bytearray(a.tobytes())
     s = np.zeros(1, dtype=E.SETREC_DTYPE)
-    s["m"], s["tot"], s["nc0"], s["nc1"], s["score"], s["npat"] = rank * 3, 1.0 + rank, 0.5, 0.25, -rank, 10 + rank
+    s["m"], s["m0"], s["m1"] = rank * 3, -rank, 2 * rank
+    s["tot"], s["nc0"], s["nc1"], s["score"], s["npat"] = 1.0 + rank, 0.5, 0.25, -rank, 10 + rank
     raw[ldg * 56: ldg * 56 + s.itemsize] = s.tobytes()
     return np.frombuffer(bytes(raw), dtype=np.uint8)
 

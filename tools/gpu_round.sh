@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-r01}
 mkdir -p $OUT
-timeout -k 10 1200 python -m pytest tests -m gpu -q -x -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 1200 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> $OUT/pytest_gpu.log
 if [ $rc -gt 1 ]; then exit $rc; fi
