@@ -35,6 +35,7 @@ struct SweepStats {           // indexed by causal-set level k
     double alg_bytes[8];      // 8 * sum_s (|C_s|^2 + |C_s|) over configurations
     double flops[8];          // FP64 operation estimate
     double merge_ms;          // device time of the record merges (all levels)
+    int exact_reruns;         // levels re-swept with the exact notSharedLL variant
 };
 
 // One decomposition of a level into wave units, with its record CSR.
@@ -53,9 +54,12 @@ struct SweepPlan {
 struct SweepPlanCache {
     std::map<std::tuple<int, int, int, int>, SweepPlan> plans;  // (k, U, rank, world)
     double* d_skew[2] = {nullptr, nullptr};  // skewed Sigma~ tiles (B <= T)
+    double* d_muS[2] = {nullptr, nullptr};   // singleton subset weights
+    int* d_nS[2] = {nullptr, nullptr};
     int skew_ldg = 0;
     const double* skew_src[2] = {nullptr, nullptr};
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    int* d_flag = nullptr;
 };
 
 bool sweep_supports(int k, int U);

@@ -44,15 +44,20 @@ struct TileArgs {
     const double* Ad[2];
     const double* y[2];
     const double* skew[2];
+    const double* muS[2];  // singleton weights {c}: mu of 2^{h_c} (d A_cc)^{-1/2}
+    const int* nS[2];      // and its integer exponent floor(h_c)
     const unsigned char* pres;
-    double d[2];
+    double d[2], rsd[2];   // d_s and d_s^{-1/2}
     int U, ldg, Ck;
     double pit[4];
 };
 
+constexpr int EMPTY = -(1 << 28);  // shift of an empty accumulator (value 0)
+
 __device__ inline Acc5 acc_zero() {
     Acc5 a;
-    a.mP = a.mS = a.mN = a.pad = 0;
+    a.mP = a.mS = a.mN = EMPTY;
+    a.pad = 0;
     a.post0 = a.post1 = a.shared = a.sll = a.nsll = 0.0;
     return a;
 }
@@ -98,93 +103,187 @@ __device__ inline void wave_fold_set(SetRec& a) {
     }
 }
 
-// Fold the 3^K study assignments of one union set given per-study subset
-// weights (mu, n) indexed by member bitmask; member j has bit (1 << j).
-// Outputs per-member Acc5 contributions and the set's scalar record.
-template <int K>
-__device__ __forceinline__ void fold_patterns(const double (&mu0)[1 << K], const int (&n0)[1 << K],
-                                              const double (&mu1)[1 << K], const int (&n1)[1 << K], int Sm0,
-                                              int Sm1, const TileArgs& A, Acc5 (&mem)[K], SetRec& sr) {
+// Branch-free folds for the hot loop.  Empty accumulators and empty
+// contributions carry shift EMPTY, so max() never lets a zero raise a shift.
+__device__ __forceinline__ void ffold1(int32_t& m, double& s, int32_t m2, double s2) {
+    const int M = max(m, m2);
+    s = ldexp(s, m - M) + ldexp(s2, m2 - M);
+    m = M;
+}
+__device__ __forceinline__ void ffold_acc(Acc5& a, const Acc5& b) {
+    const int M = max(a.mP, b.mP);
+    a.post0 = ldexp(a.post0, a.mP - M) + ldexp(b.post0, b.mP - M);
+    a.post1 = ldexp(a.post1, a.mP - M) + ldexp(b.post1, b.mP - M);
+    a.shared = ldexp(a.shared, a.mP - M) + ldexp(b.shared, b.mP - M);
+    a.mP = M;
+    ffold1(a.mS, a.sll, b.mS, b.sll);
+    ffold1(a.mN, a.nsll, b.mN, b.nsll);
+}
+__device__ __forceinline__ int nz_shift(int m, double s) { return s != 0.0 ? m : EMPTY; }
+
+// 1/sqrt(x) to full double precision: v_rsq_f64 + two Newton steps
+__device__ __forceinline__ double rsqrt_nr(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    double e = fma(-x * y, y, 1.0);
+    y = fma(0.5 * y, e, y);
+    e = fma(-x * y, y, 1.0);
+    return fma(0.5 * y, e, y);
+}
+
+// 2^f for f in [0, 1): sqrt(2) e^t, t = (f - 1/2) ln 2, degree-12 Taylor (|err| < 2e-16)
+__device__ __forceinline__ double exp2_frac(double f) {
+    const double t = (f - 0.5) * PSX_LN2;
+    double p = 2.08767569878680989792e-09;      // 1/12!
+    p = fma(p, t, 2.50521083854417187751e-08);  // 1/11!
+    p = fma(p, t, 2.75573192239858906526e-07);  // 1/10!
+    p = fma(p, t, 2.75573192239858906526e-06);  // 1/9!
+    p = fma(p, t, 2.48015873015873015873e-05);  // 1/8!
+    p = fma(p, t, 1.98412698412698412698e-04);  // 1/7!
+    p = fma(p, t, 1.38888888888888888889e-03);  // 1/6!
+    p = fma(p, t, 8.33333333333333333333e-03);  // 1/5!
+    p = fma(p, t, 4.16666666666666666667e-02);  // 1/4!
+    p = fma(p, t, 1.66666666666666666667e-01);  // 1/3!
+    p = fma(p, t, 0.5);
+    p = fma(p, t, 1.0);
+    p = fma(p, t, 1.0);
+    return p * 1.41421356237309504880;
+}
+
+// weight 2^h * rP as (n, mu), n = floor(h), mu in (0, 2)
+__device__ __forceinline__ void split2(double h, double rP, int& n, double& mu) {
+    const double fl = floor(h);
+    n = (int)fl;
+    mu = exp2_frac(h - fl) * rP;
+}
+
+// One union set: per-study subset weights (n, mu) for the 2^K subsets (bit j =
+// member j), zero-weighted where a member is absent from the study.  Folds the
+// 3^K assignments (postcal.cpp:907-1030) into per-member records and the set's
+// scalar record.
+//
+// notSharedLL (member j unshared) sums over assignment groups whose maximum sits
+// Gll - GN_j bits below the set maximum.  The fast variant rescales the group
+// sum by that gap (exact while the gap is <= 900 bits, i.e. unless j's
+// quadratic gain exceeds ~900 bits in both studies) and raises *flag otherwise;
+// the host then reruns the level with EXACT = true, which rescales each group's
+// subset weights to the group's own maximum.
+template <int K, bool EXACT>
+__device__ __forceinline__ void fold_set_patterns(const TileArgs& A, const int (&nn)[2][1 << K],
+                                                  const double (&mu)[2][1 << K], int Sm0, int Sm1,
+                                                  double wcount, int* flag, Acc5 (&out)[K], SetRec& sr) {
     constexpr int NS = 1 << K;
     constexpr int FULL = NS - 1;
-    constexpr int NP = (K == 1) ? 3 : (K == 2) ? 9 : 27;
-    const int Gll = n0[FULL] + n1[FULL] + 2;
-    int GN[K];
+    constexpr int NP = (K == 2) ? 9 : 27;
+    // pre-scale each study to its own top exponent (exact powers of two)
+    const int nb0 = nn[0][FULL], nb1 = nn[1][FULL];
+    double E0[NS], E1[NS];
 #pragma unroll
-    for (int j = 0; j < K; j++) {
-        const int bj = 1 << j;
-        GN[j] = imax(n0[FULL] + n1[FULL ^ bj], n0[FULL ^ bj] + n1[FULL]) + 2;
+    for (int T = 0; T < NS; T++) {
+        E0[T] = ((T & ~Sm0) == 0) ? ldexp(mu[0][T], nn[0][T] - nb0) : 0.0;
+        E1[T] = ((T & ~Sm1) == 0) ? ldexp(mu[1][T], nn[1][T] - nb1) : 0.0;
     }
-    const int GS = Gll + A.Ck;
-    double tot = 0, nc0 = 0, nc1 = 0, npat = 0;
-    double p0[K], p1[K], sh[K], sl[K], ns[K];
+    const int Gll = nb0 + nb1;  // E0 E1 < 4: values stay below 2^2 relative to Gll
+    double Sw[K][3], Sl[K][3];
 #pragma unroll
-    for (int j = 0; j < K; j++) p0[j] = p1[j] = sh[j] = sl[j] = ns[j] = 0.0;
+    for (int j = 0; j < K; j++)
+#pragma unroll
+        for (int x = 0; x < 3; x++) Sw[j][x] = Sl[j][x] = 0.0;
 #pragma unroll
     for (int p = 0; p < NP; p++) {
         int c0 = 0, c1 = 0, nsh = 0, r = p;
         int x[K];
 #pragma unroll
         for (int j = 0; j < K; j++) {
-            x[j] = r % 3 + 1;
+            x[j] = r % 3;  // 0: study0 only, 1: study1 only, 2: both
             r /= 3;
-            if (x[j] & 1) c0 |= 1 << j;
-            if (x[j] & 2) c1 |= 1 << j;
-            if (x[j] == 3) nsh++;
+            if (x[j] != 1) c0 |= 1 << j;
+            if (x[j] != 0) c1 |= 1 << j;
+            if (x[j] == 2) nsh++;
         }
-        const bool valid = ((c0 & ~Sm0) == 0) && ((c1 & ~Sm1) == 0);
-        const double mup = mu0[c0] * mu1[c1];
-        const int np = n0[c0] + n1[c1];
-        const double wll = valid ? ldexp(mup, np - Gll) : 0.0;
+        const double wll = E0[c0] * E1[c1];
         const double w = wll * A.pit[nsh];
-        tot += w;
-        npat += valid ? 1.0 : 0.0;
-        // noCausal[s]: the single assignment with C_s empty, on its own shift
-        if (c0 == 0) nc0 = valid ? mu1[c1] * A.pit[0] : 0.0;
-        if (c1 == 0) nc1 = valid ? mu0[c0] * A.pit[0] : 0.0;
 #pragma unroll
         for (int j = 0; j < K; j++) {
-            if (x[j] & 1) p0[j] += w;
-            if (x[j] & 2) p1[j] += w;
-            if (x[j] == 3) {
-                sh[j] += w;
-                sl[j] += wll;
-            } else {
-                ns[j] += valid ? ldexp(mup, np - GN[j]) : 0.0;
-            }
+            Sw[j][x[j]] += w;
+            Sl[j][x[j]] += wll;
         }
     }
+    // notSharedLL groups: member j unshared, max pattern 2^{GN_j - 2}
+    int GN[K], dmax = 0;
 #pragma unroll
     for (int j = 0; j < K; j++) {
-        mem[j].mP = GS;
-        mem[j].mS = Gll;
-        mem[j].mN = GN[j];
-        mem[j].pad = 0;
-        mem[j].post0 = p0[j];
-        mem[j].post1 = p1[j];
-        mem[j].shared = sh[j];
-        mem[j].sll = sl[j];
-        mem[j].nsll = ns[j];
+        const int bj = 1 << j;
+        GN[j] = max(nb0 + nn[1][FULL ^ bj], nn[0][FULL ^ bj] + nb1);
+        dmax = max(dmax, Gll - GN[j]);
     }
-    sr.m = GS;
-    sr.m0 = n1[FULL] + A.Ck;  // C0 empty => C1 = FULL: 2^{n1[FULL]} mu1[FULL] 2^{prior}
-    sr.m1 = n0[FULL] + A.Ck;
+    double ns[K];
+    if (!EXACT) {
+        if (dmax > 900) atomicOr(flag, 1);
+#pragma unroll
+        for (int j = 0; j < K; j++) ns[j] = ldexp(Sl[j][0] + Sl[j][1], Gll - GN[j]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const int bj = 1 << j;
+            // group x_j = study0 only: C0 contains j, C1 within FULL ^ bj
+            const int g1 = nb0 + nn[1][FULL ^ bj];
+            // group x_j = study1 only: C1 contains j, C0 within FULL ^ bj
+            const int g2 = nn[0][FULL ^ bj] + nb1;
+            double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                int c0 = 0, c1 = 0, r = p, xj = 0;
+#pragma unroll
+                for (int i = 0; i < K; i++) {
+                    const int xi = r % 3;
+                    r /= 3;
+                    if (xi != 1) c0 |= 1 << i;
+                    if (xi != 0) c1 |= 1 << i;
+                    if (i == j) xj = xi;
+                }
+                if (xj == 2) continue;
+                const bool ok = ((c0 & ~Sm0) == 0) && ((c1 & ~Sm1) == 0);
+                const double m = ok ? mu[0][c0] * mu[1][c1] : 0.0;
+                if (xj == 0) s1 += ldexp(m, nn[0][c0] + nn[1][c1] - g1);
+                else s2 += ldexp(m, nn[0][c0] + nn[1][c1] - g2);
+            }
+            const int G = max(s1 != 0.0 ? g1 : EMPTY, s2 != 0.0 ? g2 : EMPTY);
+            ns[j] = ldexp(s1, g1 - G) + ldexp(s2, g2 - G);
+            GN[j] = G;
+        }
+    }
+    const int GS = Gll + A.Ck;
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+        out[j].post0 = Sw[j][0] + Sw[j][2];
+        out[j].post1 = Sw[j][1] + Sw[j][2];
+        out[j].shared = Sw[j][2];
+        out[j].mP = nz_shift(GS, out[j].post0 + out[j].post1);
+        out[j].sll = Sl[j][2];
+        out[j].mS = nz_shift(Gll, out[j].sll);
+        out[j].nsll = ns[j];
+        out[j].mN = nz_shift(GN[j], ns[j]);
+        out[j].pad = 0;
+    }
+    sr.tot = Sw[0][0] + Sw[0][1] + Sw[0][2];
+    sr.m = nz_shift(GS, sr.tot);
+    // noCausal[s]: the assignment with C_s empty (all members in the other study)
+    sr.nc0 = E1[FULL] * A.pit[0];
+    sr.m0 = nz_shift(nb1 + A.Ck, sr.nc0);
+    sr.nc1 = E0[FULL] * A.pit[0];
+    sr.m1 = nz_shift(nb0 + A.Ck, sr.nc1);
     sr.pad = 0;
-    sr.tot = tot;
-    sr.nc0 = nc0;
-    sr.nc1 = nc1;
     sr.score = 1e300;
-    sr.npat = npat;
+    sr.npat = wcount;
 }
 
-__device__ __forceinline__ void split(double q, double P, int& n, double& mu) {
-    split_exp(0.5 * q * PSX_LOG2E, 1.0 / sqrt(P), n, mu);
-}
+__device__ __forceinline__ double memb_weight(unsigned p) { return p == 3u ? 3.0 : (p ? 1.0 : 0.0); }
 
-template <int K>
-__global__ __launch_bounds__(64) void k_sweep(TileArgs A, const int4* __restrict__ units, Acc5* __restrict__ rec,
-                                              SetRec* __restrict__ srec, int rec_stride) {
-    __shared__ Acc5 slot[64];
+template <int K, bool EXACT>
+__global__ __launch_bounds__(64, (K == 3 ? 2 : 4)) void k_sweep(TileArgs A, const int4* __restrict__ units, Acc5* __restrict__ rec,
+                                              SetRec* __restrict__ srec, int rec_stride, int* __restrict__ flag) {
+    __shared__ Acc5 slot[64];   // c accumulators, ownership rotates every step
+    __shared__ Acc5 sacc[2][64]; // [0] a, [1] b accumulators, lane-owned
     const int unit = blockIdx.x;
     const int t = threadIdx.x;
     const int4 un = units[unit];
@@ -194,60 +293,60 @@ __global__ __launch_bounds__(64) void k_sweep(TileArgs A, const int4* __restrict
     const int tile = T * (T + 1) / 2 + B;
     const int ldg = A.ldg;
     slot[t] = acc_zero();
-    Acc5 accb = acc_zero();
+    sacc[1][t] = acc_zero();
     SetRec accs = set_zero();
+    accs.m = accs.m0 = accs.m1 = EMPTY;
     const unsigned pb = bvalid ? A.pres[b] : 0u;
-    double Abb[2], yb[2], iAbb[2], qb[2], Pb[2];
+    // per-lane b terms
+    double Abb[2], yb[2], iAbb[2], qb[2], rPb[2];
 #pragma unroll
     for (int s = 0; s < 2; s++) {
         Abb[s] = A.Ad[s][b];
         yb[s] = A.y[s][b];
-        iAbb[s] = 1.0 / Abb[s];
+        const double r = rsqrt_nr(Abb[s]);
+        iAbb[s] = r * r;
         qb[s] = yb[s] * yb[s] * iAbb[s];
-        Pb[s] = A.d[s] * Abb[s];
+        rPb[s] = r * A.rsd[s];
     }
     const int na = (K == 3) ? (a1 - a0) : 1;
     for (int ai = 0; ai < na; ai++) {
         const int a = a0 + ai;
-        Acc5 acca = acc_zero();
-        // ---- (a, b) prefix, per study -------------------------------------------------
-        double iAaa[2], ya[2], Gab[2], qa[2], Pa[2], Dab[2], iDab[2], wab[2], qab[2], Pab[2];
-        unsigned pa = 0;
-        if (K == 3) {
-            pa = A.pres[a];
-#pragma unroll
-            for (int s = 0; s < 2; s++) {
-                const double Aaa = A.Ad[s][a];
-                iAaa[s] = 1.0 / Aaa;
-                ya[s] = A.y[s][a];
-                Gab[s] = A.G[s][(size_t)a * ldg + b];
-                qa[s] = ya[s] * ya[s] * iAaa[s];
-                Pa[s] = A.d[s] * Aaa;
-                const double l = Gab[s] * iAaa[s];
-                Dab[s] = Abb[s] - l * Gab[s];
-                iDab[s] = 1.0 / Dab[s];
-                wab[s] = yb[s] - l * ya[s];
-                qab[s] = qa[s] + wab[s] * wab[s] * iDab[s];
-                Pab[s] = Pa[s] * A.d[s] * Dab[s];
-            }
-        }
-        // subset weights not involving c (hoisted out of the c loop)
+        sacc[0][t] = acc_zero();
         constexpr int NS = 1 << K;
         double mu[2][NS];
         int nn[2][NS];
+        // ---- hoisted prefix: subsets without c ------------------------------------------
+        double iAaa[2], ya[2], Gab[2], qa[2], rPa[2], Dab[2], iDab[2], wab[2], qab[2], rPab[2];
+        unsigned pa = 0;
 #pragma unroll
         for (int s = 0; s < 2; s++) {
             mu[s][0] = 1.0;
             nn[s][0] = 0;
             if (K == 3) {
-                split(qa[s], Pa[s], nn[s][1], mu[s][1]);   // {a}
-                split(qb[s], Pb[s], nn[s][2], mu[s][2]);   // {b}
-                split(qab[s], Pab[s], nn[s][3], mu[s][3]); // {a,b}
+                const double Aaa = A.Ad[s][a];
+                const double ra = rsqrt_nr(Aaa);
+                iAaa[s] = ra * ra;
+                ya[s] = A.y[s][a];
+                Gab[s] = A.G[s][(size_t)a * ldg + b];
+                qa[s] = ya[s] * ya[s] * iAaa[s];
+                rPa[s] = ra * A.rsd[s];
+                const double l = Gab[s] * iAaa[s];
+                Dab[s] = Abb[s] - l * Gab[s];
+                const double rab = rsqrt_nr(Dab[s]);
+                iDab[s] = rab * rab;
+                wab[s] = yb[s] - l * ya[s];
+                qab[s] = qa[s] + wab[s] * wab[s] * iDab[s];
+                rPab[s] = rPa[s] * rab * A.rsd[s];
+                split2(0.5 * qa[s] * PSX_LOG2E, rPa[s], nn[s][1], mu[s][1]);     // {a}
+                split2(0.5 * qb[s] * PSX_LOG2E, rPb[s], nn[s][2], mu[s][2]);     // {b}
+                split2(0.5 * qab[s] * PSX_LOG2E, rPab[s], nn[s][3], mu[s][3]);   // {a,b}
             } else {
-                split(qb[s], Pb[s], nn[s][1], mu[s][1]);   // {b}
+                split2(0.5 * qb[s] * PSX_LOG2E, rPb[s], nn[s][1], mu[s][1]);     // {b}
             }
         }
+        if (K == 3) pa = A.pres[a];
         const bool abvalid = bvalid && (K == 2 || a < b);
+        const double wab_cnt = memb_weight(pb) * (K == 3 ? memb_weight(pa) : 1.0);
         for (int j = 0; j < 64; j++) {
             const int cc = (t + j) & 63;
             const int c = 64 * T + cc;
@@ -259,33 +358,32 @@ __global__ __launch_bounds__(64) void k_sweep(TileArgs A, const int4* __restrict
                     const double Acc_ = A.Ad[s][c];
                     const double yc = A.y[s][c];
                     const double Gbc = A.skew[s][(size_t)tile * 4096 + j * 64 + t];
-                    const double ds = A.d[s];
-                    // {c}
-                    const double qc = yc * yc / Acc_;
+                    constexpr int IC = (K == 3) ? 4 : 2, IBC = (K == 3) ? 6 : 3;
+                    mu[s][IC] = A.muS[s][c];  // {c}: precomputed per SNP
+                    nn[s][IC] = A.nS[s][c];
                     // {b, c}
                     const double l2 = Gbc * iAbb[s];
                     const double D2 = Acc_ - l2 * Gbc;
                     const double w2 = yc - l2 * yb[s];
-                    const double qbc = qb[s] + w2 * w2 / D2;
+                    const double r2 = rsqrt_nr(D2);
+                    const double t2 = w2 * r2;
+                    split2(0.5 * (qb[s] + t2 * t2) * PSX_LOG2E, rPb[s] * r2 * A.rsd[s], nn[s][IBC], mu[s][IBC]);
                     if (K == 3) {
                         const double Gac = A.G[s][(size_t)a * ldg + c];
                         // {a, c}
                         const double l1 = Gac * iAaa[s];
                         const double D1 = Acc_ - l1 * Gac;
                         const double w1 = yc - l1 * ya[s];
-                        const double qac = qa[s] + w1 * w1 / D1;
+                        const double r1 = rsqrt_nr(D1);
+                        const double t1 = w1 * r1;
+                        split2(0.5 * (qa[s] + t1 * t1) * PSX_LOG2E, rPa[s] * r1 * A.rsd[s], nn[s][5], mu[s][5]);
                         // {a, b, c}: extend the (a, b) factor by the c row
                         const double lcb = (Gbc - l1 * Gab[s]) * iDab[s];
                         const double D3 = D1 - lcb * lcb * Dab[s];
                         const double w3 = w1 - lcb * wab[s];
-                        const double qabc = qab[s] + w3 * w3 / D3;
-                        split(qc, ds * Acc_, nn[s][4], mu[s][4]);
-                        split(qac, Pa[s] * ds * D1, nn[s][5], mu[s][5]);
-                        split(qbc, Pb[s] * ds * D2, nn[s][6], mu[s][6]);
-                        split(qabc, Pab[s] * ds * D3, nn[s][7], mu[s][7]);
-                    } else {
-                        split(qc, ds * Acc_, nn[s][2], mu[s][2]);
-                        split(qbc, Pb[s] * ds * D2, nn[s][3], mu[s][3]);
+                        const double r3 = rsqrt_nr(D3);
+                        const double t3 = w3 * r3;
+                        split2(0.5 * (qab[s] + t3 * t3) * PSX_LOG2E, rPab[s] * r3 * A.rsd[s], nn[s][7], mu[s][7]);
                     }
                 }
                 int Sm0, Sm1;
@@ -296,35 +394,54 @@ __global__ __launch_bounds__(64) void k_sweep(TileArgs A, const int4* __restrict
                     Sm0 = (pb & 1) | ((pc & 1) << 1);
                     Sm1 = ((pb >> 1) & 1) | (((pc >> 1) & 1) << 1);
                 }
-                Acc5 mem[K];
+                Acc5 out[K];
                 SetRec sr;
-                fold_patterns<K>(mu[0], nn[0], mu[1], nn[1], Sm0, Sm1, A, mem, sr);
-                fold_set(accs, sr);
+                fold_set_patterns<K, EXACT>(A, nn, mu, Sm0, Sm1, wab_cnt * memb_weight(pc), flag, out, sr);
+                ffold1(accs.m, accs.tot, sr.m, sr.tot);
+                ffold1(accs.m0, accs.nc0, sr.m0, sr.nc0);
+                ffold1(accs.m1, accs.nc1, sr.m1, sr.nc1);
+                accs.npat += sr.npat;
                 if (K == 3) {
-                    fold_acc(acca, mem[0]);
-                    fold_acc(accb, mem[1]);
-                    Acc5 sl = slot[cc];
-                    fold_acc(sl, mem[2]);
-                    slot[cc] = sl;
-                } else {
-                    fold_acc(accb, mem[0]);
-                    Acc5 sl = slot[cc];
-                    fold_acc(sl, mem[1]);
-                    slot[cc] = sl;
+                    Acc5 x = sacc[0][t];
+                    ffold_acc(x, out[0]);
+                    sacc[0][t] = x;
                 }
+                {
+                    Acc5 x = sacc[1][t];
+                    ffold_acc(x, out[K - 2]);
+                    sacc[1][t] = x;
+                }
+                Acc5 sl = slot[cc];
+                ffold_acc(sl, out[K - 1]);
+                slot[cc] = sl;
             }
             __syncthreads();  // slot[] ownership rotates across lanes every step
         }
         if (K == 3) {
+            Acc5 acca = sacc[0][t];
             wave_fold_acc(acca);
             if (t == 0) rec[(size_t)unit * rec_stride + 128 + ai] = acca;
         }
     }
     __syncthreads();
     rec[(size_t)unit * rec_stride + t] = slot[t];
-    rec[(size_t)unit * rec_stride + 64 + t] = accb;
+    rec[(size_t)unit * rec_stride + 64 + t] = sacc[1][t];
     wave_fold_set(accs);
     if (t == 0) srec[unit] = accs;
+}
+
+// singleton subset weights per union SNP: h = y^2 / (2 A) log2(e), rP = (d A)^{-1/2}
+__global__ void k_build_singles(const double* __restrict__ Ad, const double* __restrict__ y, double rsd, int ldg,
+                                double* __restrict__ muS, int* __restrict__ nS) {
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= ldg) return;
+    const double r = rsqrt_nr(Ad[u]);
+    const double q = y[u] * y[u] * r * r;
+    int n;
+    double mu;
+    split2(0.5 * q * PSX_LOG2E, r * rsd, n, mu);
+    muS[u] = mu;
+    nS[u] = n;
 }
 
 // skew[tile(B,T)][j][t] = G[64B + t][64T + ((t + j) & 63)]  for B <= T
@@ -578,7 +695,18 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
 
 static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, hipStream_t st) {
     if (C.d_skew[0] && C.skew_ldg == ldg && C.skew_src[0] == a.G0 && C.skew_src[1] == a.G1) return 0;
-    for (int s = 0; s < 2; s++) { hipFree(C.d_skew[s]); C.d_skew[s] = nullptr; }
+    for (int s = 0; s < 2; s++) {
+        hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
+        hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
+        hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
+    }
+    for (int s = 0; s < 2; s++) {
+        SWCHK(hipMalloc(&C.d_muS[s], sizeof(double) * ldg));
+        SWCHK(hipMalloc(&C.d_nS[s], sizeof(int) * ldg));
+        hipLaunchKernelGGL(k_build_singles, dim3((ldg + 255) / 256), dim3(256), 0, st, s ? a.Ad1 : a.Ad0,
+                           s ? a.y1 : a.y0, 1.0 / std::sqrt(s ? a.d1 : a.d0), ldg, C.d_muS[s], C.d_nS[s]);
+        SWCHK(hipGetLastError());
+    }
     const int nblk = ldg / 64;
     const int ntile = nblk * (nblk + 1) / 2;
     for (int s = 0; s < 2; s++) {
@@ -614,17 +742,38 @@ int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, h
     A.y[0] = a.y0; A.y[1] = a.y1;
     A.skew[0] = C.d_skew[0]; A.skew[1] = C.d_skew[1];
     A.pres = a.pres;
+    A.muS[0] = C.d_muS[0]; A.muS[1] = C.d_muS[1];
+    A.nS[0] = C.d_nS[0]; A.nS[1] = C.d_nS[1];
     A.d[0] = a.d0; A.d[1] = a.d1;
+    A.rsd[0] = 1.0 / std::sqrt(a.d0); A.rsd[1] = 1.0 / std::sqrt(a.d1);
     A.U = U; A.ldg = ldg;
     A.Ck = a.Ck[k];
     for (int n = 0; n < 4; n++) A.pit[n] = (n <= k) ? a.pit[k * a.pit_ld + n] : 0.0;
+    if (!C.d_flag) SWCHK(hipMalloc(&C.d_flag, sizeof(int)));
+    SWCHK(hipMemsetAsync(C.d_flag, 0, sizeof(int), st));
     SWCHK(hipEventRecord(C.ev[0], st));
     if (k == 3)
-        hipLaunchKernelGGL(k_sweep<3>, dim3(P.n_units), dim3(64), 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride);
+        hipLaunchKernelGGL((k_sweep<3, false>), dim3(P.n_units), dim3(64), 0, st, A, P.d_units, P.d_rec, P.d_srec,
+                           P.rec_stride, C.d_flag);
     else
-        hipLaunchKernelGGL(k_sweep<2>, dim3(P.n_units), dim3(64), 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride);
+        hipLaunchKernelGGL((k_sweep<2, false>), dim3(P.n_units), dim3(64), 0, st, A, P.d_units, P.d_rec, P.d_srec,
+                           P.rec_stride, C.d_flag);
     SWCHK(hipGetLastError());
     SWCHK(hipEventRecord(C.ev[1], st));
+    int hflag = 0;
+    SWCHK(hipMemcpyAsync(&hflag, C.d_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    SWCHK(hipStreamSynchronize(st));
+    if (hflag) {  // a notSharedLL group gap beyond 900 bits: exact rerun of the level
+        if (k == 3)
+            hipLaunchKernelGGL((k_sweep<3, true>), dim3(P.n_units), dim3(64), 0, st, A, P.d_units, P.d_rec, P.d_srec,
+                               P.rec_stride, C.d_flag);
+        else
+            hipLaunchKernelGGL((k_sweep<2, true>), dim3(P.n_units), dim3(64), 0, st, A, P.d_units, P.d_rec, P.d_srec,
+                               P.rec_stride, C.d_flag);
+        SWCHK(hipGetLastError());
+        SWCHK(hipEventRecord(C.ev[1], st));
+        if (stats) stats->exact_reruns += 1;
+    }
     const int* ptr = P.d_csr;
     const int* idx = P.d_csr + P.csr_ptr_len;
     const int* rows = P.d_csr + P.csr_ptr_len + P.csr_idx_len;
@@ -653,8 +802,14 @@ void sweep_free(SweepPlanCache& C) {
         hipFree(P.d_units); hipFree(P.d_rec); hipFree(P.d_srec); hipFree(P.d_csr);
     }
     C.plans.clear();
-    for (int s = 0; s < 2; s++) { hipFree(C.d_skew[s]); C.d_skew[s] = nullptr; }
+    for (int s = 0; s < 2; s++) {
+        hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
+        hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
+        hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
+    }
     for (int i = 0; i < 4; i++) if (C.ev[i]) { hipEventDestroy(C.ev[i]); C.ev[i] = nullptr; }
+    hipFree(C.d_flag);
+    C.d_flag = nullptr;
 }
 
 }  // namespace psx
