@@ -73,6 +73,7 @@ typedef struct {
     uint64_t union_sets;    /* union subsets evaluated by the dominant kernel              */
     double alg_bytes;       /* algorithmic bytes of the dominant kernel      */
     double flops;           /* FP64 operation estimate of the dominant kernel              */
+    int32_t exact_rerun;    /* 1 if the sweep was redone with the exact notSharedLL variant */
 } psx_timing;
 
 int32_t psx_abi_version(void);

@@ -49,6 +49,8 @@ struct SweepPlan {
     SetRec* d_srec = nullptr;    // [n_units]
     int* d_csr = nullptr;        // ptr[n_rows+1], idx[...], row_snp[n_rows]
     int csr_ptr_len = 0, csr_idx_len = 0;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // kernel start/end, merges end
+    bool ran = false;
 };
 
 struct SweepPlanCache {
@@ -58,16 +60,18 @@ struct SweepPlanCache {
     int* d_nS[2] = {nullptr, nullptr};
     int skew_ldg = 0;
     const double* skew_src[2] = {nullptr, nullptr};
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    int* d_flag = nullptr;
+    int* d_flag = nullptr;  // raised when a set needs the EXACT notSharedLL variant
 };
 
 bool sweep_supports(int k, int U);
 struct PlanUnit { int a0, a1, B, T; double work; };
 int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* pres_host,
                std::vector<PlanUnit>& mine, int& ca, double& sets, double& configs, double& bytes);
+int sweep_begin(SweepPlanCache& cache, hipStream_t stream);   // zero the EXACT flag
 int sweep_level(SweepPlanCache& cache, int k, int U, int ldg, int rank, int world, hipStream_t stream,
-                const SweepArgs& a, Acc5* acc, SetRec* sacc, SweepStats* st);
+                const SweepArgs& a, Acc5* acc, SetRec* sacc, bool exact);   // async enqueue
+int sweep_flag(SweepPlanCache& cache, int* flag);                          // after sync
+int sweep_stats(SweepPlanCache& cache, int k, int U, int rank, int world, SweepStats* st);  // after sync
 void sweep_free(SweepPlanCache& cache);
 int launch_merge_members(const Acc5* rec, const int* ptr, const int* idx, const int* rows, int n_rows, Acc5* acc,
                          hipStream_t st);

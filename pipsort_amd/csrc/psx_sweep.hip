@@ -720,10 +720,21 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, hipStream
     return 0;
 }
 
+int sweep_begin(SweepPlanCache& C, hipStream_t st) {
+    if (!C.d_flag) SWCHK(hipMalloc(&C.d_flag, sizeof(int)));
+    SWCHK(hipMemsetAsync(C.d_flag, 0, sizeof(int), st));
+    return 0;
+}
+
+int sweep_flag(SweepPlanCache& C, int* flag) {
+    *flag = 0;
+    if (C.d_flag) SWCHK(hipMemcpy(flag, C.d_flag, sizeof(int), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+// Enqueue one level (kernel + record merges) on `st`; no host synchronisation.
 int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, hipStream_t st, const SweepArgs& a,
-                Acc5* acc, SetRec* sacc, SweepStats* stats) {
-    if (!C.ev[0])
-        for (int i = 0; i < 4; i++) SWCHK(hipEventCreate(&C.ev[i]));
+                Acc5* acc, SetRec* sacc, bool exact) {
     if (ensure_skew(C, a, ldg, st)) return -1;
     auto key = std::make_tuple(k, U, rank, world);
     auto it = C.plans.find(key);
@@ -732,9 +743,11 @@ int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, h
         SWCHK(hipMemcpy(pres.data(), a.pres, ldg, hipMemcpyDeviceToHost));
         SweepPlan P;
         if (build_plan(P, k, U, ldg, rank, world, pres.data())) return -1;
+        for (int i = 0; i < 3; i++) SWCHK(hipEventCreate(&P.ev[i]));
         it = C.plans.emplace(key, P).first;
     }
     SweepPlan& P = it->second;
+    P.ran = false;
     if (P.n_units == 0) return 0;
     TileArgs A;
     A.G[0] = a.G0; A.G[1] = a.G1;
@@ -749,50 +762,44 @@ int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, h
     A.U = U; A.ldg = ldg;
     A.Ck = a.Ck[k];
     for (int n = 0; n < 4; n++) A.pit[n] = (n <= k) ? a.pit[k * a.pit_ld + n] : 0.0;
-    if (!C.d_flag) SWCHK(hipMalloc(&C.d_flag, sizeof(int)));
-    SWCHK(hipMemsetAsync(C.d_flag, 0, sizeof(int), st));
-    SWCHK(hipEventRecord(C.ev[0], st));
-    if (k == 3)
-        hipLaunchKernelGGL((k_sweep<3, false>), dim3(P.n_units), dim3(64), 0, st, A, P.d_units, P.d_rec, P.d_srec,
-                           P.rec_stride, C.d_flag);
+    if (!C.d_flag && sweep_begin(C, st)) return -1;
+    SWCHK(hipEventRecord(P.ev[0], st));
+    const dim3 g(P.n_units), blk(64);
+    if (k == 3 && !exact)
+        hipLaunchKernelGGL((k_sweep<3, false>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag);
+    else if (k == 3)
+        hipLaunchKernelGGL((k_sweep<3, true>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag);
+    else if (!exact)
+        hipLaunchKernelGGL((k_sweep<2, false>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag);
     else
-        hipLaunchKernelGGL((k_sweep<2, false>), dim3(P.n_units), dim3(64), 0, st, A, P.d_units, P.d_rec, P.d_srec,
-                           P.rec_stride, C.d_flag);
+        hipLaunchKernelGGL((k_sweep<2, true>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag);
     SWCHK(hipGetLastError());
-    SWCHK(hipEventRecord(C.ev[1], st));
-    int hflag = 0;
-    SWCHK(hipMemcpyAsync(&hflag, C.d_flag, sizeof(int), hipMemcpyDeviceToHost, st));
-    SWCHK(hipStreamSynchronize(st));
-    if (hflag) {  // a notSharedLL group gap beyond 900 bits: exact rerun of the level
-        if (k == 3)
-            hipLaunchKernelGGL((k_sweep<3, true>), dim3(P.n_units), dim3(64), 0, st, A, P.d_units, P.d_rec, P.d_srec,
-                               P.rec_stride, C.d_flag);
-        else
-            hipLaunchKernelGGL((k_sweep<2, true>), dim3(P.n_units), dim3(64), 0, st, A, P.d_units, P.d_rec, P.d_srec,
-                               P.rec_stride, C.d_flag);
-        SWCHK(hipGetLastError());
-        SWCHK(hipEventRecord(C.ev[1], st));
-        if (stats) stats->exact_reruns += 1;
-    }
+    SWCHK(hipEventRecord(P.ev[1], st));
     const int* ptr = P.d_csr;
     const int* idx = P.d_csr + P.csr_ptr_len;
     const int* rows = P.d_csr + P.csr_ptr_len + P.csr_idx_len;
     if (launch_merge_members(P.d_rec, ptr, idx, rows, P.n_rows, acc, st)) return -1;
     SetRec none = set_zero();
     if (launch_merge_sets(P.d_srec, P.n_units, none, sacc, st)) return -1;
-    SWCHK(hipEventRecord(C.ev[2], st));
-    SWCHK(hipEventSynchronize(C.ev[2]));
+    SWCHK(hipEventRecord(P.ev[2], st));
+    P.ran = true;
+    return 0;
+}
+
+// After the stream has been synchronised: per-level statistics of the last run.
+int sweep_stats(SweepPlanCache& C, int k, int U, int rank, int world, SweepStats* stats) {
+    auto it = C.plans.find(std::make_tuple(k, U, rank, world));
+    if (it == C.plans.end() || !it->second.ran) return 0;
+    SweepPlan& P = it->second;
     float k_ms = 0, m_ms = 0;
-    SWCHK(hipEventElapsedTime(&k_ms, C.ev[0], C.ev[1]));
-    SWCHK(hipEventElapsedTime(&m_ms, C.ev[1], C.ev[2]));
-    if (stats) {
-        stats->kernel_ms[k] += k_ms;
-        stats->launches[k] += 1;
-        stats->union_sets[k] += P.union_sets;
-        stats->alg_bytes[k] += P.alg_bytes;
-        stats->flops[k] += P.flops;
-        stats->merge_ms += m_ms;
-    }
+    SWCHK(hipEventElapsedTime(&k_ms, P.ev[0], P.ev[1]));
+    SWCHK(hipEventElapsedTime(&m_ms, P.ev[1], P.ev[2]));
+    stats->kernel_ms[k] += k_ms;
+    stats->launches[k] += 1;
+    stats->union_sets[k] += P.union_sets;
+    stats->alg_bytes[k] += P.alg_bytes;
+    stats->flops[k] += P.flops;
+    stats->merge_ms += m_ms;
     return 0;
 }
 
@@ -800,6 +807,7 @@ void sweep_free(SweepPlanCache& C) {
     for (auto& kv : C.plans) {
         SweepPlan& P = kv.second;
         hipFree(P.d_units); hipFree(P.d_rec); hipFree(P.d_srec); hipFree(P.d_csr);
+        for (int i = 0; i < 3; i++) if (P.ev[i]) hipEventDestroy(P.ev[i]);
     }
     C.plans.clear();
     for (int s = 0; s < 2; s++) {
@@ -807,7 +815,6 @@ void sweep_free(SweepPlanCache& C) {
         hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
         hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
     }
-    for (int i = 0; i < 4; i++) if (C.ev[i]) { hipEventDestroy(C.ev[i]); C.ev[i] = nullptr; }
     hipFree(C.d_flag);
     C.d_flag = nullptr;
 }

@@ -81,6 +81,7 @@ class Timing(ctypes.Structure):
         ("union_sets", ctypes.c_uint64),
         ("alg_bytes", ctypes.c_double),
         ("flops", ctypes.c_double),
+        ("exact_rerun", ctypes.c_int32),
     ]
 
     def as_dict(self):
