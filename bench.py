@@ -155,15 +155,27 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    # PSX_DIST_BACKEND=gloo lets a multi-rank run share one GPU for validation
+    # (host-staged exchange); the real path is nccl = RCCL over xGMI.
+    backend = os.environ.get("PSX_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     t_setup = time.time()
     seam = build_seam(args.workload)
     configs_per_step = seam.count_configs()
     pc = E.PostCal(seam, device=local)
     pc.set_shard(rank, world)
+    # one stream for torch (collectives, copies) and the engine: the exchange is
+    # ordered by the stream, no host synchronisation between export and merge
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    pc.set_stream(stream.cuda_stream)
     nbytes = pc.partials_bytes()
     mine = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     gathered = torch.empty(nbytes * world, dtype=torch.uint8, device="cuda")
@@ -172,10 +184,14 @@ def main():
     def step():
         pc.run_exhaustive()
         if world > 1:
-            pc.export_partials(mine.data_ptr())
-            dist.all_gather_into_tensor(gathered, mine)  # the one exchange step (RCCL over xGMI)
-            torch.cuda.synchronize()
-            pc.merge_partials(gathered.data_ptr(), world)
+            pc.export_partials(mine.data_ptr())  # enqueued on torch's current stream
+            if backend == "nccl":
+                dist.all_gather_into_tensor(gathered, mine)  # the one exchange step (RCCL over xGMI)
+            else:
+                parts = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
+                dist.all_gather(parts, mine.cpu())
+                gathered.copy_(torch.cat(parts))
+            pc.merge_partials(gathered.data_ptr(), world)  # ordered after the collective
 
     for _ in range(args.warmup):
         step()
@@ -195,10 +211,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        x = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        x = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         elapsed = float(x.item())
     tm = pc.timing()
+    torch.cuda.synchronize()
     acc = pc.accum() if (world == 1 or rank == 0) else None
 
     if rank == 0:
@@ -231,7 +248,8 @@ def main():
             "data": "synthetic" if args.workload != "example" else "reference fixture",
             "config": {"workload": WORKLOADS[args.workload][4], "union_snps": seam.n_union,
                        "max_causal": int(seam.max_causal), "configs_per_step": configs_per_step,
-                       "parallelism": f"config-shard x{world} + 1 RCCL all-gather" if world > 1 else "single GPU"},
+                       "parallelism": (f"config-shard x{world} + 1 {'RCCL' if backend == 'nccl' else backend} all-gather"
+                            if world > 1 else "single GPU")},
             "roofline": roofline,
             "fp64": fp64,
             "setup_s": setup_s,

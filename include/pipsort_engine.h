@@ -125,6 +125,12 @@ int psx_get_accum(psx_engine *e, psx_accum *out);
  * them from all ranks (e.g. one RCCL all-gather), then merge `count`
  * concatenated partials (rank order) into this handle's accumulators. */
 int64_t psx_partials_bytes(psx_engine *e);
+/* Enqueue on a caller stream (a hipStream_t, e.g. the framework's current
+ * stream) instead of the handle's own; NULL restores the own stream.  On a
+ * caller stream psx_export_partials / psx_merge_partials only enqueue (the
+ * caller orders them against its collective); psx_run_* still return with the
+ * sweep complete. */
+int psx_set_stream(psx_engine *e, void *stream);
 int psx_export_partials(psx_engine *e, void *device_dst);
 int psx_merge_partials(psx_engine *e, const void *device_src, int32_t count);
 

@@ -288,6 +288,8 @@ __global__ void k_merge_partials(const Acc5* __restrict__ parts, int U, int ldg,
 struct psx_engine {
     int dev = 0;
     hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;  // created by psx_create
+    bool external_stream = false;      // psx_set_stream: caller orders export/merge
     int S = 2;
     int m[2] = {0, 0};
     int N = 0, U = 0, ldg = 0, maxc = 0;
@@ -350,7 +352,7 @@ psx_engine::~psx_engine() {
         for (int i = 0; i < 2; i++) if (g.ev[i]) hipEventDestroy(g.ev[i]);
     }
     for (int i = 0; i < 4; i++) hipEventDestroy(ev[i]);
-    if (stream) hipStreamDestroy(stream);
+    if (own_stream) hipStreamDestroy(own_stream);
 }
 
 namespace {
@@ -681,7 +683,8 @@ int psx_create(const psx_problem* p, int device, psx_engine** out) {
     psx_engine* e = new psx_engine();
     e->dev = device;
     auto bail = [&](int rc) { delete e; return rc; };
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(fail(PSX_EHIP, "stream"));
+    if (hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(fail(PSX_EHIP, "stream"));
+    e->stream = e->own_stream;
     for (int i = 0; i < 4; i++)
         if (hipEventCreate(&e->ev[i]) != hipSuccess) return bail(fail(PSX_EHIP, "event"));
     e->m[0] = p->m[0];
@@ -1139,7 +1142,20 @@ int psx_export_partials(psx_engine* e, void* dst) {
     char* d = (char*)dst;
     HIPCHK(hipMemcpyAsync(d, e->dacc, sizeof(Acc5) * e->ldg, hipMemcpyDeviceToDevice, e->stream));
     HIPCHK(hipMemcpyAsync(d + sizeof(Acc5) * e->ldg, e->dsacc, sizeof(SetRec), hipMemcpyDeviceToDevice, e->stream));
+    if (!e->external_stream) HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int psx_set_stream(psx_engine* e, void* stream) {
+    HIPCHK(hipSetDevice(e->dev));
     HIPCHK(hipStreamSynchronize(e->stream));
+    if (stream == nullptr) {
+        e->stream = e->own_stream;
+        e->external_stream = false;
+    } else {
+        e->stream = (hipStream_t)stream;
+        e->external_stream = true;
+    }
     return 0;
 }
 
@@ -1149,7 +1165,7 @@ int psx_merge_partials(psx_engine* e, const void* src, int32_t count) {
     hipLaunchKernelGGL(k_merge_partials, dim3((e->U + 255) / 256), dim3(256), 0, e->stream, (const Acc5*)src, e->U,
                        e->ldg, count, e->dacc, e->dsacc);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(e->stream));
+    if (!e->external_stream) HIPCHK(hipStreamSynchronize(e->stream));
     return 0;
 }
 

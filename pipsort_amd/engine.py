@@ -31,7 +31,7 @@ EXPORTED = [
     "psx_set_shard", "psx_run_exhaustive", "psx_run_configs", "psx_run_sss",
     "psx_eval_union_batch", "psx_reset", "psx_get_accum", "psx_partials_bytes",
     "psx_export_partials", "psx_merge_partials", "psx_get_timing", "psx_count_configs",
-    "psx_fold_partials_host", "psx_shard_stats",
+    "psx_fold_partials_host", "psx_shard_stats", "psx_set_stream",
     "psx_psd_shift", "psx_lowrank_study", "psx_sym_eigen",
 ]
 
@@ -122,6 +122,7 @@ def load_library(path: str = LIB_PATH):
         "psx_get_timing": (c_int, [vp, P(Timing)]),
         "psx_count_configs": (c_u64, [P(_Problem)]),
         "psx_fold_partials_host": (c_int, [vp, c_i32, c_i64, vp]),
+        "psx_set_stream": (c_int, [vp, vp]),
         "psx_shard_stats": (c_int, [P(_Problem), c_i32, c_i32, c_i32, P(c_u64), P(dbl)]),
         "psx_psd_shift": (c_int, [P(dbl), c_i32, P(dbl)]),
         "psx_lowrank_study": (c_int, [P(dbl), P(dbl), c_i32, P(dbl), P(dbl)]),
@@ -313,6 +314,10 @@ class PostCal:
             self.close()
         except Exception:
             pass
+
+    def set_stream(self, stream_handle: int | None):
+        """Enqueue on a caller HIP stream (e.g. torch.cuda.current_stream().cuda_stream)."""
+        _check(self.lib.psx_set_stream(self.h, ctypes.c_void_p(stream_handle or None)))
 
     def set_shard(self, rank: int, world: int):
         _check(self.lib.psx_set_shard(self.h, rank, world))

@@ -1,0 +1,37 @@
+"""Multi-process sharded sweep (bench.py under torch.distributed.run).  On a
+one-GPU box both ranks share cuda:0 and exchange partials over gloo
+(PSX_DIST_BACKEND=gloo, host-staged); on a node the same code uses RCCL."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_sharded_two_ranks(gpu, world):
+    env = dict(os.environ, PSX_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(world), "--steps", "2", "--warmup", "1", "--workload", "syn200c2", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == world
+    # every rank's shard folded into rank 0's accumulators: all configurations counted once
+    assert out["configs_checked"] == out["config"]["configs_per_step"] == 179_701

@@ -254,3 +254,63 @@ def test_full_size_properties(gpu):
         L, _ = O.eval_patterns(seam, np.repeat(s[None, :], 27, axis=0), bits, literal=True)
         best = L[np.argmax(np.abs(L))]
         assert abs(scores[i] - best) <= 1e-9 * abs(best)
+
+
+def test_extreme_signal_exact_rerun(gpu):
+    """A shared SNP with z ~ 45 in both studies: its quadratic gain exceeds 900
+    bits in both, so notSharedLL groups sit beyond the fast kernel's rescale
+    range; the engine must detect it and re-sweep with the exact variant."""
+    M = 80
+    idx = np.arange(M)
+    ld, z = [], []
+    for s, rho in enumerate((0.5, 0.3)):
+        sig = rho ** np.abs(idx[:, None] - idx[None, :])
+        lam = np.zeros(M)
+        lam[20] = 45.0
+        lam[60] = 6.0 if s == 0 else 0.0
+        eps = np.random.default_rng(9 + s).standard_normal(M)
+        z.append(sig @ lam + np.linalg.cholesky(sig) @ eps)
+        ld.append(sig)
+    u2l = np.stack([idx, idx]).astype(np.int32)
+    seam = E.seam_from_arrays(ld, z, u2l, (12000, 9000), max_causal=3, sharing_param=0.3)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    assert pc.timing()["exact_rerun"] == 1
+    assert_parity(pc.accum(), O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-10)
+
+
+def _cli_pair(tmp_path, src, args):
+    d1, d2 = tmp_path / "engine", tmp_path / "oracle"
+    shutil.copytree(os.path.join(loci.GOLDEN, src), d1)
+    shutil.copytree(os.path.join(loci.GOLDEN, src), d2)
+    r1 = subprocess.run([E.PIPSORT_BIN] + args, cwd=d1, capture_output=True, text=True, timeout=300)
+    r2 = subprocess.run([O.CLI] + args, cwd=d2, capture_output=True, text=True, timeout=300)
+    assert r1.returncode == 0 and r2.returncode == 0, r1.stdout + r1.stderr
+    for f in ("study0_post", "study1_post", "study0_set", "study1_set", "nocausal", "shared_pips", "log"):
+        a = open(d1 / f"out_{f}.txt").read()
+        b = open(d2 / f"out_{f}.txt").read()
+        if a != b:  # allow a last-printed-digit rounding flip, nothing more
+            la, lb = a.splitlines(), b.splitlines()
+            assert len(la) == len(lb), f
+            for x, y in zip(la, lb):
+                if x == y:
+                    continue
+                for u, v in zip(x.split("\t"), y.split("\t")):
+                    if u != v:
+                        fu, fv = float(u), float(v)
+                        assert abs(fu - fv) <= 1e-5 * max(abs(fv), 1e-300) + 1e-300, (f, x, y)
+
+
+@pytest.mark.parametrize("args", [
+    ["-c", "1"], ["-c", "2"], ["-c", "3"], ["-q", "1"], ["-c", "3", "-p", "0.5", "-g", "0.05", "-t", "0.3", "-s", "4"],
+])
+def test_cli_small_example_matches_oracle_cli(gpu, tmp_path, args):
+    base = ["-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "eur_afr_small_test_snp_map", "-n", "7000,7000",
+            "-o", "out"]
+    _cli_pair(tmp_path, "small_example", args + base)
+
+
+def test_cli_configs_file_matches_oracle_cli(gpu, tmp_path):
+    _cli_pair(tmp_path, "test_optional_configs",
+              ["-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "eur_afr_small_test_snp_map", "-n", "7000,7000",
+               "-b", "all_configs_int16", "-d", "72", "-e", "5", "-o", "out"])
