@@ -53,11 +53,32 @@ struct SweepPlan {
     bool ran = false;
 };
 
+// Arguments of the k = 3 fast kernel (psx_sweep3.hip).
+struct Sweep3Args {
+    const double* G[2];        // Sigma~_s in union coordinates, [ldg][ldg]
+    const double* Ad[2];       // diag(A_s) = 1/d_s + diag(Sigma~_s)
+    const double* ys[2];       // y_s * sqrt(log2(e) / 2)
+    const double* skew[2];     // skewed Sigma~ tiles
+    const double* muS[2];      // singleton weights {c}
+    const int* nS[2];
+    const unsigned char* pres; // bit s: SNP present in study s
+    const double* tab;         // 2^(i/256), i < 256
+    double rsd[2];             // d_s^{-1/2}
+    double rho, pit0;          // pit[nsh] = pit0 * rho^nsh (prior per member is multiplicative)
+    int U, ldg, Ck;
+};
+int launch_sweep3(bool allpres, const Sweep3Args& A, int n_units, const int4* units, Acc5* rec, SetRec* srec,
+                  int rec_stride, int* flag, hipStream_t st);
+int launch_scale_y(const double* y, int n, double* ys, hipStream_t st);
+
 struct SweepPlanCache {
     std::map<std::tuple<int, int, int, int>, SweepPlan> plans;  // (k, U, rank, world)
     double* d_skew[2] = {nullptr, nullptr};  // skewed Sigma~ tiles (B <= T)
     double* d_muS[2] = {nullptr, nullptr};   // singleton subset weights
     int* d_nS[2] = {nullptr, nullptr};
+    double* d_ys[2] = {nullptr, nullptr};    // scaled y (k = 3 fast kernel)
+    double* d_tab = nullptr;                 // 2^(i/256) table
+    bool allpres = false;                    // every union SNP is in both studies
     int skew_ldg = 0;
     const double* skew_src[2] = {nullptr, nullptr};
     int* d_flag = nullptr;  // raised when a set needs the EXACT notSharedLL variant

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "psx_sweep.h"
+#include "psx_sweep_dev.h"
 
 namespace psx {
 
@@ -38,123 +39,6 @@ const char* sweep_error() { return g_sweep_err.c_str(); }
             return -1;                                                                              \
         }                                                                                           \
     } while (0)
-
-struct TileArgs {
-    const double* G[2];
-    const double* Ad[2];
-    const double* y[2];
-    const double* skew[2];
-    const double* muS[2];  // singleton weights {c}: mu of 2^{h_c} (d A_cc)^{-1/2}
-    const int* nS[2];      // and its integer exponent floor(h_c)
-    const unsigned char* pres;
-    double d[2], rsd[2];   // d_s and d_s^{-1/2}
-    int U, ldg, Ck;
-    double pit[4];
-};
-
-constexpr int EMPTY = -(1 << 28);  // shift of an empty accumulator (value 0)
-
-__device__ inline Acc5 acc_zero() {
-    Acc5 a;
-    a.mP = a.mS = a.mN = EMPTY;
-    a.pad = 0;
-    a.post0 = a.post1 = a.shared = a.sll = a.nsll = 0.0;
-    return a;
-}
-
-__device__ inline Acc5 shfl_acc5(const Acc5& a, int o) {
-    Acc5 b;
-    b.mP = __shfl_xor(a.mP, o);
-    b.mS = __shfl_xor(a.mS, o);
-    b.mN = __shfl_xor(a.mN, o);
-    b.pad = 0;
-    b.post0 = __shfl_xor(a.post0, o);
-    b.post1 = __shfl_xor(a.post1, o);
-    b.shared = __shfl_xor(a.shared, o);
-    b.sll = __shfl_xor(a.sll, o);
-    b.nsll = __shfl_xor(a.nsll, o);
-    return b;
-}
-
-__device__ inline SetRec shfl_set(const SetRec& a, int o) {
-    SetRec b;
-    b.m = __shfl_xor(a.m, o);
-    b.m0 = __shfl_xor(a.m0, o);
-    b.m1 = __shfl_xor(a.m1, o);
-    b.pad = 0;
-    b.tot = __shfl_xor(a.tot, o);
-    b.nc0 = __shfl_xor(a.nc0, o);
-    b.nc1 = __shfl_xor(a.nc1, o);
-    b.score = __shfl_xor(a.score, o);
-    b.npat = __shfl_xor(a.npat, o);
-    return b;
-}
-
-__device__ inline void wave_fold_acc(Acc5& a) {
-    for (int o = 1; o < 64; o <<= 1) {
-        Acc5 b = shfl_acc5(a, o);
-        fold_acc(a, b);
-    }
-}
-__device__ inline void wave_fold_set(SetRec& a) {
-    for (int o = 1; o < 64; o <<= 1) {
-        SetRec b = shfl_set(a, o);
-        fold_set(a, b);
-    }
-}
-
-// Branch-free folds for the hot loop.  Empty accumulators and empty
-// contributions carry shift EMPTY, so max() never lets a zero raise a shift.
-__device__ __forceinline__ void ffold1(int32_t& m, double& s, int32_t m2, double s2) {
-    const int M = max(m, m2);
-    s = ldexp(s, m - M) + ldexp(s2, m2 - M);
-    m = M;
-}
-__device__ __forceinline__ void ffold_acc(Acc5& a, const Acc5& b) {
-    const int M = max(a.mP, b.mP);
-    a.post0 = ldexp(a.post0, a.mP - M) + ldexp(b.post0, b.mP - M);
-    a.post1 = ldexp(a.post1, a.mP - M) + ldexp(b.post1, b.mP - M);
-    a.shared = ldexp(a.shared, a.mP - M) + ldexp(b.shared, b.mP - M);
-    a.mP = M;
-    ffold1(a.mS, a.sll, b.mS, b.sll);
-    ffold1(a.mN, a.nsll, b.mN, b.nsll);
-}
-__device__ __forceinline__ int nz_shift(int m, double s) { return s != 0.0 ? m : EMPTY; }
-
-// 1/sqrt(x) to full double precision: v_rsq_f64 + two Newton steps
-__device__ __forceinline__ double rsqrt_nr(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-    double e = fma(-x * y, y, 1.0);
-    y = fma(0.5 * y, e, y);
-    e = fma(-x * y, y, 1.0);
-    return fma(0.5 * y, e, y);
-}
-
-// 2^f for f in [0, 1): sqrt(2) e^t, t = (f - 1/2) ln 2, degree-12 Taylor (|err| < 2e-16)
-__device__ __forceinline__ double exp2_frac(double f) {
-    const double t = (f - 0.5) * PSX_LN2;
-    double p = 2.08767569878680989792e-09;      // 1/12!
-    p = fma(p, t, 2.50521083854417187751e-08);  // 1/11!
-    p = fma(p, t, 2.75573192239858906526e-07);  // 1/10!
-    p = fma(p, t, 2.75573192239858906526e-06);  // 1/9!
-    p = fma(p, t, 2.48015873015873015873e-05);  // 1/8!
-    p = fma(p, t, 1.98412698412698412698e-04);  // 1/7!
-    p = fma(p, t, 1.38888888888888888889e-03);  // 1/6!
-    p = fma(p, t, 8.33333333333333333333e-03);  // 1/5!
-    p = fma(p, t, 4.16666666666666666667e-02);  // 1/4!
-    p = fma(p, t, 1.66666666666666666667e-01);  // 1/3!
-    p = fma(p, t, 0.5);
-    p = fma(p, t, 1.0);
-    p = fma(p, t, 1.0);
-    return p * 1.41421356237309504880;
-}
-
-// weight 2^h * rP as (n, mu), n = floor(h), mu in (0, 2)
-__device__ __forceinline__ void split2(double h, double rP, int& n, double& mu) {
-    const double fl = floor(h);
-    n = (int)fl;
-    mu = exp2_frac(h - fl) * rP;
-}
 
 // One union set: per-study subset weights (n, mu) for the 2^K subsets (bit j =
 // member j), zero-weighted where a member is absent from the study.  Folds the
@@ -277,7 +161,6 @@ __device__ __forceinline__ void fold_set_patterns(const TileArgs& A, const int (
     sr.npat = wcount;
 }
 
-__device__ __forceinline__ double memb_weight(unsigned p) { return p == 3u ? 3.0 : (p ? 1.0 : 0.0); }
 
 template <int K, bool EXACT>
 __global__ __launch_bounds__(64, (K == 3 ? 2 : 4)) void k_sweep(TileArgs A, const int4* __restrict__ units, Acc5* __restrict__ rec,
@@ -347,7 +230,9 @@ __global__ __launch_bounds__(64, (K == 3 ? 2 : 4)) void k_sweep(TileArgs A, cons
         if (K == 3) pa = A.pres[a];
         const bool abvalid = bvalid && (K == 2 || a < b);
         const double wab_cnt = memb_weight(pb) * (K == 3 ? memb_weight(pa) : 1.0);
-        for (int j = 0; j < 64; j++) {
+        // k = 2 units carry a j-range of the diagonal walk in (a0, a1)
+        const int j0 = (K == 2) ? a0 : 0, j1 = (K == 2) ? a1 : 64;
+        for (int j = j0; j < j1; j++) {
             const int cc = (t + j) & 63;
             const int c = 64 * T + cc;
             const bool act = abvalid && c < A.U && (B < T || cc > t);
@@ -559,12 +444,17 @@ int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* 
             }
         }
     } else if (k == 2) {
+        // one wave per (B, T) tile would leave most of the 1024 SIMDs idle:
+        // split the 64-step diagonal walk into S j-ranges (a0, a1 = j0, j1)
+        int tiles = 0;
+        for (int T = 0; T < nblk && 64 * T < U; T++) tiles += std::min(T + 1, (U + 63) / 64);
+        const int S = std::max(1, std::min(8, (1024 * world + tiles - 1) / std::max(1, tiles)));
         ca = 0;
         for (int T = 0; T < nblk; T++) {
             if (64 * T >= U) break;
             for (int B = 0; B <= T; B++) {
                 if (64 * B >= U) break;
-                all.push_back({0, 1, B, T, 1.0});
+                for (int i = 0; i < S; i++) all.push_back({64 * i / S, 64 * (i + 1) / S, B, T, 1.0 / S});
             }
         }
     } else {
@@ -618,11 +508,12 @@ int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* 
                     }
                 }
             } else {
-                for (int z = 1; z < 4; z++) {
-                    double ncz = pref[z][c_hi] - pref[z][c_lo];
-                    sets += ncz;
-                    bytes += ncz * bytes_cls[1][mb][z];
-                    configs += ncz * wcls[mb] * wcls[z];
+                for (int j = u.a0; j < u.a1; j++) {  // this unit's part of the diagonal walk
+                    const int cc = (t + j) & 63, c = 64 * u.T + cc;
+                    if (c >= U || (u.B == u.T && cc <= t) || pres_host[c] == 0) continue;
+                    sets += 1;
+                    bytes += bytes_cls[1][mb][pres_host[c]];
+                    configs += wcls[mb] * wcls[pres_host[c]];
                 }
             }
         }
@@ -693,14 +584,30 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     return 0;
 }
 
-static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, hipStream_t st) {
+static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hipStream_t st) {
     if (C.d_skew[0] && C.skew_ldg == ldg && C.skew_src[0] == a.G0 && C.skew_src[1] == a.G1) return 0;
     for (int s = 0; s < 2; s++) {
         hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
         hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
         hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
+        hipFree(C.d_ys[s]); C.d_ys[s] = nullptr;
+    }
+    hipFree(C.d_tab); C.d_tab = nullptr;
+    {
+        // 2^(i/256) correctly rounded (long double on the host)
+        double tab[256];
+        for (int i = 0; i < 256; i++) tab[i] = (double)exp2l((long double)i / 256.0L);
+        SWCHK(hipMalloc(&C.d_tab, sizeof(tab)));
+        SWCHK(hipMemcpyAsync(C.d_tab, tab, sizeof(tab), hipMemcpyHostToDevice, st));
+        std::vector<unsigned char> pres(ldg);
+        SWCHK(hipMemcpyAsync(pres.data(), a.pres, ldg, hipMemcpyDeviceToHost, st));
+        SWCHK(hipStreamSynchronize(st));
+        C.allpres = true;
+        for (int u = 0; u < U; u++) C.allpres = C.allpres && pres[u] == 3;
     }
     for (int s = 0; s < 2; s++) {
+        SWCHK(hipMalloc(&C.d_ys[s], sizeof(double) * ldg));
+        if (launch_scale_y(s ? a.y1 : a.y0, ldg, C.d_ys[s], st)) SWCHK(hipGetLastError());
         SWCHK(hipMalloc(&C.d_muS[s], sizeof(double) * ldg));
         SWCHK(hipMalloc(&C.d_nS[s], sizeof(int) * ldg));
         hipLaunchKernelGGL(k_build_singles, dim3((ldg + 255) / 256), dim3(256), 0, st, s ? a.Ad1 : a.Ad0,
@@ -735,7 +642,7 @@ int sweep_flag(SweepPlanCache& C, int* flag) {
 // Enqueue one level (kernel + record merges) on `st`; no host synchronisation.
 int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, hipStream_t st, const SweepArgs& a,
                 Acc5* acc, SetRec* sacc, bool exact) {
-    if (ensure_skew(C, a, ldg, st)) return -1;
+    if (ensure_skew(C, a, ldg, U, st)) return -1;
     auto key = std::make_tuple(k, U, rank, world);
     auto it = C.plans.find(key);
     if (it == C.plans.end()) {
@@ -765,9 +672,20 @@ int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, h
     if (!C.d_flag && sweep_begin(C, st)) return -1;
     SWCHK(hipEventRecord(P.ev[0], st));
     const dim3 g(P.n_units), blk(64);
-    if (k == 3 && !exact)
-        hipLaunchKernelGGL((k_sweep<3, false>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag);
-    else if (k == 3)
+    if (k == 3 && !exact) {
+        Sweep3Args S3;
+        for (int s = 0; s < 2; s++) {
+            S3.G[s] = A.G[s]; S3.Ad[s] = A.Ad[s]; S3.ys[s] = C.d_ys[s]; S3.skew[s] = A.skew[s];
+            S3.muS[s] = A.muS[s]; S3.nS[s] = A.nS[s]; S3.rsd[s] = A.rsd[s];
+        }
+        S3.pres = A.pres;
+        S3.tab = C.d_tab;
+        S3.pit0 = A.pit[0];
+        S3.rho = A.pit[0] > 0 ? A.pit[1] / A.pit[0] : 0.0;
+        S3.U = U; S3.ldg = ldg; S3.Ck = A.Ck;
+        if (launch_sweep3(C.allpres, S3, P.n_units, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag, st))
+            SWCHK(hipGetLastError());
+    } else if (k == 3)
         hipLaunchKernelGGL((k_sweep<3, true>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag);
     else if (!exact)
         hipLaunchKernelGGL((k_sweep<2, false>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag);
@@ -814,7 +732,9 @@ void sweep_free(SweepPlanCache& C) {
         hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
         hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
         hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
+        hipFree(C.d_ys[s]); C.d_ys[s] = nullptr;
     }
+    hipFree(C.d_tab); C.d_tab = nullptr;
     hipFree(C.d_flag);
     C.d_flag = nullptr;
 }
