@@ -29,6 +29,8 @@ namespace {
 
 thread_local std::string g_err;
 
+constexpr size_t kStatBytes = 64;  // SetRec (56 B) + EXACT flag (4 B) + pad
+
 int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
@@ -306,7 +308,9 @@ struct psx_engine {
     double* dy[2] = {nullptr, nullptr};
     unsigned char* dpres = nullptr;
     Acc5* dacc = nullptr;
-    SetRec* dsacc = nullptr;
+    SetRec* dsacc = nullptr;   // status block: SetRec, then the EXACT flag (int)
+    int* dflag = nullptr;
+    unsigned char* hstat = nullptr;  // pinned host copy of the status block
     // sweep workspace (tiled kernel)
     psx::SweepPlanCache plans;
     // generic workspace
@@ -327,6 +331,7 @@ struct psx_engine {
         SetRec* d_srec = nullptr;
         Acc5* d_mrec = nullptr;
         size_t nsets = 0;
+        int lo = 0;  // first set's rank in lexicographic order
         int ptr_len = 0, idx_len = 0, n_rows = 0;
         hipEvent_t ev[2] = {nullptr, nullptr};
         bool ran = false;
@@ -344,6 +349,7 @@ psx_engine::~psx_engine() {
     hipSetDevice(dev);
     for (int s = 0; s < 2; s++) { hipFree(dG[s]); hipFree(dAd[s]); hipFree(dy[s]); }
     hipFree(dpres); hipFree(dacc); hipFree(dsacc);
+    if (hstat) hipHostFree(hstat);
     hipFree(dsets); hipFree(dforced); hipFree(dsrec); hipFree(dmrec); hipFree(dcsr);
     psx::sweep_free(plans);
     for (auto& kv : glevels) {
@@ -463,9 +469,8 @@ int eval_generic(psx_engine* e, const std::vector<int>& sets, int stride, size_t
     return 0;
 }
 
-// fold `count` null configurations (postcal.cpp:793-822) into the scalars
-int fold_null(psx_engine* e, double count) {
-    if (count <= 0) return 0;
+// `count` null configurations (postcal.cpp:793-822) as a set record
+SetRec null_rec(const psx_engine* e, double count) {
     double h = e->L0 * PSX_LOG2E;
     double fl = std::floor(h);
     SetRec x = psx::set_zero();
@@ -474,7 +479,14 @@ int fold_null(psx_engine* e, double count) {
     x.npat = count;
     double v = std::exp2(h - fl) * count;
     x.tot = x.nc0 = x.nc1 = v;
-    if (psx::launch_merge_sets(nullptr, 0L, x, e->dsacc, e->stream)) return fail(PSX_EHIP, psx::sweep_error());
+    return x;
+}
+
+// fold `count` null configurations into the scalars
+int fold_null(psx_engine* e, double count) {
+    if (count <= 0) return 0;
+    if (psx::launch_merge_sets(nullptr, 0L, null_rec(e, count), e->dsacc, e->stream))
+        return fail(PSX_EHIP, psx::sweep_error());
     return 0;
 }
 
@@ -601,15 +613,50 @@ int enqueue_generic_level(psx_engine* e, int k) {
     return 0;
 }
 
-// One exhaustive pass, everything enqueued on the engine stream, one sync.
+// Level 1 of a pass: its member records ARE the initial per-SNP accumulators
+// (set i of this shard is SNP lo + i), so they are written in place into the
+// zeroed dacc; the set records initialise the scalars together with `extra`
+// (the null configuration on rank 0) and the EXACT flag is cleared.
+int enqueue_level1(psx_engine* e, const SetRec& extra) {
+    auto key = std::make_tuple(1, e->rank, e->world);
+    auto it = e->glevels.find(key);
+    if (it == e->glevels.end()) {
+        psx_engine::GenLevel g;
+        uint64_t lo = (uint64_t)e->U * e->rank / e->world, hi = (uint64_t)e->U * (e->rank + 1) / e->world;
+        g.lo = (int)lo;
+        g.nsets = (size_t)(hi - lo);
+        if (g.nsets) {
+            std::vector<int> sets(g.nsets);
+            for (size_t i = 0; i < g.nsets; i++) sets[i] = (int)(lo + i);
+            HIPCHK(hipMalloc(&g.d_sets, sizeof(int) * g.nsets));
+            HIPCHK(hipMemcpy(g.d_sets, sets.data(), sizeof(int) * g.nsets, hipMemcpyHostToDevice));
+            HIPCHK(hipMalloc(&g.d_srec, sizeof(SetRec) * g.nsets));
+        }
+        for (int i = 0; i < 2; i++) HIPCHK(hipEventCreate(&g.ev[i]));
+        it = e->glevels.emplace(key, g).first;
+    }
+    psx_engine::GenLevel& g = it->second;
+    HIPCHK(hipEventRecord(g.ev[0], e->stream));
+    if (g.nsets)
+        hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)g.nsets), dim3(64), 0, e->stream, e->dp, g.d_sets, 1,
+                           (const int*)nullptr, g.d_srec, e->dacc + g.lo);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(g.ev[1], e->stream));
+    if (psx::launch_merge_sets(g.d_srec, (long)g.nsets, extra, e->dsacc, e->stream, true, e->dflag))
+        return fail(PSX_EHIP, psx::sweep_error());
+    g.ran = true;
+    return 0;
+}
+
+// One exhaustive pass, everything enqueued on the engine stream; the status
+// block (scalars + EXACT flag) comes back with one async copy and one sync.
 int exhaustive_pass(psx_engine* e, bool exact, double* generic_ms) {
     int rc;
-    if ((rc = reset_acc(e))) return rc;
-    if (psx::sweep_begin(e->plans, e->stream)) return fail(PSX_EHIP, psx::sweep_error());
+    HIPCHK(hipMemsetAsync(e->dacc, 0, sizeof(Acc5) * e->ldg, e->stream));
     HIPCHK(hipEventRecord(e->ev[0], e->stream));
-    if (e->rank == 0 && (rc = fold_null(e, 1.0))) return rc;
+    if ((rc = enqueue_level1(e, e->rank == 0 ? null_rec(e, 1.0) : psx::set_zero()))) return rc;
     double kms = 0;
-    for (int k = 1; k <= e->maxc; k++) {
+    for (int k = 2; k <= e->maxc; k++) {
         if (psx::sweep_supports(k, e->U)) {
             psx::SweepArgs sa{e->dG[0], e->dG[1], e->dAd[0], e->dAd[1], e->dy[0], e->dy[1], e->dpres,
                               e->dval[0], e->dval[1], e->dp.Ck, &e->dp.pit[0][0], PSX_KMAX + 1};
@@ -623,6 +670,7 @@ int exhaustive_pass(psx_engine* e, bool exact, double* generic_ms) {
         }
     }
     HIPCHK(hipEventRecord(e->ev[1], e->stream));
+    HIPCHK(hipMemcpyAsync(e->hstat, e->dsacc, kStatBytes, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     for (int k = 1; k <= e->maxc; k++) {
         auto it = e->glevels.find(std::make_tuple(k, e->rank, e->world));
@@ -785,8 +833,11 @@ int psx_create(const psx_problem* p, int device, psx_engine** out) {
     }
     cleanup();
     if (hipMalloc(&e->dpres, e->ldg) != hipSuccess || hipMalloc(&e->dacc, sizeof(Acc5) * e->ldg) != hipSuccess ||
-        hipMalloc(&e->dsacc, sizeof(SetRec)) != hipSuccess)
+        hipMalloc(&e->dsacc, kStatBytes) != hipSuccess || hipHostMalloc(&e->hstat, kStatBytes) != hipSuccess)
         return bail(fail(PSX_EHIP, "out of device memory"));
+    e->dflag = (int*)((char*)e->dsacc + sizeof(SetRec));
+    e->plans.d_flag = e->dflag;
+    e->plans.own_flag = false;
     hipMemcpyAsync(e->dpres, e->pres.data(), e->ldg, hipMemcpyHostToDevice, e->stream);
     for (int s = 0; s < 2; s++) {
         dp.G[s] = e->dG[s];
@@ -824,8 +875,7 @@ int psx_run_exhaustive(psx_engine* e) {
     std::memset(&e->timing, 0, sizeof(e->timing));
     double gms = 0;
     if ((rc = exhaustive_pass(e, false, &gms))) return rc;
-    int flag = 0;
-    if (psx::sweep_flag(e->plans, &flag)) return fail(PSX_EHIP, psx::sweep_error());
+    int flag = *(const int*)(e->hstat + sizeof(SetRec));
     if (flag) {  // some set's notSharedLL group sits > 900 bits below its maximum: exact variant
         if ((rc = exhaustive_pass(e, true, &gms))) return rc;
     }
@@ -853,7 +903,7 @@ int psx_run_exhaustive(psx_engine* e) {
     e->timing.merge_ms = st.merge_ms;
     e->timing.exact_rerun = flag;
     SetRec s;
-    HIPCHK(hipMemcpy(&s, e->dsacc, sizeof(SetRec), hipMemcpyDeviceToHost));
+    std::memcpy(&s, e->hstat, sizeof(SetRec));
     e->timing.configs = (uint64_t)(s.npat + 0.5);
     return 0;
 }

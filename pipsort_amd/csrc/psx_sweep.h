@@ -82,6 +82,7 @@ struct SweepPlanCache {
     int skew_ldg = 0;
     const double* skew_src[2] = {nullptr, nullptr};
     int* d_flag = nullptr;  // raised when a set needs the EXACT notSharedLL variant
+    bool own_flag = true;   // false: d_flag lives in the engine's status block
 };
 
 bool sweep_supports(int k, int U);
@@ -96,7 +97,8 @@ int sweep_stats(SweepPlanCache& cache, int k, int U, int rank, int world, SweepS
 void sweep_free(SweepPlanCache& cache);
 int launch_merge_members(const Acc5* rec, const int* ptr, const int* idx, const int* rows, int n_rows, Acc5* acc,
                          hipStream_t st);
-int launch_merge_sets(const SetRec* rec, long n, const SetRec& extra, SetRec* acc, hipStream_t st);
+int launch_merge_sets(const SetRec* rec, long n, const SetRec& extra, SetRec* acc, hipStream_t st,
+                      bool init = false, int* zero_flag = nullptr);
 const char* sweep_error();
 
 }  // namespace psx

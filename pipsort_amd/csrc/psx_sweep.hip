@@ -361,22 +361,23 @@ __global__ __launch_bounds__(64) void k_merge_members(const Acc5* __restrict__ r
     }
 }
 
-__global__ __launch_bounds__(256) void k_merge_sets(const SetRec* __restrict__ rec, long n, SetRec extra,
-                                                    SetRec* __restrict__ acc) {
-    __shared__ SetRec sh[256];
+// Fold n set records (+ extra) into *acc; init: overwrite *acc instead of
+// folding into it and zero *zero_flag (start of an exhaustive pass).
+// Fixed fold order (thread-strided, then wave and block trees): deterministic.
+__global__ __launch_bounds__(512) void k_merge_sets(const SetRec* __restrict__ rec, long n, SetRec extra,
+                                                    SetRec* __restrict__ acc, int init, int* __restrict__ zero_flag) {
+    __shared__ SetRec sh[8];
     SetRec a = set_zero();
-    for (long i = threadIdx.x; i < n; i += 256) fold_set(a, rec[i]);
-    sh[threadIdx.x] = a;
+    for (long i = threadIdx.x; i < n; i += 512) fold_set(a, rec[i]);
+    wave_fold_set(a);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = a;
     __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) fold_set(sh[threadIdx.x], sh[threadIdx.x + s]);
-        __syncthreads();
-    }
     if (threadIdx.x == 0) {
-        SetRec g = *acc;
+        SetRec g = init ? set_zero() : *acc;
         fold_set(g, extra);
-        fold_set(g, sh[0]);
+        for (int w = 0; w < 8; w++) fold_set(g, sh[w]);
         *acc = g;
+        if (zero_flag) *zero_flag = 0;
     }
 }
 
@@ -388,8 +389,9 @@ int launch_merge_members(const Acc5* rec, const int* ptr, const int* idx, const 
     return 0;
 }
 
-int launch_merge_sets(const SetRec* rec, long n, const SetRec& extra, SetRec* acc, hipStream_t st) {
-    hipLaunchKernelGGL(k_merge_sets, dim3(1), dim3(256), 0, st, rec, n, extra, acc);
+int launch_merge_sets(const SetRec* rec, long n, const SetRec& extra, SetRec* acc, hipStream_t st, bool init,
+                      int* zero_flag) {
+    hipLaunchKernelGGL(k_merge_sets, dim3(1), dim3(512), 0, st, rec, n, extra, acc, init ? 1 : 0, zero_flag);
     SWCHK(hipGetLastError());
     return 0;
 }
@@ -735,7 +737,7 @@ void sweep_free(SweepPlanCache& C) {
         hipFree(C.d_ys[s]); C.d_ys[s] = nullptr;
     }
     hipFree(C.d_tab); C.d_tab = nullptr;
-    hipFree(C.d_flag);
+    if (C.own_flag) hipFree(C.d_flag);
     C.d_flag = nullptr;
 }
 

@@ -12,14 +12,12 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 CMD="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --workload $WL"
 
-timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1
-echo "list rc=$?" >> "$OUT/status.txt"
 
 i=0
 while read -r GROUP; do
     [ -z "$GROUP" ] && continue
     i=$((i + 1))
-    timeout -k 10 300 rocprofv3 --pmc $GROUP --kernel-include-regex 'k_sweep' --output-format csv \
+    timeout -k 10 300 rocprofv3 --pmc $GROUP --kernel-include-regex 'k_sweep|k_merge' --output-format csv \
         -d "$OUT/p$i" -o run -- $CMD > "$OUT/p$i.log" 2>&1
     rc=$?
     echo "pass $i [$GROUP] rc=$rc" >> "$OUT/status.txt"
@@ -30,7 +28,7 @@ done <<'EOF'
 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_INSTS_LDS
 FETCH_SIZE
 WRITE_SIZE
-SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES SQ_WAVES
-TCC_HIT_sum TCC_MISS_sum
+SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE
+SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
 EOF
 exit 0

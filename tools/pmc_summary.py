@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Summarise tools/gpu_pmc.sh output into profiles/pmc_latest.json (read by bench.py).
+
+usage: tools/pmc_summary.py gpurun_out/<TAG>/pmc WORKLOAD [KERNEL_SUBSTRING]
+
+Per-dispatch averages of every counter for the dominant kernel, plus derived
+figures.  HBM traffic per launch follows MI355X_MICROARCH.md (HBM/rocprofv3):
+FETCH_SIZE (KB) counts 64 B per 128 B request of a coalesced read, so it is
+doubled; WRITE_SIZE (KB) is taken as is.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+d, workload = sys.argv[1], sys.argv[2]
+ksub = sys.argv[3] if len(sys.argv) > 3 else "k_sweep3"
+agg = collections.defaultdict(float)
+cnt = collections.Counter()
+name = None
+for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
+    for r in csv.DictReader(open(f)):
+        if ksub not in r["Kernel_Name"]:
+            continue
+        name = r["Kernel_Name"]
+        key = (os.path.basename(os.path.dirname(f)), r["Counter_Name"], r["Dispatch_Id"])
+        agg[key] += float(r["Counter_Value"])
+per = collections.defaultdict(list)
+for (p, c, disp), v in agg.items():
+    per[c].append(v)
+c = {k: sum(v) / len(v) for k, v in per.items()}
+out = {"workload": workload, "kernel": name, "counters_per_dispatch": c}
+if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+    out["hbm_bytes_per_launch"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+    out["hbm_bytes_note"] = "2 x FETCH_SIZE + WRITE_SIZE (KB -> B), gfx950 FETCH_SIZE half-count correction"
+if "SQ_INSTS_VALU_FLOPS_FP64" in c:
+    out["fp64_flops_per_launch"] = c["SQ_INSTS_VALU_FLOPS_FP64"]
+if "SQ_INSTS_VALU" in c and "GRBM_GUI_ACTIVE" in c:
+    # every wave64 VALU instruction occupies its SIMD for 4 cycles; 1024 SIMDs
+    out["valu_busy"] = 4.0 * c["SQ_INSTS_VALU"] / (1024.0 * c["GRBM_GUI_ACTIVE"])
+for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+    if k in c and "SQ_WAVE_CYCLES" in c:
+        out[k.lower() + "_frac"] = c[k] / c["SQ_WAVE_CYCLES"]
+json.dump(out, open(os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_latest.json"), "w"), indent=1)
+print(json.dumps({k: v for k, v in out.items() if k != "counters_per_dispatch"}, indent=1))
