@@ -1252,7 +1252,10 @@ int psx_shard_stats(const psx_problem* p, int32_t k, int32_t rank, int32_t world
     if (psx::sweep_supports(k, U)) {
         std::vector<psx::PlanUnit> mine;
         int ca = 0;
-        psx::plan_units(k, U, ldg, rank, world, pres.data(), mine, ca, sets, cfg, bytes);
+        if (k == 3)  // the fast kernel's decomposition (the exact rerun covers the same sets)
+            psx::plan_units3c(U, ldg, rank, world, pres.data(), mine, ca, sets, cfg, bytes);
+        else
+            psx::plan_units(k, U, ldg, rank, world, pres.data(), mine, ca, sets, cfg, bytes);
     } else {
         uint64_t total = choose_u64(U, k);
         uint64_t lo = total * (uint64_t)rank / world, hi = total * (uint64_t)(rank + 1) / world;

@@ -45,35 +45,39 @@ struct SweepPlan {
     uint64_t union_sets = 0;
     double alg_bytes = 0, flops = 0;
     int4* d_units = nullptr;     // {a0, a1, B, T}
-    Acc5* d_rec = nullptr;       // [n_units][rec_stride]
+    Acc5* d_rec = nullptr;       // records in CSR (per-SNP) order
     SetRec* d_srec = nullptr;    // [n_units]
-    int* d_csr = nullptr;        // ptr[n_rows+1], idx[...], row_snp[n_rows]
+    int* d_csr = nullptr;        // ptr[n_rows+1], row_snp[n_rows], pos[n_units * rec_stride]
+    const int* d_pos = nullptr;  // record slot -> CSR position (inside d_csr)
     int csr_ptr_len = 0, csr_idx_len = 0;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // kernel start/end, merges end
     bool ran = false;
 };
 
-// Arguments of the k = 3 fast kernel (psx_sweep3.hip).
+// Arguments of the k = 3 fast kernel (psx_sweep3.hip).  Sweep indices live in
+// the padded space v = u + pad, pad = ldg - U (the partial block is block 0).
 struct Sweep3Args {
-    const double* G[2];        // Sigma~_s in union coordinates, [ldg][ldg]
-    const double* Ad[2];       // diag(A_s) = 1/d_s + diag(Sigma~_s)
-    const double* ys[2];       // y_s * sqrt(log2(e) / 2)
-    const double* skew[2];     // skewed Sigma~ tiles
-    const double* muS[2];      // singleton weights {c}
+    const double* G[2];        // Sigma~_s in union coordinates u, [ldg][ldg]
+    const double* Ad[2];       // diag(A_s) = 1/d_s + diag(Sigma~_s), by u
+    const double* ys[2];       // y_s * sqrt(log2(e) / 2), by u
+    const double* skewT[2];    // skewed Sigma~ tiles in v space, tile(K, C), K <= C
+    const double* muS[2];      // singleton weights {c}, by u
     const int* nS[2];
-    const unsigned char* pres; // bit s: SNP present in study s
+    const unsigned char* pres; // bit s: SNP present in study s, by u
     const double* tab;         // 2^(i/256), i < 256
     double rsd[2];             // d_s^{-1/2}
     double rho, pit0;          // pit[nsh] = pit0 * rho^nsh (prior per member is multiplicative)
-    int U, ldg, Ck;
+    int U, ldg, pad, Ck;
 };
 int launch_sweep3(bool allpres, const Sweep3Args& A, int n_units, const int4* units, Acc5* rec, SetRec* srec,
-                  int rec_stride, int* flag, hipStream_t st);
+                  int rec_stride, int* flag, const int* pos, hipStream_t st);
 int launch_scale_y(const double* y, int n, double* ys, hipStream_t st);
+int launch_build_skewT(const double* G, int ldg, int pad, double* skew, hipStream_t st);
 
 struct SweepPlanCache {
-    std::map<std::tuple<int, int, int, int>, SweepPlan> plans;  // (k, U, rank, world)
-    double* d_skew[2] = {nullptr, nullptr};  // skewed Sigma~ tiles (B <= T)
+    std::map<std::tuple<int, int, int, int, int>, SweepPlan> plans;  // (k, U, rank, world, variant)
+    double* d_skew[2] = {nullptr, nullptr};  // skewed Sigma~ tiles (B <= T), k = 2 and exact k = 3
+    double* d_skewT[2] = {nullptr, nullptr}; // lane-owns-c tiles in v space (k = 3 fast kernel)
     double* d_muS[2] = {nullptr, nullptr};   // singleton subset weights
     int* d_nS[2] = {nullptr, nullptr};
     double* d_ys[2] = {nullptr, nullptr};    // scaled y (k = 3 fast kernel)
@@ -89,6 +93,9 @@ bool sweep_supports(int k, int U);
 struct PlanUnit { int a0, a1, B, T; double work; };
 int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* pres_host,
                std::vector<PlanUnit>& mine, int& ca, double& sets, double& configs, double& bytes);
+// k = 3 fast-kernel decomposition: units (a0, a1, K, C) in v space
+int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_host, std::vector<PlanUnit>& mine,
+                 int& ca, double& sets, double& configs, double& bytes);
 int sweep_begin(SweepPlanCache& cache, hipStream_t stream);   // zero the EXACT flag
 int sweep_level(SweepPlanCache& cache, int k, int U, int ldg, int rank, int world, hipStream_t stream,
                 const SweepArgs& a, Acc5* acc, SetRec* sacc, bool exact);   // async enqueue

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -164,7 +165,8 @@ __device__ __forceinline__ void fold_set_patterns(const TileArgs& A, const int (
 
 template <int K, bool EXACT>
 __global__ __launch_bounds__(64, (K == 3 ? 2 : 4)) void k_sweep(TileArgs A, const int4* __restrict__ units, Acc5* __restrict__ rec,
-                                              SetRec* __restrict__ srec, int rec_stride, int* __restrict__ flag) {
+                                              SetRec* __restrict__ srec, int rec_stride, int* __restrict__ flag,
+                                              const int* __restrict__ pos) {
     __shared__ Acc5 slot[64];   // c accumulators, ownership rotates every step
     __shared__ Acc5 sacc[2][64]; // [0] a, [1] b accumulators, lane-owned
     const int unit = blockIdx.x;
@@ -305,12 +307,12 @@ __global__ __launch_bounds__(64, (K == 3 ? 2 : 4)) void k_sweep(TileArgs A, cons
         if (K == 3) {
             Acc5 acca = sacc[0][t];
             wave_fold_acc(acca);
-            if (t == 0) rec[(size_t)unit * rec_stride + 128 + ai] = acca;
+            if (t == 0) put_rec(rec, pos, (size_t)unit * rec_stride + 128 + ai, acca);
         }
     }
     __syncthreads();
-    rec[(size_t)unit * rec_stride + t] = slot[t];
-    rec[(size_t)unit * rec_stride + 64 + t] = sacc[1][t];
+    put_rec(rec, pos, (size_t)unit * rec_stride + t, slot[t]);
+    put_rec(rec, pos, (size_t)unit * rec_stride + 64 + t, sacc[1][t]);
     wave_fold_set(accs);
     if (t == 0) srec[unit] = accs;
 }
@@ -357,6 +359,25 @@ __global__ __launch_bounds__(64) void k_merge_members(const Acc5* __restrict__ r
         const int u = row_snp[row];
         Acc5 g = acc[u];
         fold_acc(g, a);
+        acc[u] = g;
+    }
+}
+
+// Records written in CSR order (psx_sweep plans): row r's records are the
+// contiguous run [ptr[r], ptr[r+1]); 256 threads fold it in a fixed order.
+__global__ __launch_bounds__(256) void k_merge_rows(const Acc5* __restrict__ rec, const int* __restrict__ ptr,
+                                                   const int* __restrict__ row_snp, Acc5* __restrict__ acc) {
+    __shared__ Acc5 sh[4];
+    const int row = blockIdx.x;
+    Acc5 a = acc_zero();
+    for (int i = ptr[row] + (int)threadIdx.x; i < ptr[row + 1]; i += 256) fold_acc(a, rec[i]);
+    wave_fold_acc(a);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int u = row_snp[row];
+        Acc5 g = acc[u];
+        for (int w = 0; w < 4; w++) fold_acc(g, sh[w]);
         acc[u] = g;
     }
 }
@@ -523,12 +544,97 @@ int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* 
     return 0;
 }
 
-static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, const unsigned char* pres_host) {
+// k = 3 fast-kernel decomposition (k_sweep3): units (a0, a1, K, C), K <= C, in
+// the padded space v = u + pad.  Lane t owns c = 64C + t; b runs over block K;
+// a over [a0, a1) with a < b.  Exact per-shard set / configuration / byte counts
+// in O(64 * 9) per unit from per-class prefix counts over v.
+int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_host, std::vector<PlanUnit>& mine,
+                 int& ca, double& sets, double& configs, double& bytes) {
+    const int nblk = ldg / 64, pad = ldg - U;
+    auto cls = [&](int v) { return v >= pad ? (int)pres_host[v - pad] : 0; };
+    double total_a = 0;
+    for (int C = 0; C < nblk; C++)
+        for (int K = 0; K <= C; K++) total_a += std::max(0, 64 * K + 63 - pad);
+    ca = (int)std::floor(total_a / (4096.0 * world));
+    ca = std::max(1, std::min(64, ca));
+    std::vector<PlanUnit> all;
+    for (int C = 0; C < nblk; C++) {
+        if (64 * C + 64 <= pad) continue;
+        for (int K = 0; K <= C; K++) {
+            const int amax = 64 * K + 63;  // a < b <= 64K + 63
+            for (int a0 = pad; a0 < amax; a0 += ca) {
+                const int a1 = std::min(a0 + ca, amax);
+                all.push_back({a0, a1, K, C, (double)(a1 - a0)});
+            }
+        }
+    }
+    double wsum = 0;
+    for (auto& u : all) wsum += u.work;
+    double lo = wsum * rank / world, hi = wsum * (rank + 1) / world, run = 0;
+    mine.clear();
+    for (auto& u : all) {
+        double mid = run + 0.5 * u.work;
+        if (mid >= lo && mid < hi) mine.push_back(u);
+        run += u.work;
+    }
+    double bytes_cls[4][4][4];
+    for (int x = 1; x < 4; x++)
+        for (int y = 1; y < 4; y++)
+            for (int z = 1; z < 4; z++) {
+                int m3[3] = {x, y, z};
+                bytes_cls[x][y][z] = set_alg_bytes(3, m3);
+            }
+    const double wcls[4] = {0, 1, 1, 3};
+    std::vector<int> pref[4];  // pref[x][v]: class-x SNPs with index < v (v space)
+    for (int x = 1; x < 4; x++) {
+        pref[x].assign(ldg + 1, 0);
+        for (int v = 0; v < ldg; v++) pref[x][v + 1] = pref[x][v] + (cls(v) == x);
+    }
+    sets = 0; bytes = 0; configs = 0;
+    for (auto& u : mine) {
+        // T[x][y]: number of (a, b) pairs, a of class x in [a0, min(a1, b)), b of class y,
+        // accumulated over b in block K in increasing order; c must exceed b
+        double Tcum[4][4] = {{0}};
+        std::vector<std::array<double, 16>> upto(65);  // upto[i]: T over the first i b's of the block
+        for (int i = 0; i <= 64; i++) {
+            for (int x = 0; x < 4; x++)
+                for (int y = 0; y < 4; y++) upto[i][4 * x + y] = Tcum[x][y];
+            if (i == 64) break;
+            const int b = 64 * u.B + i, y = cls(b);
+            if (y == 0) continue;
+            const int ahi = std::min(u.a1, b);
+            if (ahi <= u.a0) continue;
+            for (int x = 1; x < 4; x++) Tcum[x][y] += pref[x][ahi] - pref[x][u.a0];
+        }
+        for (int t = 0; t < 64; t++) {
+            const int c = 64 * u.T + t, z = cls(c);
+            if (z == 0) continue;
+            // b < c: all of block K when K < C, else the first t b's
+            const auto& T = upto[u.B < u.T ? 64 : t];
+            for (int x = 1; x < 4; x++)
+                for (int y = 1; y < 4; y++) {
+                    const double n = T[4 * x + y];
+                    if (n == 0) continue;
+                    sets += n;
+                    bytes += n * bytes_cls[x][y][z];
+                    configs += n * wcls[x] * wcls[y] * wcls[z];
+                }
+        }
+    }
+    return 0;
+}
+
+// variant 1: the k = 3 fast kernel's decomposition (plan_units3c, v space);
+// variant 0: plan_units (k = 2, and the exact k = 3 rerun)
+static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, const unsigned char* pres_host,
+                      int variant) {
     P.k = k; P.U = U; P.ldg = ldg; P.rank = rank; P.world = world;
     std::vector<PlanUnit> mine;
     int ca = 0;
     double sets = 0, configs = 0, bytes = 0;
-    if (plan_units(k, U, ldg, rank, world, pres_host, mine, ca, sets, configs, bytes)) {
+    const int rc = variant ? plan_units3c(U, ldg, rank, world, pres_host, mine, ca, sets, configs, bytes)
+                           : plan_units(k, U, ldg, rank, world, pres_host, mine, ca, sets, configs, bytes);
+    if (rc) {
         g_sweep_err = "unsupported sweep level";
         return -1;
     }
@@ -540,13 +646,14 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     // FP64 operation estimate per union set (prefix, c-row
     // extension, split-exps, 3^k assignment folds and record folds)
     P.flops = sets * (k == 3 ? 900.0 : 260.0);
+    const int pad = variant ? ldg - U : 0;  // record keys of variant 1 are in v space
     // device buffers
     std::vector<int4> hu(P.n_units);
     for (int i = 0; i < P.n_units; i++) hu[i] = make_int4(mine[i].a0, mine[i].a1, mine[i].B, mine[i].T);
     if (P.n_units > 0) {
         SWCHK(hipMalloc(&P.d_units, sizeof(int4) * P.n_units));
         SWCHK(hipMemcpy(P.d_units, hu.data(), sizeof(int4) * P.n_units, hipMemcpyHostToDevice));
-        SWCHK(hipMalloc(&P.d_rec, sizeof(Acc5) * (size_t)P.n_units * P.rec_stride));
+
         SWCHK(hipMalloc(&P.d_srec, sizeof(SetRec) * (size_t)P.n_units));
     }
     // CSR: record -> SNP, grouped by SNP in record order (deterministic folds)
@@ -555,13 +662,13 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
         const PlanUnit& u = mine[i];
         int* kk = key.data() + (size_t)i * P.rec_stride;
         for (int t = 0; t < 64; t++) {
-            int c = 64 * u.T + t;
-            if (c < U) kk[t] = c;
-            int b = 64 * u.B + t;
-            if (b < U) kk[64 + t] = b;
+            int c = 64 * u.T + t - pad;
+            if (c >= 0 && c < U) kk[t] = c;
+            int b = 64 * u.B + t - pad;
+            if (b >= 0 && b < U) kk[64 + t] = b;
         }
         if (k == 3)
-            for (int a = u.a0; a < u.a1; a++) kk[128 + (a - u.a0)] = a;
+            for (int a = u.a0; a < u.a1; a++) kk[128 + (a - u.a0)] = a - pad;
     }
     std::vector<int> cnt(U, 0);
     for (int v : key) if (v >= 0) cnt[v]++;
@@ -575,13 +682,18 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     P.n_rows = (int)rows.size();
     P.csr_ptr_len = (int)ptr.size();
     P.csr_idx_len = (int)idx.size();
+    // kernels write record slot i straight to its CSR position pos[i] (-1: no SNP)
+    std::vector<int> pos(key.size(), -1);
+    for (size_t q = 0; q < idx.size(); q++) pos[idx[q]] = (int)q;
     std::vector<int> packed;
     packed.insert(packed.end(), ptr.begin(), ptr.end());
-    packed.insert(packed.end(), idx.begin(), idx.end());
     packed.insert(packed.end(), rows.begin(), rows.end());
+    packed.insert(packed.end(), pos.begin(), pos.end());
+    if (!idx.empty()) SWCHK(hipMalloc(&P.d_rec, sizeof(Acc5) * idx.size()));
     if (!packed.empty()) {
         SWCHK(hipMalloc(&P.d_csr, sizeof(int) * packed.size()));
         SWCHK(hipMemcpy(P.d_csr, packed.data(), sizeof(int) * packed.size(), hipMemcpyHostToDevice));
+        P.d_pos = P.d_csr + ptr.size() + rows.size();
     }
     return 0;
 }
@@ -590,6 +702,7 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
     if (C.d_skew[0] && C.skew_ldg == ldg && C.skew_src[0] == a.G0 && C.skew_src[1] == a.G1) return 0;
     for (int s = 0; s < 2; s++) {
         hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
+        hipFree(C.d_skewT[s]); C.d_skewT[s] = nullptr;
         hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
         hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
         hipFree(C.d_ys[s]); C.d_ys[s] = nullptr;
@@ -619,6 +732,8 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
     const int nblk = ldg / 64;
     const int ntile = nblk * (nblk + 1) / 2;
     for (int s = 0; s < 2; s++) {
+        SWCHK(hipMalloc(&C.d_skewT[s], sizeof(double) * (size_t)ntile * 4096));
+        if (launch_build_skewT(s ? a.G1 : a.G0, ldg, ldg - U, C.d_skewT[s], st)) SWCHK(hipGetLastError());
         SWCHK(hipMalloc(&C.d_skew[s], sizeof(double) * (size_t)ntile * 4096));
         hipLaunchKernelGGL(k_build_skew, dim3(ntile, 64), dim3(64), 0, st, s ? a.G1 : a.G0, ldg, nblk, C.d_skew[s]);
         SWCHK(hipGetLastError());
@@ -645,18 +760,23 @@ int sweep_flag(SweepPlanCache& C, int* flag) {
 int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, hipStream_t st, const SweepArgs& a,
                 Acc5* acc, SetRec* sacc, bool exact) {
     if (ensure_skew(C, a, ldg, U, st)) return -1;
-    auto key = std::make_tuple(k, U, rank, world);
+    const int variant = (k == 3 && !exact) ? 1 : 0;
+    auto key = std::make_tuple(k, U, rank, world, variant);
     auto it = C.plans.find(key);
     if (it == C.plans.end()) {
         std::vector<unsigned char> pres(ldg);
         SWCHK(hipMemcpy(pres.data(), a.pres, ldg, hipMemcpyDeviceToHost));
         SweepPlan P;
-        if (build_plan(P, k, U, ldg, rank, world, pres.data())) return -1;
+        if (build_plan(P, k, U, ldg, rank, world, pres.data(), variant)) return -1;
         for (int i = 0; i < 3; i++) SWCHK(hipEventCreate(&P.ev[i]));
         it = C.plans.emplace(key, P).first;
     }
     SweepPlan& P = it->second;
     P.ran = false;
+    {
+        auto other = C.plans.find(std::make_tuple(k, U, rank, world, 1 - variant));
+        if (other != C.plans.end()) other->second.ran = false;  // stats: the last pass only
+    }
     if (P.n_units == 0) return 0;
     TileArgs A;
     A.G[0] = a.G0; A.G[1] = a.G1;
@@ -677,28 +797,30 @@ int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, h
     if (k == 3 && !exact) {
         Sweep3Args S3;
         for (int s = 0; s < 2; s++) {
-            S3.G[s] = A.G[s]; S3.Ad[s] = A.Ad[s]; S3.ys[s] = C.d_ys[s]; S3.skew[s] = A.skew[s];
+            S3.G[s] = A.G[s]; S3.Ad[s] = A.Ad[s]; S3.ys[s] = C.d_ys[s]; S3.skewT[s] = C.d_skewT[s];
             S3.muS[s] = A.muS[s]; S3.nS[s] = A.nS[s]; S3.rsd[s] = A.rsd[s];
         }
+        S3.pad = ldg - U;
         S3.pres = A.pres;
         S3.tab = C.d_tab;
         S3.pit0 = A.pit[0];
         S3.rho = A.pit[0] > 0 ? A.pit[1] / A.pit[0] : 0.0;
         S3.U = U; S3.ldg = ldg; S3.Ck = A.Ck;
-        if (launch_sweep3(C.allpres, S3, P.n_units, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag, st))
+        if (launch_sweep3(C.allpres, S3, P.n_units, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag, P.d_pos, st))
             SWCHK(hipGetLastError());
     } else if (k == 3)
-        hipLaunchKernelGGL((k_sweep<3, true>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag);
+        hipLaunchKernelGGL((k_sweep<3, true>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag, P.d_pos);
     else if (!exact)
-        hipLaunchKernelGGL((k_sweep<2, false>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag);
+        hipLaunchKernelGGL((k_sweep<2, false>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag, P.d_pos);
     else
-        hipLaunchKernelGGL((k_sweep<2, true>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag);
+        hipLaunchKernelGGL((k_sweep<2, true>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag, P.d_pos);
     SWCHK(hipGetLastError());
     SWCHK(hipEventRecord(P.ev[1], st));
-    const int* ptr = P.d_csr;
-    const int* idx = P.d_csr + P.csr_ptr_len;
-    const int* rows = P.d_csr + P.csr_ptr_len + P.csr_idx_len;
-    if (launch_merge_members(P.d_rec, ptr, idx, rows, P.n_rows, acc, st)) return -1;
+    if (P.n_rows > 0) {
+        hipLaunchKernelGGL(k_merge_rows, dim3(P.n_rows), dim3(256), 0, st, P.d_rec, P.d_csr,
+                           P.d_csr + P.csr_ptr_len, acc);
+        SWCHK(hipGetLastError());
+    }
     SetRec none = set_zero();
     if (launch_merge_sets(P.d_srec, P.n_units, none, sacc, st)) return -1;
     SWCHK(hipEventRecord(P.ev[2], st));
@@ -707,10 +829,18 @@ int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, h
 }
 
 // After the stream has been synchronised: per-level statistics of the last run.
+int sweep_stats_plan(SweepPlan& P, int k, SweepStats* stats);
+
 int sweep_stats(SweepPlanCache& C, int k, int U, int rank, int world, SweepStats* stats) {
-    auto it = C.plans.find(std::make_tuple(k, U, rank, world));
-    if (it == C.plans.end() || !it->second.ran) return 0;
-    SweepPlan& P = it->second;
+    for (int variant = 0; variant < 2; variant++) {
+        auto it = C.plans.find(std::make_tuple(k, U, rank, world, variant));
+        if (it == C.plans.end() || !it->second.ran) continue;
+        if (sweep_stats_plan(it->second, k, stats)) return -1;
+    }
+    return 0;
+}
+
+int sweep_stats_plan(SweepPlan& P, int k, SweepStats* stats) {
     float k_ms = 0, m_ms = 0;
     SWCHK(hipEventElapsedTime(&k_ms, P.ev[0], P.ev[1]));
     SWCHK(hipEventElapsedTime(&m_ms, P.ev[1], P.ev[2]));
@@ -732,6 +862,7 @@ void sweep_free(SweepPlanCache& C) {
     C.plans.clear();
     for (int s = 0; s < 2; s++) {
         hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
+        hipFree(C.d_skewT[s]); C.d_skewT[s] = nullptr;
         hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
         hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
         hipFree(C.d_ys[s]); C.d_ys[s] = nullptr;

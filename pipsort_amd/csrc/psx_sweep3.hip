@@ -116,186 +116,195 @@ __device__ __forceinline__ Acc5 lacc_rec(const LAcc& a, int Ck, double pit0) {
     return r;
 }
 
+// Unit = (a-chunk [a0, a1), b-block K, c-chunk C), K <= C, in the padded index
+// space v = u + pad (the partial 64-block is the lowest one, where the sweep
+// has the least work).  Lane t owns c = 64C + t for the whole unit; at step j
+// it takes b = 64K + ((t + j) & 63), so the 64 b-slot accumulators rotate
+// through LDS without conflicts.  Per a, the {a,c} pivot (lane-owned) and the
+// {a,b} pivots of the 64 b's (lane-parallel, into LDS) are computed once; per
+// step only {b,c} and {a,b,c} are new.
+//
+// Pivot factors: P_T^{-1/2} = prod_i r_i rsd over the LDL^T pivots of T.  The
+// step computes r2x = 2 / sqrt(D), so the staged factors carry rsd / 2.
 template <bool ALLPRES>
 __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __restrict__ units,
                                                   Acc5* __restrict__ rec, SetRec* __restrict__ srec, int rec_stride,
-                                                  int* __restrict__ flag) {
+                                                  int* __restrict__ flag, const int* __restrict__ pos) {
     __shared__ double tab[256];
-    __shared__ double cA[2][64], cY[2][64], cMu[2][64], cR[2][64], gA[2][64];
-    __shared__ int cN[2][64];
-    __shared__ double cW[64];
+    // b-block terms (per unit) and (a, b) terms (per a), indexed [study][b slot]
+    __shared__ double bI[2][64], bYh[2][64], bH[2][64], bR[2][64];
+    __shared__ double abG[2][64], abD[2][64], abI[2][64], abW[2][64], abH[2][64], abR[2][64], abMu[2][64],
+        abMuB[2][64];
+    __shared__ int abN[2][64];
+    __shared__ double bW[64];
     __shared__ double sP0[64], sP1[64], sSh[64], sSl[64], sNs[64];
     __shared__ int sM[64];
 
     const int unit = blockIdx.x;
     const int t = threadIdx.x;
     const int4 un = units[unit];
-    const int a0 = un.x, a1 = un.y, B = un.z, T = un.w;
-    const int b = 64 * B + t;
-    const bool bvalid = b < A.U;
-    const int tile = T * (T + 1) / 2 + B;
-    const int ldg = A.ldg;
+    const int a0 = un.x, a1 = un.y, K = un.z, C = un.w;
+    const int pad = A.pad, ldg = A.ldg;
+    const int tile = C * (C + 1) / 2 + K;
     const double rho = A.rho;
 
-    // ---- unit prologue: stage the c-tile ------------------------------------------
+    // ---- unit prologue -------------------------------------------------------------
     for (int i = t; i < 256; i += 64) tab[i] = A.tab[i];
-    {
-        const int c = 64 * T + t;  // < ldg: arrays are padded to ldg
-        const unsigned pc = A.pres[c];
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const bool in = ALLPRES || ((pc >> s) & 1u);
-            cA[s][t] = A.Ad[s][c];
-            cY[s][t] = 0.5 * A.ys[s][c];  // halved: pivots come out as 2/sqrt(D)
-            cMu[s][t] = in ? A.muS[s][c] : 0.0;
-            cN[s][t] = A.nS[s][c];
-            cR[s][t] = in ? 0.5 * A.rsd[s] : 0.0;
-        }
-        cW[t] = memb_weight(pc);
-    }
-    sM[t] = EMPTY;
-    sP0[t] = sP1[t] = sSh[t] = sSl[t] = sNs[t] = 0.0;
-    __syncthreads();
-
-    // ---- per-lane b terms ------------------------------------------------------------
-    const unsigned pb = bvalid ? A.pres[b] : 0u;
-    // rP*X: pivot-factor products, times one more rsd when every SNP is in both
-    // studies (then the c pivot factor is r_c alone; otherwise r_c * cR[c])
-    double Abb[2], yb[2], ybh[2], iAbb[2], hb[2], rPb[2], rPbX[2], chib[2], muB[2];
-    int nB[2];
+    // this lane's b of the b-block (v-space; u = v - pad)
+    const int vbl = 64 * K + t, ubl = vbl - pad;
+    const bool okb = vbl >= pad;
+    const unsigned pbl = okb ? A.pres[ubl] : 0u;
+    double chib[2];
 #pragma unroll
     for (int s = 0; s < 2; s++) {
-        chib[s] = (ALLPRES || ((pb >> s) & 1u)) ? 1.0 : 0.0;
-        Abb[s] = A.Ad[s][b];
-        yb[s] = A.ys[s][b];
-        ybh[s] = 0.5 * yb[s];
-        const double r = rsqrt_nr(Abb[s]);
-        iAbb[s] = r * r;
-        hb[s] = yb[s] * yb[s] * iAbb[s];
-        rPb[s] = r * A.rsd[s] * chib[s];
-        rPbX[s] = ALLPRES ? rPb[s] * (0.5 * A.rsd[s]) : rPb[s];
-        split3(hb[s], rPb[s], tab, nB[s], muB[s]);
+        chib[s] = (okb && (ALLPRES || ((pbl >> s) & 1u))) ? 1.0 : 0.0;
+        const double Abb = okb ? A.Ad[s][ubl] : 1.0;
+        const double yb = okb ? A.ys[s][ubl] : 0.0;
+        const double r = rsqrt_nr(Abb);
+        bI[s][t] = r * r;
+        bYh[s][t] = 0.5 * yb;
+        bH[s][t] = yb * yb * r * r;
+        bR[s][t] = r * A.rsd[s] * chib[s] * (0.5 * A.rsd[s]);  // {b} factor x (c's rsd / 2)
     }
-    const double wb = memb_weight(pb);
+    bW[t] = memb_weight(pbl);
+    sM[t] = EMPTY;
+    sP0[t] = sP1[t] = sSh[t] = sSl[t] = sNs[t] = 0.0;
 
-    LAcc accB;
-    lacc_zero(accB);
-    double totB = 0.0;
+    // c terms: lane-owned for the whole unit
+    const int vc = 64 * C + t, uc = vc - pad;
+    const bool okc = vc >= pad;
+    const unsigned pcm = okc ? A.pres[uc] : 0u;
+    double Acc[2], yc[2], ych[2], chic[2], muC[2];
+    int nC[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        chic[s] = (okc && (ALLPRES || ((pcm >> s) & 1u))) ? 1.0 : 0.0;
+        Acc[s] = okc ? A.Ad[s][uc] : 1.0;
+        yc[s] = okc ? A.ys[s][uc] : 0.0;
+        ych[s] = 0.5 * yc[s];
+        muC[s] = okc ? A.muS[s][uc] * chic[s] : 0.0;
+        nC[s] = okc ? A.nS[s][uc] : 0;
+    }
+    const double wc = memb_weight(pcm);
+
+    LAcc accC;
+    lacc_zero(accC);
+    double totC = 0.0;
     int m0 = EMPTY, m1 = EMPTY;
     double nc0 = 0.0, nc1 = 0.0, npat = 0.0;
-
-    const double* sk0 = A.skew[0] + (size_t)tile * 4096 + t;
-    const double* sk1 = A.skew[1] + (size_t)tile * 4096 + t;
+    const double* sk0 = A.skewT[0] + (size_t)tile * 4096 + t;
+    const double* sk1 = A.skewT[1] + (size_t)tile * 4096 + t;
 
     for (int ai = 0; ai < a1 - a0; ai++) {
-        const int a = a0 + ai;
-        // Sigma~ row of a over the c-tile
-#pragma unroll
-        for (int s = 0; s < 2; s++) gA[s][t] = A.G[s][(size_t)a * ldg + 64 * T + t];
-        const unsigned pa = A.pres[a];
-        double iAaa[2], yah[2], rPaX[2], Gab[2], Dab[2], iDab[2], wabh[2], hab[2], ha[2], rPabX[2];
-        // c-free subsets relative to 2^{n_ab}: E'[0] = {}, [1] = {a}, [2] = {b}, [3] = {a,b}
-        double Ep[2][4];
-        int nAB[2];
+        const int va = a0 + ai, ua = va - pad;  // a0 >= pad: a is always a real SNP
+        const unsigned pa = A.pres[ua];
+        double l1[2], D1[2], w1h[2], Ep[2][4];  // Ep: {}, {a}, {c}, {a,c} relative to 2^{n_ac}
+        int R[2];
+        __syncthreads();  // previous a's (a, b) terms fully consumed
 #pragma unroll
         for (int s = 0; s < 2; s++) {
             const double chia = (ALLPRES || ((pa >> s) & 1u)) ? 1.0 : 0.0;
-            const double ra = rsqrt_nr(A.Ad[s][a]);
-            iAaa[s] = ra * ra;
-            const double ya = A.ys[s][a];
-            yah[s] = 0.5 * ya;
-            ha[s] = ya * ya * iAaa[s];
+            const double ya = A.ys[s][ua];
+            const double ra = rsqrt_nr(A.Ad[s][ua]);
+            const double iAaa = ra * ra;
+            const double ha = ya * ya * iAaa;
             const double rPa = ra * A.rsd[s] * chia;
-            rPaX[s] = ALLPRES ? rPa * (0.5 * A.rsd[s]) : rPa;
             int nA;
-            double muA, muAB;
-            split3(ha[s], rPa, tab, nA, muA);
-            Gab[s] = A.G[s][(size_t)a * ldg + b];
-            const double l = Gab[s] * iAaa[s];
-            Dab[s] = fma(-l, Gab[s], Abb[s]);
-            const double rab = rsqrt_nr(Dab[s]);
-            iDab[s] = rab * rab;
-            const double wab = fma(-l, ya, yb[s]);
-            wabh[s] = 0.5 * wab;
-            hab[s] = fma(wab * wab, iDab[s], ha[s]);
-            const double rPab = rPa * rab * A.rsd[s] * chib[s];
-            rPabX[s] = ALLPRES ? rPab * (0.5 * A.rsd[s]) : rPab;
-            split3(hab[s], rPab, tab, nAB[s], muAB);
-            // n_ab >= n_a, n_b (nested quadratic forms), so these never overflow; a
-            // term that underflows sits > 1022 bits below its set's {a,b} weight
-            Ep[s][0] = ldexp(1.0, -nAB[s]);
-            Ep[s][1] = ldexp(muA, nA - nAB[s]);
-            Ep[s][2] = ldexp(muB[s], nB[s] - nAB[s]);
-            Ep[s][3] = muAB;
+            double muA;
+            split3(ha, rPa, tab, nA, muA);
+            {
+                // {a, b} and {b} for this lane's b, into LDS
+                const double Gab = okb ? A.G[s][(size_t)ua * ldg + ubl] : 0.0;
+                const double Abb = okb ? A.Ad[s][ubl] : 1.0;
+                const double yb = okb ? A.ys[s][ubl] : 0.0;
+                const double l = Gab * iAaa;
+                const double Dab = fma(-l, Gab, Abb);
+                const double rab = rsqrt_nr(Dab);
+                const double wab = fma(-l, ya, yb);
+                const double hab = fma(wab * wab, rab * rab, ha);
+                const double rPab = rPa * rab * A.rsd[s] * chib[s];
+                int nAB, nB;
+                double muAB, muB;
+                split3(hab, rPab, tab, nAB, muAB);
+                split3(bH[s][t], bR[s][t] * (2.0 / A.rsd[s]), tab, nB, muB);
+                abG[s][t] = Gab;
+                abD[s][t] = Dab;
+                abI[s][t] = rab * rab;
+                abW[s][t] = 0.5 * wab;
+                abH[s][t] = hab;
+                abR[s][t] = rPab * (0.5 * A.rsd[s]);
+                abMu[s][t] = muAB;
+                abMuB[s][t] = ldexp(muB, nB - nAB);  // n_ab >= n_b: nested quadratic forms
+                abN[s][t] = nAB;
+            }
+            // {a, c}: lane-owned
+            const double Gac = okc ? A.G[s][(size_t)ua * ldg + uc] : 0.0;
+            l1[s] = Gac * iAaa;
+            D1[s] = fma(-l1[s], Gac, Acc[s]);
+            const double w1 = fma(-l1[s], ya, yc[s]);
+            w1h[s] = 0.5 * w1;
+            const double r1 = rsqrt_nr(D1[s]);
+            const double h1 = fma(w1 * w1, r1 * r1, ha);
+            const double rP1 = rPa * r1 * A.rsd[s] * chic[s];
+            int n1;
+            double mu1;
+            split3(h1, rP1, tab, n1, mu1);
+            // {}, {a}, {c} never exceed {a,c} (nested forms), so these cannot overflow
+            R[s] = n1;
+            Ep[s][0] = ldexp(1.0, -n1);
+            Ep[s][1] = ldexp(muA, nA - n1);
+            Ep[s][2] = ldexp(muC[s], nC[s] - n1);
+            Ep[s][3] = mu1;
         }
-        const bool abvalid = bvalid && a < b;
-        const double wab_cnt = wb * memb_weight(pa);
+        const double wac = wc * memb_weight(pa);
         LAcc accA;
         lacc_zero(accA);
-        __syncthreads();  // gA visible
+        __syncthreads();  // (a, b) terms visible
 
         for (int j = 0; j < 64; j++) {
-            const int cc = (t + j) & 63;
-            const int c = 64 * T + cc;
-            const bool act = abvalid && c < A.U && (B < T || cc > t);
+            const int bs = (t + j) & 63;
+            const int vb = 64 * K + bs;
+            const bool act = okc && vb > va && vb < vc;
             if (act) {
                 double E[2][8];
                 int nb[2];
 #pragma unroll
                 for (int s = 0; s < 2; s++) {
-                    const double Acc_ = cA[s][cc];
-                    const double yc = cY[s][cc];
                     const double Gbc = (s ? sk1 : sk0)[j * 64];
-                    const double Gac = gA[s][cc];
                     // {b, c}
-                    const double l2 = Gbc * iAbb[s];
-                    const double D2 = fma(-l2, Gbc, Acc_);
-                    const double w2 = fma(-l2, ybh[s], yc);
+                    const double l2 = Gbc * bI[s][bs];
+                    const double D2 = fma(-l2, Gbc, Acc[s]);
+                    const double w2 = fma(-l2, bYh[s][bs], ych[s]);
                     const double r2 = rsq2x(D2);
                     const double t2 = w2 * r2;
-                    const double h2 = fma(t2, t2, hb[s]);
-                    // {a, c}
-                    const double l1 = Gac * iAaa[s];
-                    const double D1 = fma(-l1, Gac, Acc_);
-                    const double w1 = fma(-l1, yah[s], yc);
-                    const double r1 = rsq2x(D1);
-                    const double t1 = w1 * r1;
-                    const double h1 = fma(t1, t1, ha[s]);
+                    const double h2 = fma(t2, t2, bH[s][bs]);
                     // {a, b, c}: extend the (a, b) factor by the c row
-                    const double lcb = fma(-l1, Gab[s], Gbc) * iDab[s];
-                    const double u3 = lcb * Dab[s];
-                    const double D3 = fma(-u3, lcb, D1);
-                    const double w3 = fma(-lcb, wabh[s], w1);
+                    const double lcb = fma(-l1[s], abG[s][bs], Gbc) * abI[s][bs];
+                    const double u3 = lcb * abD[s][bs];
+                    const double D3 = fma(-u3, lcb, D1[s]);
+                    const double w3 = fma(-lcb, abW[s][bs], w1h[s]);
                     const double r3 = rsq2x(D3);
                     const double t3 = w3 * r3;
-                    const double h3 = fma(t3, t3, hab[s]);
-                    double rP2, rP1, rP3;
-                    if (ALLPRES) {
-                        rP2 = rPbX[s] * r2;
-                        rP1 = rPaX[s] * r1;
-                        rP3 = rPabX[s] * r3;
-                    } else {
-                        const double rc = cR[s][cc];  // rsd_s, or 0 when c is absent from study s
-                        rP2 = rPbX[s] * (r2 * rc);
-                        rP1 = rPaX[s] * (r1 * rc);
-                        rP3 = rPabX[s] * (r3 * rc);
+                    const double h3 = fma(t3, t3, abH[s][bs]);
+                    double rP2 = bR[s][bs] * r2, rP3 = abR[s][bs] * r3;
+                    if (!ALLPRES) {
+                        rP2 *= chic[s];
+                        rP3 *= chic[s];
                     }
-                    int n1, n2, n3;
-                    double mu1, mu2, mu3;
+                    int n2, n3;
+                    double mu2, mu3;
                     split3(h2, rP2, tab, n2, mu2);
-                    split3(h1, rP1, tab, n1, mu1);
                     split3(h3, rP3, tab, n3, mu3);
-                    const int nbs = n3;
-                    nb[s] = nbs;
-                    // subset weights relative to 2^nb (bit 0 = a, bit 1 = b, bit 2 = c)
-                    const int dd = nAB[s] - nbs;
-                    E[s][0] = ldexp(Ep[s][0], dd);
-                    E[s][1] = ldexp(Ep[s][1], dd);
-                    E[s][2] = ldexp(Ep[s][2], dd);
-                    E[s][3] = ldexp(Ep[s][3], dd);
-                    E[s][4] = ldexp(cMu[s][cc], cN[s][cc] - nbs);
-                    E[s][5] = ldexp(mu1, n1 - nbs);
-                    E[s][6] = ldexp(mu2, n2 - nbs);
+                    nb[s] = n3;
+                    // subset weights relative to 2^n_abc (bit 0 = a, bit 1 = b, bit 2 = c)
+                    const int dR = R[s] - n3, dAB = abN[s][bs] - n3;
+                    E[s][0] = ldexp(Ep[s][0], dR);
+                    E[s][1] = ldexp(Ep[s][1], dR);
+                    E[s][2] = ldexp(abMuB[s][bs], dAB);
+                    E[s][3] = ldexp(abMu[s][bs], dAB);
+                    E[s][4] = ldexp(Ep[s][2], dR);
+                    E[s][5] = ldexp(Ep[s][3], dR);
+                    E[s][6] = ldexp(mu2, n2 - n3);
                     E[s][7] = mu3;
                 }
                 const int Gll = nb[0] + nb[1];
@@ -354,21 +363,21 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
                 if (__builtin_amdgcn_ballot_w64((nsA < kTinyNs) | (nsB < kTinyNs) | (nsC < kTinyNs)))
                     if (nsA < kTinyNs || nsB < kTinyNs || nsC < kTinyNs) atomicOr(flag, 1);
                 const bool nz = tot != 0.0;
-                // ---- folds: a, b (registers), c (LDS slot, rotating owner), noCausal ----
+                // ---- folds: a, c (registers), b (LDS slot, rotating owner), noCausal ----
                 LAcc sl;
-                sl.m = sM[cc];
-                sl.p0 = sP0[cc];
-                sl.p1 = sP1[cc];
-                sl.sh = sSh[cc];
-                sl.sl = sSl[cc];
-                sl.ns = sNs[cc];
-                int dA = Gll - accA.m, dB = Gll - accB.m, dS = Gll - sl.m;
+                sl.m = sM[bs];
+                sl.p0 = sP0[bs];
+                sl.p1 = sP1[bs];
+                sl.sh = sSh[bs];
+                sl.sl = sSl[bs];
+                sl.ns = sNs[bs];
+                int dA = Gll - accA.m, dC = Gll - accC.m, dS = Gll - sl.m;
                 // noCausal[s]: the assignment with C_s empty (every member in the other study)
                 double x0 = ldexp(E[1][7], nb[1] - m0), x1 = ldexp(E[0][7], nb[0] - m1);
-                const bool up = (nz & (max(dA, max(dB, dS)) > 960)) | (x0 > 0x1p960) | (x1 > 0x1p960);
+                const bool up = (nz & (max(dA, max(dC, dS)) > 960)) | (x0 > 0x1p960) | (x1 > 0x1p960);
                 if (__builtin_amdgcn_ballot_w64(up)) {  // wave-uniform, rare: move shifts up
                     if (nz && dA > 960) { lacc_shift(accA, Gll); dA = 0; }
-                    if (nz && dB > 960) { lacc_shift(accB, Gll); totB = ldexp(totB, -dB); dB = 0; }
+                    if (nz && dC > 960) { lacc_shift(accC, Gll); totC = ldexp(totC, -dC); dC = 0; }
                     if (nz && dS > 960) { lacc_shift(sl, Gll); dS = 0; }
                     if (x0 > 0x1p960) { nc0 = ldexp(nc0, m0 - nb[1]); m0 = nb[1]; x0 = E[1][7]; }
                     if (x1 > 0x1p960) { nc1 = ldexp(nc1, m1 - nb[0]); m1 = nb[0]; x1 = E[0][7]; }
@@ -376,24 +385,29 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
                 nc0 += x0;
                 nc1 += x1;
                 lacc_add(accA, ldexp(1.0, min(dA, 1000)), SwA[0] + SwA[2], SwA[1] + SwA[2], SwA[2], sllA, nsA);
-                const double fB = ldexp(1.0, min(dB, 1000));
-                lacc_add(accB, fB, SwB[0] + SwB[2], SwB[1] + SwB[2], SwB[2], sllB, nsB);
-                totB = fma(tot, fB, totB);
-                lacc_add(sl, ldexp(1.0, min(dS, 1000)), SwC[0] + SwC[2], SwC[1] + SwC[2], SwC[2], sllC, nsC);
-                sM[cc] = sl.m;
-                sP0[cc] = sl.p0;
-                sP1[cc] = sl.p1;
-                sSh[cc] = sl.sh;
-                sSl[cc] = sl.sl;
-                sNs[cc] = sl.ns;
-                npat += ALLPRES ? 27.0 : wab_cnt * cW[cc];
+                lacc_add(sl, ldexp(1.0, min(dS, 1000)), SwB[0] + SwB[2], SwB[1] + SwB[2], SwB[2], sllB, nsB);
+                const double fC = ldexp(1.0, min(dC, 1000));
+                lacc_add(accC, fC, SwC[0] + SwC[2], SwC[1] + SwC[2], SwC[2], sllC, nsC);
+                totC = fma(tot, fC, totC);
+                sM[bs] = sl.m;
+                sP0[bs] = sl.p0;
+                sP1[bs] = sl.p1;
+                sSh[bs] = sl.sh;
+                sSl[bs] = sl.sl;
+                sNs[bs] = sl.ns;
+                npat += ALLPRES ? 27.0 : wac * bW[bs];
             }
-            __syncthreads();  // slot ownership rotates across lanes every step
+            // b-slot ownership rotates across lanes every step: the workgroup is one
+            // wave and LDS executes a wave's instructions in issue order, so only the
+            // compiler must keep program order (no lgkmcnt drain per step)
+            __builtin_amdgcn_wave_barrier();
         }
         Acc5 ra = lacc_rec(accA, A.Ck, A.pit0);
         wave_fold_acc(ra);
-        if (t == 0) rec[(size_t)unit * rec_stride + 128 + ai] = ra;
+        if (t == 0) put_rec(rec, pos, (size_t)unit * rec_stride + 128 + ai, ra);
     }
+    __syncthreads();
+    put_rec(rec, pos, (size_t)unit * rec_stride + t, lacc_rec(accC, A.Ck, A.pit0));
     {
         LAcc sl;
         sl.m = sM[t];
@@ -402,12 +416,11 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
         sl.sh = sSh[t];
         sl.sl = sSl[t];
         sl.ns = sNs[t];
-        rec[(size_t)unit * rec_stride + t] = lacc_rec(sl, A.Ck, A.pit0);
+        put_rec(rec, pos, (size_t)unit * rec_stride + 64 + t, lacc_rec(sl, A.Ck, A.pit0));
     }
-    rec[(size_t)unit * rec_stride + 64 + t] = lacc_rec(accB, A.Ck, A.pit0);
     SetRec sr;
-    sr.tot = totB * A.pit0;
-    sr.m = (sr.tot != 0.0) ? accB.m + A.Ck : EMPTY;
+    sr.tot = totC * A.pit0;
+    sr.m = (sr.tot != 0.0) ? accC.m + A.Ck : EMPTY;
     sr.nc0 = nc0 * A.pit0;
     sr.m0 = (sr.nc0 != 0.0) ? m0 + A.Ck : EMPTY;
     sr.nc1 = nc1 * A.pit0;
@@ -419,12 +432,31 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
     if (t == 0) srec[unit] = sr;
 }
 
+// skewT[tile(K, C)][j][t] = G~[64C + t][64K + ((t + j) & 63)] for K <= C, in the
+// padded index space v = u + pad (zero where either index is padding)
+__global__ void k_build_skewT(const double* __restrict__ G, int ldg, int pad, double* __restrict__ skew) {
+    const int tile = blockIdx.x;
+    const int j = blockIdx.y;
+    const int t = threadIdx.x;
+    int C = 0;
+    while ((C + 1) * (C + 2) / 2 <= tile) C++;
+    const int K = tile - C * (C + 1) / 2;
+    const int v = 64 * C + t, w = 64 * K + ((t + j) & 63);
+    skew[(size_t)tile * 4096 + j * 64 + t] = (v >= pad && w >= pad) ? G[(size_t)(v - pad) * ldg + (w - pad)] : 0.0;
+}
+
+int launch_build_skewT(const double* G, int ldg, int pad, double* skew, hipStream_t st) {
+    const int nblk = ldg / 64;
+    hipLaunchKernelGGL(k_build_skewT, dim3(nblk * (nblk + 1) / 2, 64), dim3(64), 0, st, G, ldg, pad, skew);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_sweep3(bool allpres, const Sweep3Args& A, int n_units, const int4* units, Acc5* rec, SetRec* srec,
-                  int rec_stride, int* flag, hipStream_t st) {
+                  int rec_stride, int* flag, const int* pos, hipStream_t st) {
     if (allpres)
-        hipLaunchKernelGGL((k_sweep3<true>), dim3(n_units), dim3(64), 0, st, A, units, rec, srec, rec_stride, flag);
+        hipLaunchKernelGGL((k_sweep3<true>), dim3(n_units), dim3(64), 0, st, A, units, rec, srec, rec_stride, flag, pos);
     else
-        hipLaunchKernelGGL((k_sweep3<false>), dim3(n_units), dim3(64), 0, st, A, units, rec, srec, rec_stride, flag);
+        hipLaunchKernelGGL((k_sweep3<false>), dim3(n_units), dim3(64), 0, st, A, units, rec, srec, rec_stride, flag, pos);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -127,6 +127,12 @@ __device__ __forceinline__ void split2(double h, double rP, int& n, double& mu) 
     mu = exp2_frac(h - fl) * rP;
 }
 
+// record slot i goes to its CSR position pos[i] (merges then read contiguous runs)
+__device__ __forceinline__ void put_rec(Acc5* rec, const int* pos, size_t i, const Acc5& v) {
+    const int q = pos[i];
+    if (q >= 0) rec[q] = v;
+}
+
 __device__ __forceinline__ double memb_weight(unsigned p) { return p == 3u ? 3.0 : (p ? 1.0 : 0.0); }
 
 }  // namespace psx
