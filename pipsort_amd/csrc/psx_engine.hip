@@ -9,6 +9,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <map>
@@ -21,6 +22,7 @@
 #include "../../include/pipsort_engine.h"
 #include "psx_math.h"
 #include "psx_sweep.h"
+#include "psx_sweep_dev.h"
 
 using psx::Acc5;
 using psx::SetRec;
@@ -282,6 +284,131 @@ __global__ void k_merge_partials(const Acc5* __restrict__ parts, int U, int ldg,
     }
 }
 
+// Level 1 for one union SNP u, per thread: k_eval_sets with k = 1 written out
+// (subsets {} and {u} per study; assignments x in {study0, study1, both}
+// filtered by presence, postcal.cpp:907-955), same arithmetic and fold order.
+__device__ void eval_single(const DevProb& P, int u, Acc5& a, SetRec& r) {
+    const unsigned pr = P.pres[u];
+    const int S0 = pr & 1u, S1 = (pr >> 1) & 1u;
+    double mu[2][2], f[2][2];
+    int n[2][2];
+    for (int s = 0; s < 2; s++) {
+        mu[s][0] = 1.0;
+        n[s][0] = 0;
+        f[s][0] = 0.0;
+        double q, Pd;
+        psx::ldlt_terms(P.G[s], P.ldg, P.Ad[s], P.y[s], P.dval[s], &u, 1, q, Pd);
+        psx::split_exp(0.5 * q * PSX_LOG2E, 1.0 / sqrt(Pd), n[s][1], mu[s][1]);
+        f[s][1] = 0.5 * q - 0.5 * log(Pd);
+    }
+    const int Ck = P.Ck[1];
+    const int Gll = n[0][S0] + n[1][S1] + 2;
+    const int GN = psx::imax(n[0][S0] + n[1][0], n[0][0] + n[1][S1]) + 2;
+    const int GS = Gll + Ck;
+    const int Gnc0 = n[1][S1] + Ck, Gnc1 = n[0][S0] + Ck;
+    double tot = 0, nc0 = 0, nc1 = 0, smin = 1e300, npat = 0;
+    double p0 = 0, p1 = 0, sh = 0, sl = 0, ns = 0;
+    for (int x = 1; x <= 3; x++) {
+        const int c0 = x & 1, c1 = (x >> 1) & 1;
+        if ((c0 & ~S0) || (c1 & ~S1)) continue;
+        const int nsh = c0 & c1;
+        const double mup = mu[0][c0] * mu[1][c1];
+        const int np = n[0][c0] + n[1][c1];
+        const double wll = ldexp(mup, np - Gll);
+        const double w = wll * P.pit[1][nsh];
+        npat += 1.0;
+        tot += w;
+        if (c0 == 0) nc0 += ldexp(mup * P.pit[1][0], np - (Gnc0 - Ck));
+        if (c1 == 0) nc1 += ldexp(mup * P.pit[1][0], np - (Gnc1 - Ck));
+        smin = fmin(smin, f[0][c0] + f[1][c1] + P.prior[1][nsh]);
+        if (x & 1) p0 += w;
+        if (x & 2) p1 += w;
+        if (x == 3) {
+            sh += w;
+            sl += wll;
+        } else {
+            ns += ldexp(mup, np - GN);
+        }
+    }
+    a.mP = GS; a.mS = Gll; a.mN = GN; a.pad = 0;
+    a.post0 = p0; a.post1 = p1; a.shared = sh; a.sll = sl; a.nsll = ns;
+    r = psx::set_zero();
+    r.m = GS; r.m0 = Gnc0; r.m1 = Gnc1;
+    r.tot = tot; r.nc0 = nc0; r.nc1 = nc1; r.score = smin; r.npat = npat;
+}
+
+// The whole-pass merge of the fused exhaustive pass, with level 1 folded in.
+//   block 0:     scalars = extra (null configuration) + level-1 sets of this
+//                shard + every tiled-level unit record (srec[0, nsrec))
+//   block 1 + u: acc[u] = level-1 record of u (if in this shard), then u's
+//                records of level A and level B (dense per-SNP runs)
+// Fixed fold order: deterministic.
+__global__ __launch_bounds__(256) void k_merge_pass_l1(DevProb P, int lo, int hi, const Acc5* __restrict__ recA,
+                                                       const int* __restrict__ dptrA, const Acc5* __restrict__ recB,
+                                                       const int* __restrict__ dptrB, const SetRec* __restrict__ srec,
+                                                       long nsrec, SetRec extra, Acc5* __restrict__ acc,
+                                                       SetRec* __restrict__ sacc, int* __restrict__ flag) {
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0) {
+        __shared__ SetRec ss[4];
+        SetRec a = psx::set_zero();
+        for (int u = lo + tid; u < hi; u += 256) {
+            Acc5 dummy;
+            SetRec r;
+            eval_single(P, u, dummy, r);
+            psx::fold_set(a, r);
+        }
+        long i = tid;
+        for (; i + 768 < nsrec; i += 1024) {  // four independent loads in flight per thread
+            const SetRec r0 = srec[i], r1 = srec[i + 256], r2 = srec[i + 512], r3 = srec[i + 768];
+            psx::fold_set(a, r0); psx::fold_set(a, r1); psx::fold_set(a, r2); psx::fold_set(a, r3);
+        }
+        for (; i < nsrec; i += 256) psx::fold_set(a, srec[i]);
+        psx::wave_fold_set(a);
+        if ((tid & 63) == 0) ss[tid >> 6] = a;
+        __syncthreads();
+        if (tid == 0) {
+            SetRec g = psx::set_zero();
+            psx::fold_set(g, extra);
+            for (int w = 0; w < 4; w++) psx::fold_set(g, ss[w]);
+            // hand the pass's EXACT flag to the host in the status record and re-arm
+            // it for the next pass (the kernels that raise it have completed)
+            g.pad = *flag;
+            *flag = 0;
+            *sacc = g;
+        }
+        return;
+    }
+    __shared__ Acc5 sh[4];
+    const int u = blockIdx.x - 1;
+    if (u >= P.U) return;
+    const int a0 = dptrA ? dptrA[u] : 0, na = dptrA ? dptrA[u + 1] - a0 : 0;
+    const int b0 = dptrB ? dptrB[u] : 0, nb = dptrB ? dptrB[u + 1] - b0 : 0;
+    const int n = na + nb;
+    Acc5 a = psx::acc_zero();
+    int i = tid;
+    for (; i + 256 < n; i += 512) {  // two independent loads in flight per thread
+        const Acc5 x0 = i < na ? recA[a0 + i] : recB[b0 + i - na];
+        const int j = i + 256;
+        const Acc5 x1 = j < na ? recA[a0 + j] : recB[b0 + j - na];
+        psx::fold_acc(a, x0);
+        psx::fold_acc(a, x1);
+    }
+    for (; i < n; i += 256) psx::fold_acc(a, i < na ? recA[a0 + i] : recB[b0 + i - na]);
+    psx::wave_fold_acc(a);
+    if ((tid & 63) == 0) sh[tid >> 6] = a;
+    __syncthreads();
+    if (tid == 0) {
+        Acc5 g = {0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        if (u >= lo && u < hi) {
+            SetRec dummy;
+            eval_single(P, u, g, dummy);
+        }
+        for (int w = 0; w < 4; w++) psx::fold_acc(g, sh[w]);
+        acc[u] = g;
+    }
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -307,10 +434,16 @@ struct psx_engine {
     double* dAd[2] = {nullptr, nullptr};
     double* dy[2] = {nullptr, nullptr};
     unsigned char* dpres = nullptr;
+    // accumulator image, one allocation of ldg + 2 slots: per-SNP Acc5[ldg], then
+    // the SetRec scalars (slot ldg), then the status word (EXACT flag, slot ldg+1);
+    // the first ldg + 1 slots are the exported partial image
     Acc5* dacc = nullptr;
-    SetRec* dsacc = nullptr;   // status block: SetRec, then the EXACT flag (int)
-    int* dflag = nullptr;
+    SetRec* dsacc = nullptr;   // = slot ldg
+    int* dflag = nullptr;      // = slot ldg + 1
     unsigned char* hstat = nullptr;  // pinned host copy of the status block
+    // fused exhaustive pass: every unit set record of the pass in one buffer
+    SetRec* dpass = nullptr;
+    size_t cap_pass = 0;
     // sweep workspace (tiled kernel)
     psx::SweepPlanCache plans;
     // generic workspace
@@ -348,9 +481,9 @@ struct psx_engine {
 psx_engine::~psx_engine() {
     hipSetDevice(dev);
     for (int s = 0; s < 2; s++) { hipFree(dG[s]); hipFree(dAd[s]); hipFree(dy[s]); }
-    hipFree(dpres); hipFree(dacc); hipFree(dsacc);
+    hipFree(dpres); hipFree(dacc);
     if (hstat) hipHostFree(hstat);
-    hipFree(dsets); hipFree(dforced); hipFree(dsrec); hipFree(dmrec); hipFree(dcsr);
+    hipFree(dsets); hipFree(dforced); hipFree(dsrec); hipFree(dmrec); hipFree(dcsr); hipFree(dpass);
     psx::sweep_free(plans);
     for (auto& kv : glevels) {
         GenLevel& g = kv.second;
@@ -617,7 +750,7 @@ int enqueue_generic_level(psx_engine* e, int k) {
 // (set i of this shard is SNP lo + i), so they are written in place into the
 // zeroed dacc; the set records initialise the scalars together with `extra`
 // (the null configuration on rank 0) and the EXACT flag is cleared.
-int enqueue_level1(psx_engine* e, const SetRec& extra) {
+int get_level1(psx_engine* e, psx_engine::GenLevel** out) {
     auto key = std::make_tuple(1, e->rank, e->world);
     auto it = e->glevels.find(key);
     if (it == e->glevels.end()) {
@@ -635,7 +768,15 @@ int enqueue_level1(psx_engine* e, const SetRec& extra) {
         for (int i = 0; i < 2; i++) HIPCHK(hipEventCreate(&g.ev[i]));
         it = e->glevels.emplace(key, g).first;
     }
-    psx_engine::GenLevel& g = it->second;
+    *out = &it->second;
+    return 0;
+}
+
+int enqueue_level1(psx_engine* e, const SetRec& extra) {
+    psx_engine::GenLevel* gp = nullptr;
+    int rc = get_level1(e, &gp);
+    if (rc) return rc;
+    psx_engine::GenLevel& g = *gp;
     HIPCHK(hipEventRecord(g.ev[0], e->stream));
     if (g.nsets)
         hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)g.nsets), dim3(64), 0, e->stream, e->dp, g.d_sets, 1,
@@ -681,6 +822,62 @@ int exhaustive_pass(psx_engine* e, bool exact, double* generic_ms) {
         }
     }
     *generic_ms = kms;
+    return 0;
+}
+
+psx::SweepArgs sweep_args(psx_engine* e) {
+    return psx::SweepArgs{e->dG[0], e->dG[1], e->dAd[0], e->dAd[1], e->dy[0], e->dy[1], e->dpres,
+                          e->dval[0], e->dval[1], e->dp.Ck, &e->dp.pit[0][0], PSX_KMAX + 1};
+}
+
+// The fused pass is the shape of every BASELINE config: c in {2, 3}, all
+// levels >= 2 on the tiled sweep.
+bool fused_eligible(const psx_engine* e) {
+    return (e->maxc == 2 || e->maxc == 3) && psx::sweep_supports(2, e->U) && psx::sweep_supports(e->maxc, e->U);
+}
+
+// One exhaustive pass with the fast kernels and a single merge, four device
+// operations on one stream:
+//   zero image + flag | top level (k = c) | level 2 (c = 3) | merge (+ level 1) | status copy
+// The dominant kernel is the second call the host makes, level 1 is computed
+// inside the merge (it is one 1x1 factor per SNP), and all record folds (per
+// SNP: level 1, then 2, then 3; scalars: null configuration, level-1 sets,
+// every unit record) are one launch.  Deterministic: the fold order is fixed
+// by the plans, not by scheduling.
+int fused_pass(psx_engine* e, int* flag) {
+    const psx::SweepArgs sa = sweep_args(e);
+    psx::SweepPlan* P2 = nullptr;
+    psx::SweepPlan* P3 = nullptr;
+    if (psx::sweep_prepare(e->plans, 2, e->U, e->ldg, e->rank, e->world, e->stream, sa, false, &P2) ||
+        (e->maxc == 3 && psx::sweep_prepare(e->plans, 3, e->U, e->ldg, e->rank, e->world, e->stream, sa, false, &P3)))
+        return fail(PSX_EHIP, std::string("sweep plan: ") + psx::sweep_error());
+    psx::SweepPlan* top = P3 ? P3 : P2;
+    psx::SweepPlan* low = P3 ? P2 : nullptr;
+    const size_t nl = low ? (size_t)low->n_units : 0, nt = (size_t)top->n_units;
+    int rc;
+    if ((rc = ensure(e->dpass, e->cap_pass, nl + nt + 1))) return rc;
+    hipStream_t A = e->stream;
+    // no zeroing pass: the merge overwrites every per-SNP slot and the scalars,
+    // padding slots stay zero from psx_create, and the EXACT flag was re-armed
+    // by the previous merge (or psx_create)
+    HIPCHK(hipEventRecord(e->ev[0], A));
+    // the top level; level 2 (c = 3) rides in the same launch
+    if (psx::sweep_kernel(e->plans, *top, A, sa, e->dpass + nl, false, low, e->dpass))
+        return fail(PSX_EHIP, std::string("sweep level ") + std::to_string(top->k) + ": " + psx::sweep_error());
+    const int lo = (int)((int64_t)e->U * e->rank / e->world), hi = (int)((int64_t)e->U * (e->rank + 1) / e->world);
+    const SetRec extra = e->rank == 0 ? null_rec(e, 1.0) : psx::set_zero();
+    const psx::SweepPlan* mA = low ? low : top;
+    const psx::SweepPlan* mB = low ? top : nullptr;
+    hipLaunchKernelGGL(k_merge_pass_l1, dim3(e->U + 1), dim3(256), 0, A, e->dp, lo, hi, mA->d_rec, mA->d_dptr,
+                       mB ? mB->d_rec : nullptr, mB ? mB->d_dptr : nullptr, e->dpass, (long)(nl + nt), extra,
+                       e->dacc, e->dsacc, e->dflag);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e->ev[1], A));
+    HIPCHK(hipMemcpyAsync(e->hstat, e->dsacc, kStatBytes, hipMemcpyDeviceToHost, A));
+    HIPCHK(hipStreamSynchronize(A));
+    SetRec s;
+    std::memcpy(&s, e->hstat, sizeof(SetRec));
+    *flag = s.pad;
     return 0;
 }
 
@@ -832,10 +1029,13 @@ int psx_create(const psx_problem* p, int device, psx_engine** out) {
         soff += M;
     }
     cleanup();
-    if (hipMalloc(&e->dpres, e->ldg) != hipSuccess || hipMalloc(&e->dacc, sizeof(Acc5) * e->ldg) != hipSuccess ||
-        hipMalloc(&e->dsacc, kStatBytes) != hipSuccess || hipHostMalloc(&e->hstat, kStatBytes) != hipSuccess)
+    if (hipMalloc(&e->dpres, e->ldg) != hipSuccess ||
+        hipMalloc(&e->dacc, sizeof(Acc5) * ((size_t)e->ldg + 2)) != hipSuccess ||
+        hipHostMalloc(&e->hstat, kStatBytes) != hipSuccess)
         return bail(fail(PSX_EHIP, "out of device memory"));
-    e->dflag = (int*)((char*)e->dsacc + sizeof(SetRec));
+    static_assert(sizeof(SetRec) == sizeof(Acc5), "SetRec occupies one image slot");
+    e->dsacc = reinterpret_cast<SetRec*>(e->dacc + e->ldg);
+    e->dflag = reinterpret_cast<int*>(e->dacc + e->ldg + 1);
     e->plans.d_flag = e->dflag;
     e->plans.own_flag = false;
     hipMemcpyAsync(e->dpres, e->pres.data(), e->ldg, hipMemcpyHostToDevice, e->stream);
@@ -845,6 +1045,8 @@ int psx_create(const psx_problem* p, int device, psx_engine** out) {
         dp.y[s] = e->dy[s];
     }
     dp.pres = e->dpres;
+    if (hipMemsetAsync(e->dacc, 0, sizeof(Acc5) * ((size_t)e->ldg + 2), e->stream) != hipSuccess)
+        return bail(fail(PSX_EHIP, "memset"));
     if (reset_acc(e)) return bail(PSX_EHIP);
     if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(fail(PSX_EHIP, "create sync"));
     std::memset(&e->timing, 0, sizeof(e->timing));
@@ -874,8 +1076,13 @@ int psx_run_exhaustive(psx_engine* e) {
     int rc;
     std::memset(&e->timing, 0, sizeof(e->timing));
     double gms = 0;
-    if ((rc = exhaustive_pass(e, false, &gms))) return rc;
-    int flag = *(const int*)(e->hstat + sizeof(SetRec));
+    int flag = 0;
+    if (fused_eligible(e) && !std::getenv("PSX_NO_FUSED_PASS")) {
+        if ((rc = fused_pass(e, &flag))) return rc;
+    } else {
+        if ((rc = exhaustive_pass(e, false, &gms))) return rc;
+        flag = *(const int*)(e->hstat + sizeof(SetRec));
+    }
     if (flag) {  // some set's notSharedLL group sits > 900 bits below its maximum: exact variant
         if ((rc = exhaustive_pass(e, true, &gms))) return rc;
     }
@@ -1189,9 +1396,8 @@ int64_t psx_partials_bytes(psx_engine* e) { return (int64_t)(sizeof(Acc5) * ((si
 
 int psx_export_partials(psx_engine* e, void* dst) {
     HIPCHK(hipSetDevice(e->dev));
-    char* d = (char*)dst;
-    HIPCHK(hipMemcpyAsync(d, e->dacc, sizeof(Acc5) * e->ldg, hipMemcpyDeviceToDevice, e->stream));
-    HIPCHK(hipMemcpyAsync(d + sizeof(Acc5) * e->ldg, e->dsacc, sizeof(SetRec), hipMemcpyDeviceToDevice, e->stream));
+    // per-SNP slots and the SetRec slot are contiguous: the image is one copy
+    HIPCHK(hipMemcpyAsync(dst, e->dacc, sizeof(Acc5) * ((size_t)e->ldg + 1), hipMemcpyDeviceToDevice, e->stream));
     if (!e->external_stream) HIPCHK(hipStreamSynchronize(e->stream));
     return 0;
 }

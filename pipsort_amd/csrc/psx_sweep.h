@@ -49,7 +49,10 @@ struct SweepPlan {
     SetRec* d_srec = nullptr;    // [n_units]
     int* d_csr = nullptr;        // ptr[n_rows+1], row_snp[n_rows], pos[n_units * rec_stride]
     const int* d_pos = nullptr;  // record slot -> CSR position (inside d_csr)
+    const int* d_dptr = nullptr; // [U+1] dense per-SNP record runs (inside d_csr)
     int csr_ptr_len = 0, csr_idx_len = 0;
+    int variant = 0;             // 1: the k = 3 fast kernel's decomposition
+    double fused_bytes = 0, fused_flops = 0;  // in-launch level-2 work of the last launch
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // kernel start/end, merges end
     bool ran = false;
 };
@@ -69,8 +72,9 @@ struct Sweep3Args {
     double rho, pit0;          // pit[nsh] = pit0 * rho^nsh (prior per member is multiplicative)
     int U, ldg, pad, Ck;
 };
+struct Level2Blocks;  // psx_sweep_dev.h
 int launch_sweep3(bool allpres, const Sweep3Args& A, int n_units, const int4* units, Acc5* rec, SetRec* srec,
-                  int rec_stride, int* flag, const int* pos, hipStream_t st);
+                  int rec_stride, int* flag, const int* pos, hipStream_t st, const Level2Blocks* l2);
 int launch_scale_y(const double* y, int n, double* ys, hipStream_t st);
 int launch_build_skewT(const double* G, int ldg, int pad, double* skew, hipStream_t st);
 
@@ -99,6 +103,14 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
 int sweep_begin(SweepPlanCache& cache, hipStream_t stream);   // zero the EXACT flag
 int sweep_level(SweepPlanCache& cache, int k, int U, int ldg, int rank, int world, hipStream_t stream,
                 const SweepArgs& a, Acc5* acc, SetRec* sacc, bool exact);   // async enqueue
+// Pieces of the fused exhaustive pass: the level's plan (built on first use)
+// and its kernel alone (set records into srec_out, or the plan's own buffer).
+// With l2 (a level-2 plan) the level-2 units run in the same launch as the
+// k = 3 fast kernel (set records into srec2), else right after it.
+int sweep_prepare(SweepPlanCache& cache, int k, int U, int ldg, int rank, int world, hipStream_t stream,
+                  const SweepArgs& a, bool exact, SweepPlan** out);
+int sweep_kernel(SweepPlanCache& cache, SweepPlan& plan, hipStream_t stream, const SweepArgs& a, SetRec* srec_out,
+                 bool exact, SweepPlan* l2, SetRec* srec2);
 int sweep_flag(SweepPlanCache& cache, int* flag);                          // after sync
 int sweep_stats(SweepPlanCache& cache, int k, int U, int rank, int world, SweepStats* st);  // after sync
 void sweep_free(SweepPlanCache& cache);

@@ -25,6 +25,7 @@
 
 #include "psx_sweep.h"
 #include "psx_sweep_dev.h"
+#include "psx_sweep_unit.h"
 
 namespace psx {
 
@@ -41,280 +42,12 @@ const char* sweep_error() { return g_sweep_err.c_str(); }
         }                                                                                           \
     } while (0)
 
-// One union set: per-study subset weights (n, mu) for the 2^K subsets (bit j =
-// member j), zero-weighted where a member is absent from the study.  Folds the
-// 3^K assignments (postcal.cpp:907-1030) into per-member records and the set's
-// scalar record.
-//
-// notSharedLL (member j unshared) sums over assignment groups whose maximum sits
-// Gll - GN_j bits below the set maximum.  The fast variant rescales the group
-// sum by that gap (exact while the gap is <= 900 bits, i.e. unless j's
-// quadratic gain exceeds ~900 bits in both studies) and raises *flag otherwise;
-// the host then reruns the level with EXACT = true, which rescales each group's
-// subset weights to the group's own maximum.
-template <int K, bool EXACT>
-__device__ __forceinline__ void fold_set_patterns(const TileArgs& A, const int (&nn)[2][1 << K],
-                                                  const double (&mu)[2][1 << K], int Sm0, int Sm1,
-                                                  double wcount, int* flag, Acc5 (&out)[K], SetRec& sr) {
-    constexpr int NS = 1 << K;
-    constexpr int FULL = NS - 1;
-    constexpr int NP = (K == 2) ? 9 : 27;
-    // pre-scale each study to its own top exponent (exact powers of two)
-    const int nb0 = nn[0][FULL], nb1 = nn[1][FULL];
-    double E0[NS], E1[NS];
-#pragma unroll
-    for (int T = 0; T < NS; T++) {
-        E0[T] = ((T & ~Sm0) == 0) ? ldexp(mu[0][T], nn[0][T] - nb0) : 0.0;
-        E1[T] = ((T & ~Sm1) == 0) ? ldexp(mu[1][T], nn[1][T] - nb1) : 0.0;
-    }
-    const int Gll = nb0 + nb1;  // E0 E1 < 4: values stay below 2^2 relative to Gll
-    double Sw[K][3], Sl[K][3];
-#pragma unroll
-    for (int j = 0; j < K; j++)
-#pragma unroll
-        for (int x = 0; x < 3; x++) Sw[j][x] = Sl[j][x] = 0.0;
-#pragma unroll
-    for (int p = 0; p < NP; p++) {
-        int c0 = 0, c1 = 0, nsh = 0, r = p;
-        int x[K];
-#pragma unroll
-        for (int j = 0; j < K; j++) {
-            x[j] = r % 3;  // 0: study0 only, 1: study1 only, 2: both
-            r /= 3;
-            if (x[j] != 1) c0 |= 1 << j;
-            if (x[j] != 0) c1 |= 1 << j;
-            if (x[j] == 2) nsh++;
-        }
-        const double wll = E0[c0] * E1[c1];
-        const double w = wll * A.pit[nsh];
-#pragma unroll
-        for (int j = 0; j < K; j++) {
-            Sw[j][x[j]] += w;
-            Sl[j][x[j]] += wll;
-        }
-    }
-    // notSharedLL groups: member j unshared, max pattern 2^{GN_j - 2}
-    int GN[K], dmax = 0;
-#pragma unroll
-    for (int j = 0; j < K; j++) {
-        const int bj = 1 << j;
-        GN[j] = max(nb0 + nn[1][FULL ^ bj], nn[0][FULL ^ bj] + nb1);
-        dmax = max(dmax, Gll - GN[j]);
-    }
-    double ns[K];
-    if (!EXACT) {
-        if (dmax > 900) atomicOr(flag, 1);
-#pragma unroll
-        for (int j = 0; j < K; j++) ns[j] = ldexp(Sl[j][0] + Sl[j][1], Gll - GN[j]);
-    } else {
-#pragma unroll
-        for (int j = 0; j < K; j++) {
-            const int bj = 1 << j;
-            // group x_j = study0 only: C0 contains j, C1 within FULL ^ bj
-            const int g1 = nb0 + nn[1][FULL ^ bj];
-            // group x_j = study1 only: C1 contains j, C0 within FULL ^ bj
-            const int g2 = nn[0][FULL ^ bj] + nb1;
-            double s1 = 0.0, s2 = 0.0;
-#pragma unroll
-            for (int p = 0; p < NP; p++) {
-                int c0 = 0, c1 = 0, r = p, xj = 0;
-#pragma unroll
-                for (int i = 0; i < K; i++) {
-                    const int xi = r % 3;
-                    r /= 3;
-                    if (xi != 1) c0 |= 1 << i;
-                    if (xi != 0) c1 |= 1 << i;
-                    if (i == j) xj = xi;
-                }
-                if (xj == 2) continue;
-                const bool ok = ((c0 & ~Sm0) == 0) && ((c1 & ~Sm1) == 0);
-                const double m = ok ? mu[0][c0] * mu[1][c1] : 0.0;
-                if (xj == 0) s1 += ldexp(m, nn[0][c0] + nn[1][c1] - g1);
-                else s2 += ldexp(m, nn[0][c0] + nn[1][c1] - g2);
-            }
-            const int G = max(s1 != 0.0 ? g1 : EMPTY, s2 != 0.0 ? g2 : EMPTY);
-            ns[j] = ldexp(s1, g1 - G) + ldexp(s2, g2 - G);
-            GN[j] = G;
-        }
-    }
-    const int GS = Gll + A.Ck;
-#pragma unroll
-    for (int j = 0; j < K; j++) {
-        out[j].post0 = Sw[j][0] + Sw[j][2];
-        out[j].post1 = Sw[j][1] + Sw[j][2];
-        out[j].shared = Sw[j][2];
-        out[j].mP = nz_shift(GS, out[j].post0 + out[j].post1);
-        out[j].sll = Sl[j][2];
-        out[j].mS = nz_shift(Gll, out[j].sll);
-        out[j].nsll = ns[j];
-        out[j].mN = nz_shift(GN[j], ns[j]);
-        out[j].pad = 0;
-    }
-    sr.tot = Sw[0][0] + Sw[0][1] + Sw[0][2];
-    sr.m = nz_shift(GS, sr.tot);
-    // noCausal[s]: the assignment with C_s empty (all members in the other study)
-    sr.nc0 = E1[FULL] * A.pit[0];
-    sr.m0 = nz_shift(nb1 + A.Ck, sr.nc0);
-    sr.nc1 = E0[FULL] * A.pit[0];
-    sr.m1 = nz_shift(nb0 + A.Ck, sr.nc1);
-    sr.pad = 0;
-    sr.score = 1e300;
-    sr.npat = wcount;
-}
-
-
 template <int K, bool EXACT>
 __global__ __launch_bounds__(64, (K == 3 ? 2 : 4)) void k_sweep(TileArgs A, const int4* __restrict__ units, Acc5* __restrict__ rec,
                                               SetRec* __restrict__ srec, int rec_stride, int* __restrict__ flag,
                                               const int* __restrict__ pos) {
-    __shared__ Acc5 slot[64];   // c accumulators, ownership rotates every step
-    __shared__ Acc5 sacc[2][64]; // [0] a, [1] b accumulators, lane-owned
-    const int unit = blockIdx.x;
-    const int t = threadIdx.x;
-    const int4 un = units[unit];
-    const int a0 = un.x, a1 = un.y, B = un.z, T = un.w;
-    const int b = 64 * B + t;
-    const bool bvalid = b < A.U;
-    const int tile = T * (T + 1) / 2 + B;
-    const int ldg = A.ldg;
-    slot[t] = acc_zero();
-    sacc[1][t] = acc_zero();
-    SetRec accs = set_zero();
-    accs.m = accs.m0 = accs.m1 = EMPTY;
-    const unsigned pb = bvalid ? A.pres[b] : 0u;
-    // per-lane b terms
-    double Abb[2], yb[2], iAbb[2], qb[2], rPb[2];
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-        Abb[s] = A.Ad[s][b];
-        yb[s] = A.y[s][b];
-        const double r = rsqrt_nr(Abb[s]);
-        iAbb[s] = r * r;
-        qb[s] = yb[s] * yb[s] * iAbb[s];
-        rPb[s] = r * A.rsd[s];
-    }
-    const int na = (K == 3) ? (a1 - a0) : 1;
-    for (int ai = 0; ai < na; ai++) {
-        const int a = a0 + ai;
-        sacc[0][t] = acc_zero();
-        constexpr int NS = 1 << K;
-        double mu[2][NS];
-        int nn[2][NS];
-        // ---- hoisted prefix: subsets without c ------------------------------------------
-        double iAaa[2], ya[2], Gab[2], qa[2], rPa[2], Dab[2], iDab[2], wab[2], qab[2], rPab[2];
-        unsigned pa = 0;
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            mu[s][0] = 1.0;
-            nn[s][0] = 0;
-            if (K == 3) {
-                const double Aaa = A.Ad[s][a];
-                const double ra = rsqrt_nr(Aaa);
-                iAaa[s] = ra * ra;
-                ya[s] = A.y[s][a];
-                Gab[s] = A.G[s][(size_t)a * ldg + b];
-                qa[s] = ya[s] * ya[s] * iAaa[s];
-                rPa[s] = ra * A.rsd[s];
-                const double l = Gab[s] * iAaa[s];
-                Dab[s] = Abb[s] - l * Gab[s];
-                const double rab = rsqrt_nr(Dab[s]);
-                iDab[s] = rab * rab;
-                wab[s] = yb[s] - l * ya[s];
-                qab[s] = qa[s] + wab[s] * wab[s] * iDab[s];
-                rPab[s] = rPa[s] * rab * A.rsd[s];
-                split2(0.5 * qa[s] * PSX_LOG2E, rPa[s], nn[s][1], mu[s][1]);     // {a}
-                split2(0.5 * qb[s] * PSX_LOG2E, rPb[s], nn[s][2], mu[s][2]);     // {b}
-                split2(0.5 * qab[s] * PSX_LOG2E, rPab[s], nn[s][3], mu[s][3]);   // {a,b}
-            } else {
-                split2(0.5 * qb[s] * PSX_LOG2E, rPb[s], nn[s][1], mu[s][1]);     // {b}
-            }
-        }
-        if (K == 3) pa = A.pres[a];
-        const bool abvalid = bvalid && (K == 2 || a < b);
-        const double wab_cnt = memb_weight(pb) * (K == 3 ? memb_weight(pa) : 1.0);
-        // k = 2 units carry a j-range of the diagonal walk in (a0, a1)
-        const int j0 = (K == 2) ? a0 : 0, j1 = (K == 2) ? a1 : 64;
-        for (int j = j0; j < j1; j++) {
-            const int cc = (t + j) & 63;
-            const int c = 64 * T + cc;
-            const bool act = abvalid && c < A.U && (B < T || cc > t);
-            if (act) {
-                const unsigned pc = A.pres[c];
-#pragma unroll
-                for (int s = 0; s < 2; s++) {
-                    const double Acc_ = A.Ad[s][c];
-                    const double yc = A.y[s][c];
-                    const double Gbc = A.skew[s][(size_t)tile * 4096 + j * 64 + t];
-                    constexpr int IC = (K == 3) ? 4 : 2, IBC = (K == 3) ? 6 : 3;
-                    mu[s][IC] = A.muS[s][c];  // {c}: precomputed per SNP
-                    nn[s][IC] = A.nS[s][c];
-                    // {b, c}
-                    const double l2 = Gbc * iAbb[s];
-                    const double D2 = Acc_ - l2 * Gbc;
-                    const double w2 = yc - l2 * yb[s];
-                    const double r2 = rsqrt_nr(D2);
-                    const double t2 = w2 * r2;
-                    split2(0.5 * (qb[s] + t2 * t2) * PSX_LOG2E, rPb[s] * r2 * A.rsd[s], nn[s][IBC], mu[s][IBC]);
-                    if (K == 3) {
-                        const double Gac = A.G[s][(size_t)a * ldg + c];
-                        // {a, c}
-                        const double l1 = Gac * iAaa[s];
-                        const double D1 = Acc_ - l1 * Gac;
-                        const double w1 = yc - l1 * ya[s];
-                        const double r1 = rsqrt_nr(D1);
-                        const double t1 = w1 * r1;
-                        split2(0.5 * (qa[s] + t1 * t1) * PSX_LOG2E, rPa[s] * r1 * A.rsd[s], nn[s][5], mu[s][5]);
-                        // {a, b, c}: extend the (a, b) factor by the c row
-                        const double lcb = (Gbc - l1 * Gab[s]) * iDab[s];
-                        const double D3 = D1 - lcb * lcb * Dab[s];
-                        const double w3 = w1 - lcb * wab[s];
-                        const double r3 = rsqrt_nr(D3);
-                        const double t3 = w3 * r3;
-                        split2(0.5 * (qab[s] + t3 * t3) * PSX_LOG2E, rPab[s] * r3 * A.rsd[s], nn[s][7], mu[s][7]);
-                    }
-                }
-                int Sm0, Sm1;
-                if (K == 3) {
-                    Sm0 = (pa & 1) | ((pb & 1) << 1) | ((pc & 1) << 2);
-                    Sm1 = ((pa >> 1) & 1) | (((pb >> 1) & 1) << 1) | (((pc >> 1) & 1) << 2);
-                } else {
-                    Sm0 = (pb & 1) | ((pc & 1) << 1);
-                    Sm1 = ((pb >> 1) & 1) | (((pc >> 1) & 1) << 1);
-                }
-                Acc5 out[K];
-                SetRec sr;
-                fold_set_patterns<K, EXACT>(A, nn, mu, Sm0, Sm1, wab_cnt * memb_weight(pc), flag, out, sr);
-                ffold1(accs.m, accs.tot, sr.m, sr.tot);
-                ffold1(accs.m0, accs.nc0, sr.m0, sr.nc0);
-                ffold1(accs.m1, accs.nc1, sr.m1, sr.nc1);
-                accs.npat += sr.npat;
-                if (K == 3) {
-                    Acc5 x = sacc[0][t];
-                    ffold_acc(x, out[0]);
-                    sacc[0][t] = x;
-                }
-                {
-                    Acc5 x = sacc[1][t];
-                    ffold_acc(x, out[K - 2]);
-                    sacc[1][t] = x;
-                }
-                Acc5 sl = slot[cc];
-                ffold_acc(sl, out[K - 1]);
-                slot[cc] = sl;
-            }
-            __syncthreads();  // slot[] ownership rotates across lanes every step
-        }
-        if (K == 3) {
-            Acc5 acca = sacc[0][t];
-            wave_fold_acc(acca);
-            if (t == 0) put_rec(rec, pos, (size_t)unit * rec_stride + 128 + ai, acca);
-        }
-    }
-    __syncthreads();
-    put_rec(rec, pos, (size_t)unit * rec_stride + t, slot[t]);
-    put_rec(rec, pos, (size_t)unit * rec_stride + 64 + t, sacc[1][t]);
-    wave_fold_set(accs);
-    if (t == 0) srec[unit] = accs;
+    __shared__ SweepUnitSmem sm;
+    sweep_unit<K, EXACT>(A, blockIdx.x, units, rec, srec, rec_stride, flag, pos, sm);
 }
 
 // singleton subset weights per union SNP: h = y^2 / (2 A) log2(e), rP = (d A)^{-1/2}
@@ -685,15 +418,24 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     // kernels write record slot i straight to its CSR position pos[i] (-1: no SNP)
     std::vector<int> pos(key.size(), -1);
     for (size_t q = 0; q < idx.size(); q++) pos[idx[q]] = (int)q;
+    // dense per-SNP pointers (rows are in increasing SNP order): SNP u's run is
+    // [dptr[u], dptr[u+1]), empty when u has no record
+    std::vector<int> dptr(U + 1, 0);
+    for (int u = 0, r = 0; u <= U; u++) {
+        while (r < (int)rows.size() && rows[r] < u) r++;
+        dptr[u] = r < (int)rows.size() ? ptr[r] : acc;
+    }
     std::vector<int> packed;
     packed.insert(packed.end(), ptr.begin(), ptr.end());
     packed.insert(packed.end(), rows.begin(), rows.end());
     packed.insert(packed.end(), pos.begin(), pos.end());
+    packed.insert(packed.end(), dptr.begin(), dptr.end());
     if (!idx.empty()) SWCHK(hipMalloc(&P.d_rec, sizeof(Acc5) * idx.size()));
     if (!packed.empty()) {
         SWCHK(hipMalloc(&P.d_csr, sizeof(int) * packed.size()));
         SWCHK(hipMemcpy(P.d_csr, packed.data(), sizeof(int) * packed.size(), hipMemcpyHostToDevice));
         P.d_pos = P.d_csr + ptr.size() + rows.size();
+        P.d_dptr = P.d_pos + pos.size();
     }
     return 0;
 }
@@ -756,28 +498,50 @@ int sweep_flag(SweepPlanCache& C, int* flag) {
     return 0;
 }
 
-// Enqueue one level (kernel + record merges) on `st`; no host synchronisation.
-int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, hipStream_t st, const SweepArgs& a,
-                Acc5* acc, SetRec* sacc, bool exact) {
+// The level's plan for (rank, world), built (host decomposition + CSR upload)
+// on first use; also builds the shared skewed layouts.
+int sweep_prepare(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, hipStream_t st, const SweepArgs& a,
+                  bool exact, SweepPlan** out) {
     if (ensure_skew(C, a, ldg, U, st)) return -1;
     const int variant = (k == 3 && !exact) ? 1 : 0;
     auto key = std::make_tuple(k, U, rank, world, variant);
     auto it = C.plans.find(key);
     if (it == C.plans.end()) {
         std::vector<unsigned char> pres(ldg);
+        SWCHK(hipStreamSynchronize(st));
         SWCHK(hipMemcpy(pres.data(), a.pres, ldg, hipMemcpyDeviceToHost));
         SweepPlan P;
         if (build_plan(P, k, U, ldg, rank, world, pres.data(), variant)) return -1;
+        P.variant = variant;
         for (int i = 0; i < 3; i++) SWCHK(hipEventCreate(&P.ev[i]));
         it = C.plans.emplace(key, P).first;
     }
-    SweepPlan& P = it->second;
-    P.ran = false;
-    {
-        auto other = C.plans.find(std::make_tuple(k, U, rank, world, 1 - variant));
-        if (other != C.plans.end()) other->second.ran = false;  // stats: the last pass only
-    }
+    *out = &it->second;
+    return 0;
+}
+
+// Enqueue one level (kernel + record merges) on `st`; no host synchronisation.
+int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, hipStream_t st, const SweepArgs& a,
+                Acc5* acc, SetRec* sacc, bool exact) {
+    SweepPlan* PP = nullptr;
+    if (sweep_prepare(C, k, U, ldg, rank, world, st, a, exact, &PP)) return -1;
+    if (sweep_kernel(C, *PP, st, a, nullptr, exact, nullptr, nullptr)) return -1;
+    SweepPlan& P = *PP;
     if (P.n_units == 0) return 0;
+    if (P.n_rows > 0) {
+        hipLaunchKernelGGL(k_merge_rows, dim3(P.n_rows), dim3(256), 0, st, P.d_rec, P.d_csr,
+                           P.d_csr + P.csr_ptr_len, acc);
+        SWCHK(hipGetLastError());
+    }
+    SetRec none = set_zero();
+    if (launch_merge_sets(P.d_srec, P.n_units, none, sacc, st)) return -1;
+    SWCHK(hipEventRecord(P.ev[2], st));
+    return 0;
+}
+
+// Launch only the level's kernel: per-SNP records into the plan's CSR buffer,
+// set records into srec_out (the plan's own buffer when null).
+static TileArgs tile_args(const SweepPlanCache& C, const SweepArgs& a, int k, int U, int ldg) {
     TileArgs A;
     A.G[0] = a.G0; A.G[1] = a.G1;
     A.Ad[0] = a.Ad0; A.Ad[1] = a.Ad1;
@@ -791,6 +555,28 @@ int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, h
     A.U = U; A.ldg = ldg;
     A.Ck = a.Ck[k];
     for (int n = 0; n < 4; n++) A.pit[n] = (n <= k) ? a.pit[k * a.pit_ld + n] : 0.0;
+    return A;
+}
+
+static void mark_last(SweepPlanCache& C, SweepPlan& P) {
+    P.ran = false;
+    auto other = C.plans.find(std::make_tuple(P.k, P.U, P.rank, P.world, 1 - P.variant));
+    if (other != C.plans.end()) other->second.ran = false;  // stats: the last pass only
+}
+
+int sweep_kernel(SweepPlanCache& C, SweepPlan& P, hipStream_t st, const SweepArgs& a, SetRec* srec_out, bool exact,
+                 SweepPlan* l2, SetRec* srec2) {
+    const int k = P.k, U = P.U, ldg = P.ldg;
+    mark_last(C, P);
+    P.fused_bytes = P.fused_flops = 0;
+    const bool ride = l2 && k == 3 && !exact && l2->k == 2 && l2->n_units > 0;
+    if (l2) mark_last(C, *l2);
+    if (P.n_units == 0 && !ride) {
+        if (l2 && sweep_kernel(C, *l2, st, a, srec2, exact, nullptr, nullptr)) return -1;
+        return 0;
+    }
+    SetRec* srec = srec_out ? srec_out : P.d_srec;
+    const TileArgs A = tile_args(C, a, k, U, ldg);
     if (!C.d_flag && sweep_begin(C, st)) return -1;
     SWCHK(hipEventRecord(P.ev[0], st));
     const dim3 g(P.n_units), blk(64);
@@ -806,25 +592,27 @@ int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, h
         S3.pit0 = A.pit[0];
         S3.rho = A.pit[0] > 0 ? A.pit[1] / A.pit[0] : 0.0;
         S3.U = U; S3.ldg = ldg; S3.Ck = A.Ck;
-        if (launch_sweep3(C.allpres, S3, P.n_units, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag, P.d_pos, st))
+        Level2Blocks b{0, TileArgs{}, nullptr, nullptr, nullptr, nullptr};
+        if (ride) {  // level 2 in the same launch: its units are the first blocks of the grid
+            b = Level2Blocks{l2->n_units, tile_args(C, a, 2, U, ldg), l2->d_units, l2->d_rec,
+                             srec2 ? srec2 : l2->d_srec, l2->d_pos};
+            P.fused_bytes = l2->alg_bytes;
+            P.fused_flops = l2->flops;
+        }
+        if (launch_sweep3(C.allpres, S3, P.n_units, P.d_units, P.d_rec, srec, P.rec_stride, C.d_flag, P.d_pos, st,
+                          ride ? &b : nullptr))
             SWCHK(hipGetLastError());
     } else if (k == 3)
-        hipLaunchKernelGGL((k_sweep<3, true>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag, P.d_pos);
+        hipLaunchKernelGGL((k_sweep<3, true>), g, blk, 0, st, A, P.d_units, P.d_rec, srec, P.rec_stride, C.d_flag, P.d_pos);
     else if (!exact)
-        hipLaunchKernelGGL((k_sweep<2, false>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag, P.d_pos);
+        hipLaunchKernelGGL((k_sweep<2, false>), g, blk, 0, st, A, P.d_units, P.d_rec, srec, P.rec_stride, C.d_flag, P.d_pos);
     else
-        hipLaunchKernelGGL((k_sweep<2, true>), g, blk, 0, st, A, P.d_units, P.d_rec, P.d_srec, P.rec_stride, C.d_flag, P.d_pos);
+        hipLaunchKernelGGL((k_sweep<2, true>), g, blk, 0, st, A, P.d_units, P.d_rec, srec, P.rec_stride, C.d_flag, P.d_pos);
     SWCHK(hipGetLastError());
     SWCHK(hipEventRecord(P.ev[1], st));
-    if (P.n_rows > 0) {
-        hipLaunchKernelGGL(k_merge_rows, dim3(P.n_rows), dim3(256), 0, st, P.d_rec, P.d_csr,
-                           P.d_csr + P.csr_ptr_len, acc);
-        SWCHK(hipGetLastError());
-    }
-    SetRec none = set_zero();
-    if (launch_merge_sets(P.d_srec, P.n_units, none, sacc, st)) return -1;
-    SWCHK(hipEventRecord(P.ev[2], st));
+    SWCHK(hipEventRecord(P.ev[2], st));  // merges (if any) re-record ev[2]
     P.ran = true;
+    if (l2 && !ride && sweep_kernel(C, *l2, st, a, srec2, exact, nullptr, nullptr)) return -1;
     return 0;
 }
 
@@ -847,8 +635,8 @@ int sweep_stats_plan(SweepPlan& P, int k, SweepStats* stats) {
     stats->kernel_ms[k] += k_ms;
     stats->launches[k] += 1;
     stats->union_sets[k] += P.union_sets;
-    stats->alg_bytes[k] += P.alg_bytes;
-    stats->flops[k] += P.flops;
+    stats->alg_bytes[k] += P.alg_bytes + P.fused_bytes;  // per launch: in-launch level-2 work included
+    stats->flops[k] += P.flops + P.fused_flops;
     stats->merge_ms += m_ms;
     return 0;
 }

@@ -36,6 +36,7 @@
 
 #include "psx_sweep.h"
 #include "psx_sweep_dev.h"
+#include "psx_sweep_unit.h"
 
 namespace psx {
 
@@ -126,21 +127,57 @@ __device__ __forceinline__ Acc5 lacc_rec(const LAcc& a, int Ck, double pit0) {
 //
 // Pivot factors: P_T^{-1/2} = prod_i r_i rsd over the LDL^T pivots of T.  The
 // step computes r2x = 2 / sqrt(D), so the staged factors carry rsd / 2.
+// LDS of a k = 3 unit: b-block terms (per unit) and (a, b) terms (per a),
+// indexed [study][b slot], the exp2 table and the rotating b-slot accumulators
+struct Sweep3Smem {
+    double tab[256];
+    double bI[2][64], bYh[2][64], bH[2][64], bR[2][64];
+    double abG[2][64], abD[2][64], abI[2][64], abW[2][64], abH[2][64], abR[2][64], abMu[2][64], abMuB[2][64];
+    int abN[2][64];
+    double bW[64];
+    double sP0[64], sP1[64], sSh[64], sSl[64], sNs[64];
+    int sM[64];
+};
+union SweepSmem {  // a block runs either a k = 3 unit or a level-2 unit
+    Sweep3Smem s3;
+    SweepUnitSmem u2;
+};
+
 template <bool ALLPRES>
 __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __restrict__ units,
                                                   Acc5* __restrict__ rec, SetRec* __restrict__ srec, int rec_stride,
-                                                  int* __restrict__ flag, const int* __restrict__ pos) {
-    __shared__ double tab[256];
-    // b-block terms (per unit) and (a, b) terms (per a), indexed [study][b slot]
-    __shared__ double bI[2][64], bYh[2][64], bH[2][64], bR[2][64];
-    __shared__ double abG[2][64], abD[2][64], abI[2][64], abW[2][64], abH[2][64], abR[2][64], abMu[2][64],
-        abMuB[2][64];
-    __shared__ int abN[2][64];
-    __shared__ double bW[64];
-    __shared__ double sP0[64], sP1[64], sSh[64], sSl[64], sNs[64];
-    __shared__ int sM[64];
+                                                  int* __restrict__ flag, const int* __restrict__ pos, int n2,
+                                                  TileArgs A2, const int4* __restrict__ units2,
+                                                  Acc5* __restrict__ rec2, SetRec* __restrict__ srec2,
+                                                  const int* __restrict__ pos2) {
+    __shared__ SweepSmem sm;
+    if ((int)blockIdx.x < n2) {  // level-2 units ride in the same launch (dispatched first)
+        sweep_unit<2, false>(A2, blockIdx.x, units2, rec2, srec2, 128, flag, pos2, sm.u2);
+        return;
+    }
+    double (&tab)[256] = sm.s3.tab;
+    double (&bI)[2][64] = sm.s3.bI;
+    double (&bYh)[2][64] = sm.s3.bYh;
+    double (&bH)[2][64] = sm.s3.bH;
+    double (&bR)[2][64] = sm.s3.bR;
+    double (&abG)[2][64] = sm.s3.abG;
+    double (&abD)[2][64] = sm.s3.abD;
+    double (&abI)[2][64] = sm.s3.abI;
+    double (&abW)[2][64] = sm.s3.abW;
+    double (&abH)[2][64] = sm.s3.abH;
+    double (&abR)[2][64] = sm.s3.abR;
+    double (&abMu)[2][64] = sm.s3.abMu;
+    double (&abMuB)[2][64] = sm.s3.abMuB;
+    int (&abN)[2][64] = sm.s3.abN;
+    double (&bW)[64] = sm.s3.bW;
+    double (&sP0)[64] = sm.s3.sP0;
+    double (&sP1)[64] = sm.s3.sP1;
+    double (&sSh)[64] = sm.s3.sSh;
+    double (&sSl)[64] = sm.s3.sSl;
+    double (&sNs)[64] = sm.s3.sNs;
+    int (&sM)[64] = sm.s3.sM;
 
-    const int unit = blockIdx.x;
+    const int unit = blockIdx.x - n2;
     const int t = threadIdx.x;
     const int4 un = units[unit];
     const int a0 = un.x, a1 = un.y, K = un.z, C = un.w;
@@ -452,11 +489,16 @@ int launch_build_skewT(const double* G, int ldg, int pad, double* skew, hipStrea
 }
 
 int launch_sweep3(bool allpres, const Sweep3Args& A, int n_units, const int4* units, Acc5* rec, SetRec* srec,
-                  int rec_stride, int* flag, const int* pos, hipStream_t st) {
+                  int rec_stride, int* flag, const int* pos, hipStream_t st, const Level2Blocks* l2) {
+    const Level2Blocks none{0, TileArgs{}, nullptr, nullptr, nullptr, nullptr};
+    const Level2Blocks& b = l2 ? *l2 : none;
+    const dim3 grid(n_units + b.n);
     if (allpres)
-        hipLaunchKernelGGL((k_sweep3<true>), dim3(n_units), dim3(64), 0, st, A, units, rec, srec, rec_stride, flag, pos);
+        hipLaunchKernelGGL((k_sweep3<true>), grid, dim3(64), 0, st, A, units, rec, srec, rec_stride, flag, pos, b.n, b.A,
+                           b.units, b.rec, b.srec, b.pos);
     else
-        hipLaunchKernelGGL((k_sweep3<false>), dim3(n_units), dim3(64), 0, st, A, units, rec, srec, rec_stride, flag, pos);
+        hipLaunchKernelGGL((k_sweep3<false>), grid, dim3(64), 0, st, A, units, rec, srec, rec_stride, flag, pos, b.n,
+                           b.A, b.units, b.rec, b.srec, b.pos);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

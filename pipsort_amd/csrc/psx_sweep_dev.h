@@ -23,6 +23,16 @@ struct TileArgs {
     double pit[4];
 };
 
+// level-2 units launched as extra blocks of the k = 3 fast kernel
+struct Level2Blocks {
+    int n;
+    TileArgs A;
+    const int4* units;
+    Acc5* rec;
+    SetRec* srec;
+    const int* pos;
+};
+
 constexpr int EMPTY = -(1 << 28);  // shift of an empty accumulator (value 0)
 
 __device__ inline Acc5 acc_zero() {

@@ -1,0 +1,83 @@
+"""Strong-scaling rehearsal on ONE GPU: time every rank's shard of the exhaustive
+sweep for world = 1, 2, 4, 8 (one after another on the same device) and report
+the slowest rank's step time, i.e. the step time an N-GPU node would see minus
+the RCCL all-gather (latency-bound, ~56 KB per rank at M = 1000).
+
+    python tools/shard_rehearsal.py [--workload syn1000c3] [--steps 10]
+
+Each rank's step = run_exhaustive (its shard) + export_partials + merge of
+`world` images (the gathered buffer is filled with this rank's image, which
+costs the same to fold).  Developer tool (not the bench): prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+import bench  # noqa: E402
+from pipsort_amd import engine as E  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="syn1000c3")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--worlds", default="1,2,4,8")
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    seam = bench.build_seam(args.workload)
+    pc = E.PostCal(seam, device=0)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    pc.set_stream(stream.cuda_stream)
+    nb = pc.partials_bytes()
+    out = {"workload": args.workload, "worlds": {}}
+    for world in [int(w) for w in args.worlds.split(",")]:
+        mine = torch.empty(nb, dtype=torch.uint8, device="cuda")
+        gathered = torch.empty(nb * world, dtype=torch.uint8, device="cuda")
+        ranks = []
+        for rank in range(world):
+            pc.set_shard(rank, world)
+
+            def step():
+                pc.run_exhaustive()
+                if world > 1:
+                    pc.export_partials(mine.data_ptr())
+                    for r in range(world):
+                        gathered[r * nb:(r + 1) * nb].copy_(mine)
+                    pc.merge_partials(gathered.data_ptr(), world)
+
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
+            kms = 0.0
+            sweep = 0.0
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+                t = pc.timing()
+                kms += t["kernel_ms"]
+                sweep += t["sweep_ms"]
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) * 1e3 / args.steps
+            ranks.append({"rank": rank, "step_ms": dt, "kernel_ms": kms / args.steps, "sweep_ms": sweep / args.steps})
+        worst = max(r["step_ms"] for r in ranks)
+        out["worlds"][world] = {"max_step_ms": worst, "ranks": ranks}
+        print(f"world {world}: max step {worst:.3f} ms; kernel ms per rank "
+              f"{[round(r['kernel_ms'], 3) for r in ranks]}; sweep ms {[round(r['sweep_ms'], 3) for r in ranks]}",
+              flush=True)
+    base = out["worlds"].get(1, {}).get("max_step_ms")
+    if base:
+        for w, d in out["worlds"].items():
+            d["predicted_speedup_excl_allgather"] = base / d["max_step_ms"]
+    print(json.dumps(out))
+    pc.close()
+
+
+if __name__ == "__main__":
+    main()
