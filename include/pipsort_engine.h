@@ -87,6 +87,43 @@ int psx_device_count(int *count);
 int psx_create(const psx_problem *prob, int device, psx_engine **out);
 void psx_destroy(psx_engine *e);
 
+/* Model setup + PostCal::PostCal on the GPU (model.h:171-265, util.cpp:195-263).
+ * Takes what Model reads from its input files instead of the low-rank B/S':
+ * per-study LD matrices (row-major M_s x M_s as util.cpp:86-96 parses them)
+ * and z-scores.  The PSD shift (util.cpp:195-226) runs as a device LU whose
+ * determinant is bit-identical to the reference elimination; when Sigma'_s is
+ * positive definite, Sigma~_s = B_s^T B_s = Sigma'_s, y_s = B_s^T S'_s = z_s and
+ * ||S'_s||^2 = z_s^T Sigma'_s^-1 z_s exactly, so no eigendecomposition is done
+ * (otherwise the reference's eigen route runs on the host for that study). */
+typedef struct {
+    int32_t n_studies;              /* must be 2                                         */
+    const int32_t *m;               /* [n_studies] M_s                                   */
+    const double *ld;               /* LD_s, row-major M_s x M_s, concatenated           */
+    const double *z;                /* [N] z-scores, study-major (S_LONG_VEC before the transform) */
+    int32_t n_union;
+    const int32_t *union_to_local;  /* [n_studies][n_union], -1 = absent                 */
+    int32_t max_causal;
+    const int32_t *sample_sizes;
+    double sharing_param, gamma, t_squared, s_squared;
+} psx_ld_problem;
+
+typedef struct {
+    double psd_added[2];       /* diagonal shift per study (util.cpp:195-226)            */
+    int32_t psd_iterations[2]; /* LU determinants evaluated per study                    */
+    int32_t eigen_route[2];    /* 1 if Sigma'_s was not positive definite (host eigen)   */
+    double min_pivot_ratio[2]; /* smallest L D L^T pivot / largest |diagonal|            */
+    double setup_ms;           /* wall time of the whole setup + create                  */
+} psx_setup_info;
+
+int psx_create_from_ld(const psx_ld_problem *prob, int device, psx_engine **out, psx_setup_info *info);
+
+/* The PSD shift alone on the GPU (util.cpp:195-226): same contract as the host
+ * psx_psd_shift (pipsort_model.h), for parity tests and the CLI. */
+int psx_psd_shift_gpu(double *sigma, int32_t m, double *added, int device);
+/* One GSL-order partial-pivot LU determinant on the GPU (a row-major m x m, not
+ * modified): bit-identical to the host psx_lu_det (pipsort_model.h). */
+int psx_lu_det_gpu(const double *a, int32_t m, int device, double *det);
+
 /* Multi-GPU sharding of the exhaustive sweep (one process per GPU): this handle
  * evaluates shard `rank` of `world` equal slices of every causal-set level; the
  * null configuration belongs to rank 0.  Default (0, 1). */

@@ -20,6 +20,9 @@ extern "C" {
  * place; *added receives the total diagonal shift. */
 int psx_psd_shift(double *sigma, int32_t m, double *added);
 
+/* The determinant psx_psd_shift tests (a row-major m x m, not modified). */
+int psx_lu_det(const double *a, int32_t m, double *det);
+
 /* model.h:213-259 with util.cpp:228-263: Sigma' = Q W Q^T, B = |W|^(1/2) Q^T
  * (column-major m x m, Armadillo layout) and S' = |W|^(-1/2) Q^T z. */
 int psx_lowrank_study(const double *sigma, const double *z, int32_t m, double *B_out, double *sprime_out);

@@ -43,6 +43,13 @@ static double lu_det(std::vector<double>& a, int n) {
     return det;
 }
 
+int psx_lu_det(const double* a, int32_t m, double* det) {
+    if (m <= 0 || !det) return -1;
+    std::vector<double> t(a, a + (size_t)m * m);
+    *det = lu_det(t, m);
+    return 0;
+}
+
 int psx_psd_shift(double* sigma, int32_t m, double* added) {
     if (m <= 0) return -1;
     double add = 0;

@@ -242,44 +242,78 @@ int main(int argc, char* argv[]) {
         if (cnt != m[i]) { printf("Invariant does not hold\n"); exit(1); }
     }
     const int N = m[0] + m[1];
-    vector<double> B, sp(N);
-    size_t boff = 0;
-    int off = 0;
-    B.resize((size_t)m[0] * m[0] + (size_t)m[1] * m[1]);
-    for (int i = 0; i < S; i++) {
-        auto b0 = std::chrono::steady_clock::now();
-        double add = 0;
-        psx_psd_shift(sig[i].data(), m[i], &add);  // model.h:194
-        auto b1 = std::chrono::steady_clock::now();
-        std::cout << "Time to make psd = " << std::chrono::duration_cast<std::chrono::microseconds>(b1 - b0).count()
-                  << "[µs]" << std::endl;
-        psx_lowrank_study(sig[i].data(), zs[i].data(), m[i], B.data() + boff, sp.data() + off);  // model.h:213-259
-        auto b2 = std::chrono::steady_clock::now();
-        std::cout << "Time for eigen decomp = "
-                  << std::chrono::duration_cast<std::chrono::microseconds>(b2 - b1).count() << "[µs]" << std::endl;
-        boff += (size_t)m[i] * m[i];
-        off += m[i];
-    }
     vector<int32_t> u2l_flat(2 * U);
     for (int s = 0; s < 2; s++)
         for (int u = 0; u < U; u++) u2l_flat[s * U + u] = u2l[s][u];
-    psx_problem prob;
-    prob.n_studies = 2;
-    prob.m = m.data();
-    prob.B = B.data();
-    prob.s_prime = sp.data();
-    prob.n_union = U;
-    prob.union_to_local = u2l_flat.data();
-    prob.max_causal = totalCausalSNP;
-    prob.sample_sizes = sample_sizes.data();
-    prob.sharing_param = sharing_param;
-    prob.gamma = gamma;
-    prob.t_squared = tau_sqr;
-    prob.s_squared = sigma_g_squared;
     int device = 0;
     if (const char* d = getenv("PSX_DEVICE")) device = atoi(d);
     psx_engine* eng = nullptr;
-    int rc = psx_create(&prob, device, &eng);  // model.h:265
+    int rc;
+    const char* hs = getenv("PSX_HOST_SETUP");
+    if (!(hs && atoi(hs))) {
+        // Model setup on the GPU (model.h:171-264): PSD shift by device LU, then
+        // Sigma~ = Sigma', y = z, ||S'||^2 = z^T Sigma'^-1 z when Sigma' is PD
+        vector<double> ld, z;
+        ld.reserve((size_t)m[0] * m[0] + (size_t)m[1] * m[1]);
+        for (int i = 0; i < S; i++) {
+            ld.insert(ld.end(), sig[i].begin(), sig[i].end());
+            z.insert(z.end(), zs[i].begin(), zs[i].end());
+        }
+        psx_ld_problem q;
+        q.n_studies = 2;
+        q.m = m.data();
+        q.ld = ld.data();
+        q.z = z.data();
+        q.n_union = U;
+        q.union_to_local = u2l_flat.data();
+        q.max_causal = totalCausalSNP;
+        q.sample_sizes = sample_sizes.data();
+        q.sharing_param = sharing_param;
+        q.gamma = gamma;
+        q.t_squared = tau_sqr;
+        q.s_squared = sigma_g_squared;
+        psx_setup_info info;
+        rc = psx_create_from_ld(&q, device, &eng, &info);  // model.h:171-265
+        if (rc == 0)
+            for (int i = 0; i < S; i++)
+                std::cout << "study " << i << ": psd shift " << info.psd_added[i] << " ("
+                          << info.psd_iterations[i] << " LU), "
+                          << (info.eigen_route[i] ? "eigen route" : "positive definite, no eigen") << std::endl;
+    } else {
+        // host restatement of the reference setup (PSX_HOST_SETUP=1)
+        vector<double> B, sp(N);
+        size_t boff = 0;
+        int off = 0;
+        B.resize((size_t)m[0] * m[0] + (size_t)m[1] * m[1]);
+        for (int i = 0; i < S; i++) {
+            auto b0 = std::chrono::steady_clock::now();
+            double add = 0;
+            psx_psd_shift(sig[i].data(), m[i], &add);  // model.h:194
+            auto b1 = std::chrono::steady_clock::now();
+            std::cout << "Time to make psd = "
+                      << std::chrono::duration_cast<std::chrono::microseconds>(b1 - b0).count() << "[µs]" << std::endl;
+            psx_lowrank_study(sig[i].data(), zs[i].data(), m[i], B.data() + boff, sp.data() + off);  // model.h:213-259
+            auto b2 = std::chrono::steady_clock::now();
+            std::cout << "Time for eigen decomp = "
+                      << std::chrono::duration_cast<std::chrono::microseconds>(b2 - b1).count() << "[µs]" << std::endl;
+            boff += (size_t)m[i] * m[i];
+            off += m[i];
+        }
+        psx_problem prob;
+        prob.n_studies = 2;
+        prob.m = m.data();
+        prob.B = B.data();
+        prob.s_prime = sp.data();
+        prob.n_union = U;
+        prob.union_to_local = u2l_flat.data();
+        prob.max_causal = totalCausalSNP;
+        prob.sample_sizes = sample_sizes.data();
+        prob.sharing_param = sharing_param;
+        prob.gamma = gamma;
+        prob.t_squared = tau_sqr;
+        prob.s_squared = sigma_g_squared;
+        rc = psx_create(&prob, device, &eng);  // model.h:265
+    }
     if (rc) die_engine(rc);
     auto t_setup1 = std::chrono::steady_clock::now();
     std::cout << "Time for setup = " << std::chrono::duration_cast<std::chrono::microseconds>(t_setup1 - t_setup0).count()

@@ -20,7 +20,9 @@
 #include <vector>
 
 #include "../../include/pipsort_engine.h"
+#include "../../include/pipsort_model.h"
 #include "psx_math.h"
+#include "psx_setup.h"
 #include "psx_sweep.h"
 #include "psx_sweep_dev.h"
 
@@ -915,8 +917,14 @@ uint64_t psx_count_configs(const psx_problem* p) {
     return (uint64_t)(t + 0.5L);
 }
 
-int psx_create(const psx_problem* p, int device, psx_engine** out) {
+namespace {
+
+// PostCal::PostCal (postcal.h:118-195) from either the low-rank seam inputs
+// (p->B, p->s_prime) or, with ld != nullptr, the Model inputs (LD + z) through
+// the GPU Model setup (psx_setup.hip).
+int create_impl(const psx_problem* p, const psx_ld_problem* ld, int device, psx_engine** out, psx_setup_info* info) {
     *out = nullptr;
+    auto tc0 = std::chrono::steady_clock::now();
     if (!p || p->n_studies != 2) return fail(PSX_EINVAL, "only two studies are supported (postcal.cpp:20-23)");
     if (p->max_causal < 0 || p->max_causal > PSX_KMAX) return fail(PSX_ERANGE, "max_causal outside [0, 6]");
     if (p->n_union <= 0 || p->m[0] <= 0 || p->m[1] <= 0) return fail(PSX_EINVAL, "empty problem");
@@ -953,8 +961,8 @@ int psx_create(const psx_problem* p, int device, psx_engine** out) {
     int mn = std::min(p->sample_sizes[0], p->sample_sizes[1]);
     for (int s = 0; s < 2; s++) e->dval[s] = p->s_squared * (double(p->sample_sizes[s]) / mn) + p->t_squared;
     double spsq = 0;
-    for (int i = 0; i < e->N; i++) spsq += p->s_prime[i] * p->s_prime[i];
-    e->K = -spsq / 2;
+    if (!ld)
+        for (int i = 0; i < e->N; i++) spsq += p->s_prime[i] * p->s_prime[i];
     // null configuration (postcal.cpp:799-803): -res/2 - sqrt(|1|) + U log(1-gamma); K factored out
     e->L0 = -std::sqrt(std::fabs(1.0)) + e->U * std::log(1 - p->gamma);
 
@@ -1002,12 +1010,50 @@ int psx_create(const psx_problem* p, int device, psx_engine** out) {
             cleanup();
             return bail(fail(PSX_EHIP, "out of device memory"));
         }
-        hipMemcpyAsync(dB, p->B + boff, (size_t)M * M * sizeof(double), hipMemcpyHostToDevice, e->stream);
-        hipMemcpyAsync(dsp, p->s_prime + soff, (size_t)M * sizeof(double), hipMemcpyHostToDevice, e->stream);
         hipMemcpyAsync(du2l, p->union_to_local + s * e->U, e->U * sizeof(int), hipMemcpyHostToDevice, e->stream);
-        dim3 g((M + 15) / 16, (M + 15) / 16);
-        hipLaunchKernelGGL(k_btb, g, dim3(256), 0, e->stream, dB, M, dS);
-        hipLaunchKernelGGL(k_bts, dim3(M), dim3(64), 0, e->stream, dB, dsp, M, dyl);
+        bool lowrank = true;  // Sigma~ = B^T B, y = B^T S' from (B, S')
+        const double* Bs = ld ? nullptr : p->B + boff;
+        const double* Ss = ld ? nullptr : p->s_prime + soff;
+        std::vector<double> hB, hS;
+        if (ld) {
+            psx::LdStudyResult r;
+            std::string err;
+            if (psx::ld_study_setup(ld->ld + boff, ld->z + soff, M, e->stream, dS, dyl, &r, &err)) {
+                cleanup();
+                return bail(fail(PSX_EHIP, "GPU model setup: " + err));
+            }
+            if (info) {
+                info->psd_added[s] = r.added;
+                info->psd_iterations[s] = r.psd_iterations;
+                info->eigen_route[s] = r.path;
+                info->min_pivot_ratio[s] = r.min_pivot_ratio;
+            }
+            if (r.path == 0) {
+                lowrank = false;
+                spsq += r.spsq;
+            } else {
+                // Sigma' not (comfortably) positive definite: the reference's eigen
+                // route, model.h:213-259 (host restatement), then B^T B on the GPU
+                std::vector<double> sig(ld->ld + boff, ld->ld + boff + (size_t)M * M);
+                for (int i = 0; i < M; i++) sig[(size_t)i * M + i] += r.added;
+                hB.resize((size_t)M * M);
+                hS.resize(M);
+                if (psx_lowrank_study(sig.data(), ld->z + soff, M, hB.data(), hS.data())) {
+                    cleanup();
+                    return bail(fail(PSX_EINVAL, "eigen route failed"));
+                }
+                for (int i = 0; i < M; i++) spsq += hS[i] * hS[i];
+                Bs = hB.data();
+                Ss = hS.data();
+            }
+        }
+        if (lowrank) {
+            hipMemcpyAsync(dB, Bs, (size_t)M * M * sizeof(double), hipMemcpyHostToDevice, e->stream);
+            hipMemcpyAsync(dsp, Ss, (size_t)M * sizeof(double), hipMemcpyHostToDevice, e->stream);
+            dim3 g((M + 15) / 16, (M + 15) / 16);
+            hipLaunchKernelGGL(k_btb, g, dim3(256), 0, e->stream, dB, M, dS);
+            hipLaunchKernelGGL(k_bts, dim3(M), dim3(64), 0, e->stream, dB, dsp, M, dyl);
+        }
         hipLaunchKernelGGL(k_to_union, dim3((e->ldg + 255) / 256, e->ldg), dim3(256), 0, e->stream, dS, M, du2l,
                            e->U, e->ldg, e->dG[s]);
         if (hipGetLastError() != hipSuccess) { cleanup(); return bail(fail(PSX_EHIP, "setup kernel launch")); }
@@ -1029,6 +1075,7 @@ int psx_create(const psx_problem* p, int device, psx_engine** out) {
         soff += M;
     }
     cleanup();
+    e->K = -spsq / 2;
     if (hipMalloc(&e->dpres, e->ldg) != hipSuccess ||
         hipMalloc(&e->dacc, sizeof(Acc5) * ((size_t)e->ldg + 2)) != hipSuccess ||
         hipHostMalloc(&e->hstat, kStatBytes) != hipSuccess)
@@ -1050,7 +1097,89 @@ int psx_create(const psx_problem* p, int device, psx_engine** out) {
     if (reset_acc(e)) return bail(PSX_EHIP);
     if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(fail(PSX_EHIP, "create sync"));
     std::memset(&e->timing, 0, sizeof(e->timing));
+    if (info) info->setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count();
     *out = e;
+    return 0;
+}
+
+}  // namespace
+
+int psx_create(const psx_problem* p, int device, psx_engine** out) {
+    if (!out) return fail(PSX_EINVAL, "null out");
+    *out = nullptr;
+    if (!p || !p->B || !p->s_prime) return fail(PSX_EINVAL, "null problem");
+    return create_impl(p, nullptr, device, out, nullptr);
+}
+
+int psx_create_from_ld(const psx_ld_problem* q, int device, psx_engine** out, psx_setup_info* info) {
+    if (!out) return fail(PSX_EINVAL, "null out");
+    *out = nullptr;
+    if (!q || !q->ld || !q->z || !q->m) return fail(PSX_EINVAL, "null problem");
+    if (info) std::memset(info, 0, sizeof(*info));
+    psx_problem p;
+    std::memset(&p, 0, sizeof(p));
+    p.n_studies = q->n_studies;
+    p.m = q->m;
+    p.n_union = q->n_union;
+    p.union_to_local = q->union_to_local;
+    p.max_causal = q->max_causal;
+    p.sample_sizes = q->sample_sizes;
+    p.sharing_param = q->sharing_param;
+    p.gamma = q->gamma;
+    p.t_squared = q->t_squared;
+    p.s_squared = q->s_squared;
+    return create_impl(&p, q, device, out, info);
+}
+
+namespace {
+int gpu_ready(int device) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(PSX_ENODEV, "no HIP device: the engine has no CPU fallback");
+    if (device < 0 || device >= ndev) return fail(PSX_EINVAL, "device index out of range");
+    HIPCHK(hipSetDevice(device));
+    return 0;
+}
+}  // namespace
+
+int psx_lu_det_gpu(const double* a, int32_t m, int device, double* det) {
+    if (!a || m <= 0 || !det) return fail(PSX_EINVAL, "bad argument");
+    int rc;
+    if ((rc = gpu_ready(device))) return rc;
+    double* dA = nullptr;
+    double* dd = nullptr;
+    int* ds = nullptr;
+    const size_t nn = (size_t)m * m;
+    if (hipMalloc(&dA, nn * sizeof(double)) != hipSuccess || hipMalloc(&dd, m * sizeof(double)) != hipSuccess ||
+        hipMalloc(&ds, m * sizeof(int)) != hipSuccess) {
+        hipFree(dA); hipFree(dd); hipFree(ds);
+        return fail(PSX_EHIP, "out of device memory");
+    }
+    std::string err;
+    rc = 0;
+    if (hipMemcpy(dA, a, nn * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) rc = fail(PSX_EHIP, "upload");
+    else if (psx::lu_det_device(dA, m, ds, dd, nullptr, det, &err)) rc = fail(PSX_EHIP, err);
+    hipFree(dA); hipFree(dd); hipFree(ds);
+    return rc;
+}
+
+int psx_psd_shift_gpu(double* sigma, int32_t m, double* added, int device) {
+    if (!sigma || m <= 0) return fail(PSX_EINVAL, "bad argument");
+    int rc;
+    if ((rc = gpu_ready(device))) return rc;
+    std::vector<double> t((size_t)m * m);
+    double add = 0;
+    for (int guard = 0;; guard++) {
+        if (guard >= 100000) return fail(PSX_EINVAL, "PSD shift did not terminate");
+        std::memcpy(t.data(), sigma, t.size() * sizeof(double));
+        for (int i = 0; i < m; i++) t[(size_t)i * m + i] = sigma[(size_t)i * m + i] + add;
+        double det = 0;
+        if ((rc = psx_lu_det_gpu(t.data(), m, device, &det))) return rc;
+        if (det > 0) break;
+        add += 0.01;
+    }
+    for (int i = 0; i < m; i++) sigma[(size_t)i * m + i] += add;
+    if (added) *added = add;
     return 0;
 }
 

@@ -1,0 +1,32 @@
+// psx_setup.h — GPU Model setup (model.h:171-264, util.cpp:195-263); see psx_setup.hip.
+#ifndef PSX_SETUP_H
+#define PSX_SETUP_H
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+namespace psx {
+
+struct LdStudyResult {
+    double added;             // diagonal shift of util.cpp:195-226
+    int psd_iterations;       // LU determinants evaluated
+    int path;                 // 0: Sigma' positive definite (identity route), 1: eigen route needed
+    int sigma_host_needed;    // path 1: the caller rebuilds Sigma' = LD + added I on the host
+    double min_pivot_ratio;   // min L D L^T pivot / max |diag|
+    double spsq;              // path 0: ||S'_s||^2 = z^T Sigma'^-1 z
+};
+
+// Partial-pivot LU determinant of the device matrix dA (n x n row-major,
+// destroyed), bit-identical to the host restatement (model.cpp lu_det).
+// dswp: n ints, ddiag: n doubles of device scratch.
+int lu_det_device(double* dA, int n, int* dswp, double* ddiag, hipStream_t st, double* det, std::string* err);
+
+// One study: LD (host, row-major M x M as parsed, util.cpp:86-96) and z (host,
+// M) -> dS = Sigma~_s (device, row-major M x M) and dy = y_s (device, M).
+int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, double* dS, double* dy,
+                   LdStudyResult* res, std::string* err);
+
+}  // namespace psx
+
+#endif

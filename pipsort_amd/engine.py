@@ -32,7 +32,8 @@ EXPORTED = [
     "psx_eval_union_batch", "psx_reset", "psx_get_accum", "psx_partials_bytes",
     "psx_export_partials", "psx_merge_partials", "psx_get_timing", "psx_count_configs",
     "psx_fold_partials_host", "psx_shard_stats", "psx_set_stream",
-    "psx_psd_shift", "psx_lowrank_study", "psx_sym_eigen",
+    "psx_psd_shift", "psx_lowrank_study", "psx_sym_eigen", "psx_lu_det",
+    "psx_create_from_ld", "psx_psd_shift_gpu", "psx_lu_det_gpu",
 ]
 
 
@@ -57,6 +58,36 @@ class _Problem(ctypes.Structure):
         ("t_squared", ctypes.c_double),
         ("s_squared", ctypes.c_double),
     ]
+
+
+class _LdProblem(ctypes.Structure):
+    _fields_ = [
+        ("n_studies", ctypes.c_int32),
+        ("m", ctypes.POINTER(ctypes.c_int32)),
+        ("ld", ctypes.POINTER(ctypes.c_double)),
+        ("z", ctypes.POINTER(ctypes.c_double)),
+        ("n_union", ctypes.c_int32),
+        ("union_to_local", ctypes.POINTER(ctypes.c_int32)),
+        ("max_causal", ctypes.c_int32),
+        ("sample_sizes", ctypes.POINTER(ctypes.c_int32)),
+        ("sharing_param", ctypes.c_double),
+        ("gamma", ctypes.c_double),
+        ("t_squared", ctypes.c_double),
+        ("s_squared", ctypes.c_double),
+    ]
+
+
+class SetupInfo(ctypes.Structure):
+    _fields_ = [
+        ("psd_added", ctypes.c_double * 2),
+        ("psd_iterations", ctypes.c_int32 * 2),
+        ("eigen_route", ctypes.c_int32 * 2),
+        ("min_pivot_ratio", ctypes.c_double * 2),
+        ("setup_ms", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {f: (list(getattr(self, f)) if f != "setup_ms" else self.setup_ms) for f, _ in self._fields_}
 
 
 class _Accum(ctypes.Structure):
@@ -127,6 +158,10 @@ def load_library(path: str = LIB_PATH):
         "psx_psd_shift": (c_int, [P(dbl), c_i32, P(dbl)]),
         "psx_lowrank_study": (c_int, [P(dbl), P(dbl), c_i32, P(dbl), P(dbl)]),
         "psx_sym_eigen": (c_int, [P(dbl), c_i32, P(dbl), P(dbl)]),
+        "psx_lu_det": (c_int, [P(dbl), c_i32, P(dbl)]),
+        "psx_create_from_ld": (c_int, [P(_LdProblem), c_int, P(vp), P(SetupInfo)]),
+        "psx_psd_shift_gpu": (c_int, [P(dbl), c_i32, P(dbl), c_int]),
+        "psx_lu_det_gpu": (c_int, [P(dbl), c_i32, c_int, P(dbl)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -159,6 +194,26 @@ def psd_shift(sigma: np.ndarray):
     s = np.ascontiguousarray(sigma, dtype=np.float64).copy()
     add = ctypes.c_double(0.0)
     _check(load_library().psx_psd_shift(_ptr(s, ctypes.c_double), s.shape[0], ctypes.byref(add)))
+    return s, add.value
+
+
+def lu_det(a: np.ndarray, gpu: bool = False, device: int = 0) -> float:
+    """The determinant util.cpp:214-215 tests (GSL-order LU, index-order product)."""
+    aa = np.ascontiguousarray(a, dtype=np.float64)
+    d = ctypes.c_double(0.0)
+    lib = load_library()
+    if gpu:
+        _check(lib.psx_lu_det_gpu(_ptr(aa, ctypes.c_double), aa.shape[0], int(device), ctypes.byref(d)))
+    else:
+        _check(lib.psx_lu_det(_ptr(aa, ctypes.c_double), aa.shape[0], ctypes.byref(d)))
+    return d.value
+
+
+def psd_shift_gpu(sigma: np.ndarray, device: int = 0):
+    """util.cpp:195-226 with the determinants on the GPU: returns (sigma + a I, a)."""
+    s = np.ascontiguousarray(sigma, dtype=np.float64).copy()
+    add = ctypes.c_double(0.0)
+    _check(load_library().psx_psd_shift_gpu(_ptr(s, ctypes.c_double), s.shape[0], ctypes.byref(add), int(device)))
     return s, add.value
 
 
@@ -256,6 +311,81 @@ def seam_from_arrays(ld, z, union_to_local, sample_sizes, **params) -> Seam:
                 sample_sizes=np.asarray(sample_sizes, dtype=np.int32), **params)
 
 
+@dataclass
+class ModelInputs:
+    """What Model reads from the input files (model.h:60-160): per-study LD and z,
+    the snp map and the CLI parameters.  PostCal(ModelInputs) runs the Model
+    setup on the GPU (psx_create_from_ld) instead of taking B / S'."""
+    ld: list
+    z: list
+    union_to_local: np.ndarray
+    sample_sizes: np.ndarray
+    max_causal: int = 3
+    sharing_param: float = 0.75
+    gamma: float = 0.01
+    t_squared: float = 0.52
+    s_squared: float = 5.2
+
+    def __post_init__(self):
+        self.ld = [np.ascontiguousarray(x, dtype=np.float64) for x in self.ld]
+        self.z = [np.ascontiguousarray(x, dtype=np.float64) for x in self.z]
+        self.m = np.array([x.shape[0] for x in self.ld], dtype=np.int32)
+
+    @property
+    def n_union(self):
+        return int(np.asarray(self.union_to_local).shape[1])
+
+    @property
+    def N(self):
+        return int(self.m.sum())
+
+    def _struct(self):
+        """psx_problem view (shape and parameters only; B / S' are not formed)."""
+        self._keep = [self.m, np.ascontiguousarray(self.union_to_local, dtype=np.int32),
+                      np.ascontiguousarray(self.sample_sizes, dtype=np.int32)]
+        m, u2l, n = self._keep
+        p = _Problem()
+        p.n_studies = 2
+        p.m = _ptr(m, ctypes.c_int32)
+        p.n_union = u2l.shape[1]
+        p.union_to_local = _ptr(u2l, ctypes.c_int32)
+        p.max_causal = int(self.max_causal)
+        p.sample_sizes = _ptr(n, ctypes.c_int32)
+        p.sharing_param = float(self.sharing_param)
+        p.gamma = float(self.gamma)
+        p.t_squared = float(self.t_squared)
+        p.s_squared = float(self.s_squared)
+        return p
+
+    def _ld_struct(self):
+        self._keep_ld = [self.m, np.concatenate([x.ravel() for x in self.ld]), np.concatenate(self.z),
+                         np.ascontiguousarray(self.union_to_local, dtype=np.int32),
+                         np.ascontiguousarray(self.sample_sizes, dtype=np.int32)]
+        m, ld, z, u2l, n = self._keep_ld
+        q = _LdProblem()
+        q.n_studies = 2
+        q.m = _ptr(m, ctypes.c_int32)
+        q.ld = _ptr(ld, ctypes.c_double)
+        q.z = _ptr(z, ctypes.c_double)
+        q.n_union = u2l.shape[1]
+        q.union_to_local = _ptr(u2l, ctypes.c_int32)
+        q.max_causal = int(self.max_causal)
+        q.sample_sizes = _ptr(n, ctypes.c_int32)
+        q.sharing_param = float(self.sharing_param)
+        q.gamma = float(self.gamma)
+        q.t_squared = float(self.t_squared)
+        q.s_squared = float(self.s_squared)
+        return q
+
+    count_configs = Seam.count_configs
+    shard_stats = Seam.shard_stats
+
+
+def model_inputs(ld, z, union_to_local, sample_sizes, **params) -> ModelInputs:
+    return ModelInputs(list(ld), list(z), np.asarray(union_to_local, dtype=np.int32),
+                       np.asarray(sample_sizes, dtype=np.int32), **params)
+
+
 def fold_partials_host(images: np.ndarray) -> np.ndarray:
     """Fold partial images (uint8 [count, image_bytes], rank order) on the host."""
     imgs = np.ascontiguousarray(images, dtype=np.uint8)
@@ -296,12 +426,22 @@ class Accumulators:
 class PostCal:
     """The engine handle: one per GPU (postcal.h:118 PostCal::PostCal)."""
 
-    def __init__(self, seam: Seam, device: int = 0):
+    def __init__(self, seam, device: int = 0):
+        """seam: a Seam (PostCal's own inputs, B / S') or ModelInputs (LD / z;
+        the Model setup then runs on the GPU, psx_create_from_ld)."""
         self.lib = load_library()
         self.seam = seam
-        self._p = seam._struct()
         h = ctypes.c_void_p()
-        _check(self.lib.psx_create(ctypes.byref(self._p), int(device), ctypes.byref(h)))
+        self.setup_info = None
+        if isinstance(seam, ModelInputs):
+            self._p = seam._ld_struct()
+            info = SetupInfo()
+            _check(self.lib.psx_create_from_ld(ctypes.byref(self._p), int(device), ctypes.byref(h),
+                                               ctypes.byref(info)))
+            self.setup_info = info.as_dict()
+        else:
+            self._p = seam._struct()
+            _check(self.lib.psx_create(ctypes.byref(self._p), int(device), ctypes.byref(h)))
         self.h = h
 
     def close(self):

@@ -108,3 +108,29 @@ def test_partial_fold_is_associative_and_order_fixed():
         np.testing.assert_allclose(val(A, m, s), val(B, m, s), rtol=0, atol=1e-12)
     sa = np.frombuffer(full[ldg * 56: ldg * 56 + 56].tobytes(), dtype=E.SETREC_DTYPE)[0]
     assert sa["npat"] == 28 and sa["score"] == -3.0
+
+
+def test_model_inputs_shape_helpers_without_gpu():
+    """ModelInputs (the psx_create_from_ld route) exposes the same host-only
+    helpers as Seam; creating an engine from it without a GPU fails loudly."""
+    L = loci.read_locus("example")
+    mi = E.model_inputs(L["ld"], L["z"], L["u2l"], (334324, 6771), max_causal=2, sharing_param=0.25)
+    assert mi.count_configs() == 216_817
+    assert mi.N == 441 and mi.n_union == L["u2l"].shape[1]
+    if E.device_count() > 0:
+        pytest.skip("a HIP device is present")
+    with pytest.raises(E.EngineError) as ei:
+        E.PostCal(mi)
+    assert ei.value.code == E.PSX_ENODEV
+    with pytest.raises(E.EngineError):
+        E.lu_det(np.eye(3), gpu=True)
+
+
+def test_host_lu_det_matches_numpy_and_underflows_like_gsl():
+    rng = np.random.default_rng(1)
+    a = rng.standard_normal((30, 30))
+    assert math.isclose(E.lu_det(a), np.linalg.det(a), rel_tol=1e-10)
+    idx = np.arange(1800)
+    # index-order product of U_ii = 0.64 sticks at the smallest subnormal; 0.19 flushes to 0
+    assert E.lu_det(0.6 ** np.abs(idx[:, None] - idx[None, :])) == 5e-324
+    assert E.lu_det(0.9 ** np.abs(idx[:, None] - idx[None, :])) == 0.0

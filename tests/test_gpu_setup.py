@@ -1,0 +1,144 @@
+"""GPU Model setup (psx_create_from_ld; model.h:171-264, util.cpp:195-263).
+
+* The PSD-shift determinant on the GPU is bit-identical to the host
+  restatement of GSL's elimination (model.cpp lu_det), including the
+  index-order product's underflow behaviour.
+* PostCal built from LD + z on the GPU (no eigendecomposition when Sigma' is
+  positive definite) matches PostCal built from the reference's own low-rank
+  B / S' (host eigen route) and the oracle.
+Marked gpu; run on an MI355X."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import loci
+from oracle import oracle as O
+from pipsort_amd import engine as E
+from pipsort_amd import synth
+from test_gpu_parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(x):
+    return np.float64(x).view(np.uint64)
+
+
+def _det_cases():
+    rng = np.random.default_rng(5)
+    cases = {
+        "n1": np.array([[0.3]]),
+        "n2_swap": np.array([[1e-3, 2.0], [3.0, 4.0]]),
+        "rand64": rng.standard_normal((64, 64)),
+        "rand257": rng.standard_normal((257, 257)),
+        "ties": rng.integers(-3, 4, (96, 96)).astype(np.float64),  # equal |pivots|: first one wins
+        "singular": np.ones((40, 40)),
+        "ar1_sticky": 0.6 ** np.abs(np.arange(2000)[:, None] - np.arange(2000)[None, :]),  # sticks at 5e-324
+        "ar1_zero": 0.9 ** np.abs(np.arange(1200)[:, None] - np.arange(1200)[None, :]),  # underflows to 0
+    }
+    for d in ("example", "small_example"):
+        L = loci.read_locus(d)
+        for s in range(2):
+            cases[f"{d}{s}"] = L["ld"][s]
+            cases[f"{d}{s}_shift"] = L["ld"][s] + 0.01 * np.eye(L["ld"][s].shape[0])
+    return cases
+
+
+@pytest.mark.parametrize("name", sorted(_det_cases()))
+def test_lu_det_bit_identical(gpu, name):
+    a = _det_cases()[name]
+    h = E.lu_det(a)
+    g = E.lu_det(a, gpu=True)
+    assert _bits(h) == _bits(g), (name, h, g)
+
+
+@pytest.mark.parametrize("d", ["example", "small_example"])
+def test_psd_shift_gpu_matches_host(gpu, d):
+    L = loci.read_locus(d)
+    for s in range(2):
+        sh, ah = E.psd_shift(L["ld"][s])
+        sg, ag = E.psd_shift_gpu(L["ld"][s])
+        assert ah == ag
+        assert np.array_equal(sh, sg)
+
+
+def _both(ld, z, u2l, n, **kw):
+    seam = E.seam_from_arrays(ld, z, u2l, n, **kw)
+    mi = E.model_inputs(ld, z, u2l, n, **kw)
+    return seam, mi
+
+
+def _run(x):
+    pc = E.PostCal(x)
+    pc.run_exhaustive()
+    return pc, pc.accum()
+
+
+@pytest.mark.parametrize("spec", ["example", "small_example"])
+def test_ld_route_matches_eigen_route(gpu, spec):
+    sp = loci.EXAMPLE if spec == "example" else loci.SMALL
+    L = loci.read_locus(sp["dirname"])
+    seam, mi = _both(L["ld"], L["z"], L["u2l"], sp["n"], max_causal=sp["c"], sharing_param=sp["p"])
+    pc, got = _run(mi)
+    info = pc.setup_info
+    assert info["eigen_route"] == [0, 0]
+    for s in range(2):
+        assert info["psd_added"][s] == E.psd_shift(L["ld"][s])[1]
+    assert_parity(got, O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-9)
+    _, ref = _run(seam)
+    assert_parity(got, ref.__dict__, pip_tol=1e-9, ll_rtol=1e-9)
+
+
+@pytest.mark.parametrize("M0,M1,shared,c", [(90, 110, 60, 3), (130, 70, 5, 2), (1, 3, 1, 3)])
+def test_ld_route_mixed_loci(gpu, M0, M1, shared, c):
+    ld, z, _, _, u2l = synth.mixed_locus(M0, M1, shared, seed=M0 + M1)
+    seam, mi = _both(ld, z, u2l, (5000, 9000), max_causal=c, sharing_param=0.5)
+    _, got = _run(mi)
+    assert_parity(got, O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-9)
+
+
+def test_ld_route_syn1000(gpu):
+    """The bench locus: GPU setup vs host eigen route, full sweep, PIPs 1e-9."""
+    ld, z, _, _, u2l = synth.syn_v1(1000)
+    seam, mi = _both(ld, z, u2l, (10000, 8000), max_causal=2, sharing_param=0.25)
+    pc, got = _run(mi)
+    assert pc.setup_info["eigen_route"] == [0, 0]
+    _, ref = _run(seam)
+    assert_parity(got, ref.__dict__, pip_tol=1e-9, ll_rtol=1e-9)
+
+
+def test_indefinite_sigma_takes_eigen_route(gpu):
+    """det > 0 with two negative eigenvalues: the PSD loop stops at a = 0 and the
+    reference's |W| differs from Sigma'; the engine must take the eigen route."""
+    rng = np.random.default_rng(3)
+    M = 40
+    q, _ = np.linalg.qr(rng.standard_normal((M, M)))
+    w = np.linspace(0.2, 3.0, M)
+    w[:2] = [-0.3, -0.5]
+    sig = (q * w) @ q.T
+    sig = (sig + sig.T) / 2
+    assert E.lu_det(sig) > 0
+    ld = [sig, 0.5 ** np.abs(np.arange(M)[:, None] - np.arange(M)[None, :])]
+    z = [rng.standard_normal(M) * 2, rng.standard_normal(M) * 2]
+    u2l = np.stack([np.arange(M), np.arange(M)]).astype(np.int32)
+    seam, mi = _both(ld, z, u2l, (6000, 7000), max_causal=2, sharing_param=0.4)
+    pc, got = _run(mi)
+    assert pc.setup_info["eigen_route"] == [1, 0]
+    assert_parity(got, O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-9)
+
+
+def test_cli_host_setup_route_still_reproduces_goldens(gpu, tmp_path):
+    """PSX_HOST_SETUP=1 keeps the reference's eigen route in the drop-in CLI."""
+    d = tmp_path / "example"
+    shutil.copytree(os.path.join(loci.GOLDEN, "example"), d)
+    env = dict(os.environ, PSX_HOST_SETUP="1")
+    r = subprocess.run([E.PIPSORT_BIN, "-c", "2", "-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "snp_map", "-n",
+                        "334324,6771", "-p", "0.25", "-o", "pipsort_results"], cwd=d, capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Time for eigen decomp" in r.stdout
+    for f in ("study0_post", "study1_post", "study0_set", "study1_set", "nocausal"):
+        assert open(d / f"pipsort_results_{f}.txt").read() == open(d / f"expected_{f}.txt").read(), f
