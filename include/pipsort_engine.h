@@ -134,6 +134,22 @@ int psx_set_shard(psx_engine *e, int rank, int world);
  * checkOR (postcal.cpp:1111-1126).  Resets and fills the accumulators. */
 int psx_run_exhaustive(psx_engine *e);
 
+/* Asynchronous exhaustive pass: enqueue one pass on the engine stream and
+ * return at once (no host synchronisation), so back-to-back passes and the
+ * multi-GPU exchange (psx_export_partials / collective / psx_merge_partials on
+ * the same stream) pipeline on the device.  The fast kernel's EXACT flag is
+ * collected in a sticky device word (and OR-ed across ranks by
+ * psx_merge_partials); psx_sync waits for the stream and reports it.  Results
+ * are valid only when psx_sync returns *exact_needed == 0; otherwise redo the
+ * pass with psx_run_exhaustive (which reruns the exact variant where needed)
+ * and repeat the exchange.  Falls back to psx_run_exhaustive for problems the
+ * fused pass does not cover (c not in {2, 3}). */
+int psx_run_exhaustive_async(psx_engine *e);
+/* Wait for all work enqueued on the engine stream; *exact_needed = sticky EXACT
+ * flag since the last psx_sync (cleared).  Timing of the asynchronous passes
+ * since the last sync: kernel_ms summed over kernel_launches passes. */
+int psx_sync(psx_engine *e, int32_t *exact_needed);
+
 /* PostCal::computeTotalLikelihoodGivenConfigs (postcal.cpp:400-714): rows of
  * int16 global SNP indices (-1 = none), [n_rows][n_groups] (the -b file). */
 int psx_run_configs(psx_engine *e, const int16_t *rows, int64_t n_rows, int32_t n_groups);

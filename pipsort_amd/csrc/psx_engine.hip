@@ -270,7 +270,7 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
 // merge `count` concatenated partial images (rank order) into acc / sacc.
 // Image layout: Acc5[ldg] followed by one Acc5-sized slot holding the SetRec.
 __global__ void k_merge_partials(const Acc5* __restrict__ parts, int U, int ldg, int count, Acc5* __restrict__ acc,
-                                 SetRec* __restrict__ sacc) {
+                                 SetRec* __restrict__ sacc, int* __restrict__ flag) {
     const size_t stride = (size_t)ldg + 1;
     int u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u < U) {
@@ -280,8 +280,14 @@ __global__ void k_merge_partials(const Acc5* __restrict__ parts, int U, int ldg,
     }
     if (u == 0) {
         SetRec s = psx::set_zero();
-        for (int r = 0; r < count; r++)
-            psx::fold_set(s, *reinterpret_cast<const SetRec*>(parts + (size_t)r * stride + ldg));
+        int f = 0;
+        for (int r = 0; r < count; r++) {
+            const SetRec& x = *reinterpret_cast<const SetRec*>(parts + (size_t)r * stride + ldg);
+            psx::fold_set(s, x);
+            f |= x.pad;  // any rank's EXACT flag
+        }
+        s.pad = f;
+        flag[1] |= f;
         *sacc = s;
     }
 }
@@ -376,6 +382,7 @@ __global__ __launch_bounds__(256) void k_merge_pass_l1(DevProb P, int lo, int hi
             // hand the pass's EXACT flag to the host in the status record and re-arm
             // it for the next pass (the kernels that raise it have completed)
             g.pad = *flag;
+            flag[1] |= g.pad;  // sticky copy for asynchronous passes (psx_sync)
             *flag = 0;
             *sacc = g;
         }
@@ -472,6 +479,12 @@ struct psx_engine {
         bool ran = false;
     };
     std::map<std::tuple<int, int, int>, GenLevel> glevels;
+    // asynchronous passes (psx_run_exhaustive_async): ring of (start, end)
+    // event pairs around the dominant kernel, consumed oldest-first
+    static constexpr int kRing = 64;
+    hipEvent_t aev[2 * kRing] = {};
+    int a_head = 0, a_pending = 0, a_count = 0;
+    double a_kms = 0;
     // timing
     hipEvent_t ev[4];
     psx_timing timing;
@@ -493,6 +506,7 @@ psx_engine::~psx_engine() {
         for (int i = 0; i < 2; i++) if (g.ev[i]) hipEventDestroy(g.ev[i]);
     }
     for (int i = 0; i < 4; i++) hipEventDestroy(ev[i]);
+    for (int i = 0; i < 2 * kRing; i++) if (aev[i]) hipEventDestroy(aev[i]);
     if (own_stream) hipStreamDestroy(own_stream);
 }
 
@@ -846,7 +860,19 @@ bool fused_eligible(const psx_engine* e) {
 // SNP: level 1, then 2, then 3; scalars: null configuration, level-1 sets,
 // every unit record) are one launch.  Deterministic: the fold order is fixed
 // by the plans, not by scheduling.
-int fused_pass(psx_engine* e, int* flag) {
+// consume the oldest recorded asynchronous kernel interval
+int consume_async(psx_engine* e) {
+    const int r = ((e->a_head - e->a_pending) % psx_engine::kRing + psx_engine::kRing) % psx_engine::kRing;
+    HIPCHK(hipEventSynchronize(e->aev[2 * r + 1]));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e->aev[2 * r], e->aev[2 * r + 1]));
+    e->a_kms += ms;
+    e->a_count++;
+    e->a_pending--;
+    return 0;
+}
+
+int fused_pass(psx_engine* e, int* flag, bool async = false) {
     const psx::SweepArgs sa = sweep_args(e);
     psx::SweepPlan* P2 = nullptr;
     psx::SweepPlan* P3 = nullptr;
@@ -863,9 +889,22 @@ int fused_pass(psx_engine* e, int* flag) {
     // padding slots stay zero from psx_create, and the EXACT flag was re-armed
     // by the previous merge (or psx_create)
     HIPCHK(hipEventRecord(e->ev[0], A));
+    int slot = 0;
+    if (async) {
+        if (e->a_pending == psx_engine::kRing && (rc = consume_async(e))) return rc;
+        slot = e->a_head;
+        for (int i = 0; i < 2; i++)
+            if (!e->aev[2 * slot + i]) HIPCHK(hipEventCreate(&e->aev[2 * slot + i]));
+        HIPCHK(hipEventRecord(e->aev[2 * slot], A));
+    }
     // the top level; level 2 (c = 3) rides in the same launch
     if (psx::sweep_kernel(e->plans, *top, A, sa, e->dpass + nl, false, low, e->dpass))
         return fail(PSX_EHIP, std::string("sweep level ") + std::to_string(top->k) + ": " + psx::sweep_error());
+    if (async) {
+        HIPCHK(hipEventRecord(e->aev[2 * slot + 1], A));
+        e->a_head = (e->a_head + 1) % psx_engine::kRing;
+        e->a_pending++;
+    }
     const int lo = (int)((int64_t)e->U * e->rank / e->world), hi = (int)((int64_t)e->U * (e->rank + 1) / e->world);
     const SetRec extra = e->rank == 0 ? null_rec(e, 1.0) : psx::set_zero();
     const psx::SweepPlan* mA = low ? low : top;
@@ -875,6 +914,10 @@ int fused_pass(psx_engine* e, int* flag) {
                        e->dacc, e->dsacc, e->dflag);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(e->ev[1], A));
+    if (async) {
+        *flag = 0;
+        return 0;
+    }
     HIPCHK(hipMemcpyAsync(e->hstat, e->dsacc, kStatBytes, hipMemcpyDeviceToHost, A));
     HIPCHK(hipStreamSynchronize(A));
     SetRec s;
@@ -882,6 +925,8 @@ int fused_pass(psx_engine* e, int* flag) {
     *flag = s.pad;
     return 0;
 }
+
+int fill_timing(psx_engine* e, double gms, int flag);
 
 }  // namespace
 
@@ -1214,7 +1259,42 @@ int psx_run_exhaustive(psx_engine* e) {
     }
     if (flag) {  // some set's notSharedLL group sits > 900 bits below its maximum: exact variant
         if ((rc = exhaustive_pass(e, true, &gms))) return rc;
+        HIPCHK(hipMemsetAsync(e->dflag + 1, 0, sizeof(int), e->stream));  // handled: clear the sticky copy
     }
+    return fill_timing(e, gms, flag);
+}
+
+int psx_run_exhaustive_async(psx_engine* e) {
+    HIPCHK(hipSetDevice(e->dev));
+    if (!fused_eligible(e) || std::getenv("PSX_NO_FUSED_PASS")) return psx_run_exhaustive(e);
+    int flag = 0;
+    return fused_pass(e, &flag, true);
+}
+
+int psx_sync(psx_engine* e, int32_t* exact_needed) {
+    HIPCHK(hipSetDevice(e->dev));
+    int rc;
+    HIPCHK(hipMemcpyAsync(e->hstat, e->dsacc, kStatBytes, hipMemcpyDeviceToHost, e->stream));
+    int sticky = 0;
+    HIPCHK(hipMemcpyAsync(&sticky, e->dflag + 1, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemsetAsync(e->dflag + 1, 0, sizeof(int), e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (exact_needed) *exact_needed = sticky;
+    if (e->a_pending == 0 && e->a_count == 0) return 0;  // nothing asynchronous since the last sync
+    while (e->a_pending > 0)
+        if ((rc = consume_async(e))) return rc;
+    if ((rc = fill_timing(e, 0.0, sticky))) return rc;
+    e->timing.kernel_ms = e->a_kms;
+    e->timing.kernel_launches = e->a_count;
+    e->a_kms = 0;
+    e->a_count = 0;
+    return 0;
+}
+
+}  // extern "C"
+
+namespace {
+int fill_timing(psx_engine* e, double gms, int flag) {
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
     psx::SweepStats st;
@@ -1243,6 +1323,9 @@ int psx_run_exhaustive(psx_engine* e) {
     e->timing.configs = (uint64_t)(s.npat + 0.5);
     return 0;
 }
+}  // namespace
+
+extern "C" {
 
 int psx_eval_union_batch(psx_engine* e, const int32_t* sets, int32_t stride, int32_t n_sets, int accumulate,
                          double* score_out) {
@@ -1548,7 +1631,7 @@ int psx_merge_partials(psx_engine* e, const void* src, int32_t count) {
     HIPCHK(hipSetDevice(e->dev));
     if (count < 1) return fail(PSX_EINVAL, "count < 1");
     hipLaunchKernelGGL(k_merge_partials, dim3((e->U + 255) / 256), dim3(256), 0, e->stream, (const Acc5*)src, e->U,
-                       e->ldg, count, e->dacc, e->dsacc);
+                       e->ldg, count, e->dacc, e->dsacc, e->dflag);
     HIPCHK(hipGetLastError());
     if (!e->external_stream) HIPCHK(hipStreamSynchronize(e->stream));
     return 0;

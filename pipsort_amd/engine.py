@@ -34,6 +34,7 @@ EXPORTED = [
     "psx_fold_partials_host", "psx_shard_stats", "psx_set_stream",
     "psx_psd_shift", "psx_lowrank_study", "psx_sym_eigen", "psx_lu_det",
     "psx_create_from_ld", "psx_psd_shift_gpu", "psx_lu_det_gpu",
+    "psx_run_exhaustive_async", "psx_sync",
 ]
 
 
@@ -162,6 +163,8 @@ def load_library(path: str = LIB_PATH):
         "psx_create_from_ld": (c_int, [P(_LdProblem), c_int, P(vp), P(SetupInfo)]),
         "psx_psd_shift_gpu": (c_int, [P(dbl), c_i32, P(dbl), c_int]),
         "psx_lu_det_gpu": (c_int, [P(dbl), c_i32, c_int, P(dbl)]),
+        "psx_run_exhaustive_async": (c_int, [vp]),
+        "psx_sync": (c_int, [vp, P(c_i32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -465,6 +468,17 @@ class PostCal:
     def run_exhaustive(self):
         """postcal.cpp:716 computeTotalLikelihood."""
         _check(self.lib.psx_run_exhaustive(self.h))
+
+    def run_exhaustive_async(self):
+        """Enqueue one exhaustive pass without host synchronisation (psx_run_exhaustive_async)."""
+        _check(self.lib.psx_run_exhaustive_async(self.h))
+
+    def sync(self) -> bool:
+        """Wait for the engine stream; True if some asynchronous pass since the last
+        sync needs the exact rerun (its results are then not valid)."""
+        f = ctypes.c_int32(0)
+        _check(self.lib.psx_sync(self.h, ctypes.byref(f)))
+        return bool(f.value)
 
     def run_configs(self, rows: np.ndarray):
         """postcal.cpp:400 computeTotalLikelihoodGivenConfigs; rows int16 [n, groups]."""

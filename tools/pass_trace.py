@@ -19,7 +19,7 @@ ap.add_argument("--world", type=int, default=8)
 ap.add_argument("--steps", type=int, default=20)
 a = ap.parse_args()
 torch.cuda.set_device(0)
-seam = bench.build_seam(a.workload)
+seam = bench.build_inputs(a.workload)
 pc = E.PostCal(seam, device=0)
 pc.set_shard(a.rank, a.world)
 import time
