@@ -355,7 +355,8 @@ __global__ __launch_bounds__(256) void k_merge_pass_l1(DevProb P, int lo, int hi
                                                        const int* __restrict__ dptrA, const Acc5* __restrict__ recB,
                                                        const int* __restrict__ dptrB, const SetRec* __restrict__ srec,
                                                        long nsrec, SetRec extra, Acc5* __restrict__ acc,
-                                                       SetRec* __restrict__ sacc, int* __restrict__ flag) {
+                                                       SetRec* __restrict__ sacc, int* __restrict__ flag,
+                                                       int* __restrict__ sticky) {
     const int tid = threadIdx.x;
     if (blockIdx.x == 0) {
         __shared__ SetRec ss[4];
@@ -381,9 +382,10 @@ __global__ __launch_bounds__(256) void k_merge_pass_l1(DevProb P, int lo, int hi
             for (int w = 0; w < 4; w++) psx::fold_set(g, ss[w]);
             // hand the pass's EXACT flag to the host in the status record and re-arm
             // it for the next pass (the kernels that raise it have completed)
-            g.pad = *flag;
-            flag[1] |= g.pad;  // sticky copy for asynchronous passes (psx_sync)
-            *flag = 0;
+            // (atomic exchange: with pipelined passes the next pass's sweep may
+            // already be raising its own flag word; the sticky word collects all)
+            g.pad = atomicExch(flag, 0);
+            atomicOr(sticky, g.pad);  // sticky copy for asynchronous passes (psx_sync)
             *sacc = g;
         }
         return;
@@ -482,6 +484,13 @@ struct psx_engine {
     // asynchronous passes (psx_run_exhaustive_async): ring of (start, end)
     // event pairs around the dominant kernel, consumed oldest-first
     static constexpr int kRing = 64;
+    // pipelined asynchronous passes: sweeps on a compute stream, merges (and the
+    // caller's exchange) on `stream`; record buffers alternate by pass parity
+    hipStream_t cstream = nullptr;
+    static constexpr int kBufs = 3;  // record buffer sets: sweep i waits for merge i - 3
+    hipEvent_t mdone[kBufs] = {};
+    bool mdone_rec[kBufs] = {};
+    int a_par = kBufs - 1;
     hipEvent_t aev[2 * kRing] = {};
     int a_head = 0, a_pending = 0, a_count = 0;
     double a_kms = 0;
@@ -507,6 +516,9 @@ psx_engine::~psx_engine() {
     }
     for (int i = 0; i < 4; i++) hipEventDestroy(ev[i]);
     for (int i = 0; i < 2 * kRing; i++) if (aev[i]) hipEventDestroy(aev[i]);
+    for (int i = 0; i < kBufs; i++)
+        if (mdone[i]) hipEventDestroy(mdone[i]);
+    if (cstream) { hipStreamSynchronize(cstream); hipStreamDestroy(cstream); }
     if (own_stream) hipStreamDestroy(own_stream);
 }
 
@@ -872,6 +884,10 @@ int consume_async(psx_engine* e) {
     return 0;
 }
 
+// Asynchronous passes are pipelined: pass i's sweep runs on the compute stream
+// into the record buffers of parity i & 1 while the merge of pass i - 1 and the
+// caller's exchange (export / collective / merge of partials) run on the engine
+// stream.  Sweep i waits for merge i - 2 (same buffers), merge i for sweep i.
 int fused_pass(psx_engine* e, int* flag, bool async = false) {
     const psx::SweepArgs sa = sweep_args(e);
     psx::SweepPlan* P2 = nullptr;
@@ -882,44 +898,68 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     psx::SweepPlan* top = P3 ? P3 : P2;
     psx::SweepPlan* low = P3 ? P2 : nullptr;
     const size_t nl = low ? (size_t)low->n_units : 0, nt = (size_t)top->n_units;
+    const size_t npass = nl + nt + 1;
     int rc;
-    if ((rc = ensure(e->dpass, e->cap_pass, nl + nt + 1))) return rc;
-    hipStream_t A = e->stream;
+    if ((rc = ensure(e->dpass, e->cap_pass, psx_engine::kBufs * npass))) return rc;
+    hipStream_t X = e->stream;  // merges (and the caller's exchange)
+    hipStream_t S = X;          // sweeps
+    int par = 0;
+    if (async) {
+        if (!e->cstream) {
+            HIPCHK(hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking));
+            for (int i = 0; i < psx_engine::kBufs; i++)
+                HIPCHK(hipEventCreateWithFlags(&e->mdone[i], hipEventDisableTiming));
+        }
+        S = e->cstream;
+        par = e->a_par = (e->a_par + 1) % psx_engine::kBufs;
+        // the merge that last read this buffer set (pass i - kBufs) must be done.
+        // Host-side flow control: blocking here only when the device is more than
+        // kBufs - 1 passes behind keeps barrier packets off the compute stream
+        // (back-to-back sweeps then dispatch with no marker between them).
+        if (e->mdone_rec[par]) HIPCHK(hipEventSynchronize(e->mdone[par]));
+    }
+    SetRec* const dpass = e->dpass + par * npass;
+    int* const pflag = e->dflag + (par ? 1 + par : 0);  // EXACT flag word of this buffer set ([1]: sticky word)
     // no zeroing pass: the merge overwrites every per-SNP slot and the scalars,
-    // padding slots stay zero from psx_create, and the EXACT flag was re-armed
-    // by the previous merge (or psx_create)
-    HIPCHK(hipEventRecord(e->ev[0], A));
+    // padding slots stay zero from psx_create, and the EXACT flag word was
+    // re-armed by the merge that last used it (or psx_create)
     int slot = 0;
+    hipEvent_t k0 = nullptr, k1 = nullptr;  // the sweep launch's own start / stop events
     if (async) {
         if (e->a_pending == psx_engine::kRing && (rc = consume_async(e))) return rc;
         slot = e->a_head;
         for (int i = 0; i < 2; i++)
             if (!e->aev[2 * slot + i]) HIPCHK(hipEventCreate(&e->aev[2 * slot + i]));
-        HIPCHK(hipEventRecord(e->aev[2 * slot], A));
+        k0 = e->aev[2 * slot];
+        k1 = e->aev[2 * slot + 1];
+    } else {
+        HIPCHK(hipEventRecord(e->ev[0], S));
     }
     // the top level; level 2 (c = 3) rides in the same launch
-    if (psx::sweep_kernel(e->plans, *top, A, sa, e->dpass + nl, false, low, e->dpass))
+    if (psx::sweep_kernel(e->plans, *top, S, sa, dpass + nl, false, low, dpass, par, pflag, !async, k0, k1))
         return fail(PSX_EHIP, std::string("sweep level ") + std::to_string(top->k) + ": " + psx::sweep_error());
     if (async) {
-        HIPCHK(hipEventRecord(e->aev[2 * slot + 1], A));
         e->a_head = (e->a_head + 1) % psx_engine::kRing;
         e->a_pending++;
+        HIPCHK(hipStreamWaitEvent(X, k1, 0));  // merge i after sweep i (stop event of its dispatch)
     }
     const int lo = (int)((int64_t)e->U * e->rank / e->world), hi = (int)((int64_t)e->U * (e->rank + 1) / e->world);
     const SetRec extra = e->rank == 0 ? null_rec(e, 1.0) : psx::set_zero();
-    const psx::SweepPlan* mA = low ? low : top;
-    const psx::SweepPlan* mB = low ? top : nullptr;
-    hipLaunchKernelGGL(k_merge_pass_l1, dim3(e->U + 1), dim3(256), 0, A, e->dp, lo, hi, mA->d_rec, mA->d_dptr,
-                       mB ? mB->d_rec : nullptr, mB ? mB->d_dptr : nullptr, e->dpass, (long)(nl + nt), extra,
-                       e->dacc, e->dsacc, e->dflag);
+    psx::SweepPlan* mA = low ? low : top;
+    psx::SweepPlan* mB = low ? top : nullptr;
+    hipLaunchKernelGGL(k_merge_pass_l1, dim3(e->U + 1), dim3(256), 0, X, e->dp, lo, hi, psx::plan_records(*mA, par),
+                       mA->d_dptr, mB ? psx::plan_records(*mB, par) : nullptr, mB ? mB->d_dptr : nullptr, dpass,
+                       (long)(nl + nt), extra, e->dacc, e->dsacc, pflag, e->dflag + 1);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(e->ev[1], A));
     if (async) {
+        HIPCHK(hipEventRecord(e->mdone[par], X));
+        e->mdone_rec[par] = true;
         *flag = 0;
         return 0;
     }
-    HIPCHK(hipMemcpyAsync(e->hstat, e->dsacc, kStatBytes, hipMemcpyDeviceToHost, A));
-    HIPCHK(hipStreamSynchronize(A));
+    HIPCHK(hipEventRecord(e->ev[1], X));
+    HIPCHK(hipMemcpyAsync(e->hstat, e->dsacc, kStatBytes, hipMemcpyDeviceToHost, X));
+    HIPCHK(hipStreamSynchronize(X));
     SetRec s;
     std::memcpy(&s, e->hstat, sizeof(SetRec));
     *flag = s.pad;
@@ -1283,9 +1323,26 @@ int psx_sync(psx_engine* e, int32_t* exact_needed) {
     if (e->a_pending == 0 && e->a_count == 0) return 0;  // nothing asynchronous since the last sync
     while (e->a_pending > 0)
         if ((rc = consume_async(e))) return rc;
-    if ((rc = fill_timing(e, 0.0, sticky))) return rc;
+    // timing of the asynchronous passes since the last sync: the dominant
+    // kernel's summed device time over its launches, per-launch work from the plan
+    std::memset(&e->timing, 0, sizeof(e->timing));
+    const psx::SweepArgs sa = sweep_args(e);
+    psx::SweepPlan* P2 = nullptr;
+    psx::SweepPlan* P3 = nullptr;
+    if (psx::sweep_prepare(e->plans, 2, e->U, e->ldg, e->rank, e->world, e->stream, sa, false, &P2) ||
+        (e->maxc == 3 && psx::sweep_prepare(e->plans, 3, e->U, e->ldg, e->rank, e->world, e->stream, sa, false, &P3)))
+        return fail(PSX_EHIP, std::string("sweep plan: ") + psx::sweep_error());
+    const psx::SweepPlan* top = P3 ? P3 : P2;
     e->timing.kernel_ms = e->a_kms;
     e->timing.kernel_launches = e->a_count;
+    e->timing.sweep_ms = e->a_count ? e->a_kms / e->a_count : 0.0;
+    e->timing.union_sets = top->union_sets;
+    e->timing.alg_bytes = top->alg_bytes + top->fused_bytes;
+    e->timing.flops = top->flops + top->fused_flops;
+    e->timing.exact_rerun = sticky;
+    SetRec st;
+    std::memcpy(&st, e->hstat, sizeof(SetRec));
+    e->timing.configs = (uint64_t)(st.npat + 0.5);
     e->a_kms = 0;
     e->a_count = 0;
     return 0;

@@ -46,6 +46,8 @@ struct SweepPlan {
     double alg_bytes = 0, flops = 0;
     int4* d_units = nullptr;     // {a0, a1, B, T}
     Acc5* d_rec = nullptr;       // records in CSR (per-SNP) order
+    Acc5* d_rec_alt[2] = {nullptr, nullptr};  // more record buffers (pipelined asynchronous passes)
+    size_t rec_len = 0;          // records per buffer
     SetRec* d_srec = nullptr;    // [n_units]
     int* d_csr = nullptr;        // ptr[n_rows+1], row_snp[n_rows], pos[n_units * rec_stride]
     const int* d_pos = nullptr;  // record slot -> CSR position (inside d_csr)
@@ -71,10 +73,12 @@ struct Sweep3Args {
     double rsd[2];             // d_s^{-1/2}
     double rho, pit0;          // pit[nsh] = pit0 * rho^nsh (prior per member is multiplicative)
     int U, ldg, pad, Ck;
+    unsigned long long* trace = nullptr;  // diagnostics (PSX_UNIT_TRACE): per unit {start, end, hw id, unit}
 };
 struct Level2Blocks;  // psx_sweep_dev.h
 int launch_sweep3(bool allpres, const Sweep3Args& A, int n_units, const int4* units, Acc5* rec, SetRec* srec,
-                  int rec_stride, int* flag, const int* pos, hipStream_t st, const Level2Blocks* l2);
+                  int rec_stride, int* flag, const int* pos, hipStream_t st, const Level2Blocks* l2, hipEvent_t ev0 = nullptr,
+                  hipEvent_t ev1 = nullptr);
 int launch_scale_y(const double* y, int n, double* ys, hipStream_t st);
 int launch_build_skewT(const double* G, int ldg, int pad, double* skew, hipStream_t st);
 
@@ -94,7 +98,7 @@ struct SweepPlanCache {
 };
 
 bool sweep_supports(int k, int U);
-struct PlanUnit { int a0, a1, B, T; double work; };
+struct PlanUnit { int a0, a1, B, T; double work; int j0 = 0, j1 = 64; };
 int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* pres_host,
                std::vector<PlanUnit>& mine, int& ca, double& sets, double& configs, double& bytes);
 // k = 3 fast-kernel decomposition: units (a0, a1, K, C) in v space
@@ -109,8 +113,16 @@ int sweep_level(SweepPlanCache& cache, int k, int U, int ldg, int rank, int worl
 // k = 3 fast kernel (set records into srec2), else right after it.
 int sweep_prepare(SweepPlanCache& cache, int k, int U, int ldg, int rank, int world, hipStream_t stream,
                   const SweepArgs& a, bool exact, SweepPlan** out);
+// parity selects the record buffer (0: d_rec, 1, 2: d_rec_alt, allocated on
+// first use); flag overrides the cache's EXACT flag word; timed = false skips the
+// plan's own timing events (asynchronous passes time the kernel themselves).
+// ev0 / ev1 (optional): start / stop events recorded by the top-level kernel's
+// own dispatch (hipExtLaunchKernel), used by pipelined asynchronous passes.
 int sweep_kernel(SweepPlanCache& cache, SweepPlan& plan, hipStream_t stream, const SweepArgs& a, SetRec* srec_out,
-                 bool exact, SweepPlan* l2, SetRec* srec2);
+                 bool exact, SweepPlan* l2, SetRec* srec2, int parity = 0, int* flag = nullptr, bool timed = true,
+                 hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+// the record buffer of a parity (allocating the second one on first use)
+Acc5* plan_records(SweepPlan& plan, int parity);
 int sweep_flag(SweepPlanCache& cache, int* flag);                          // after sync
 int sweep_stats(SweepPlanCache& cache, int k, int U, int rank, int world, SweepStats* st);  // after sync
 void sweep_free(SweepPlanCache& cache);

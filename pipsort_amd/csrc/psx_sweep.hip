@@ -15,6 +15,10 @@
 // step), turns each into a split weight 2^n * mu (psx_math.h), and folds the
 // 3^k study assignments (postcal.cpp:907-1030 for the masks passing checkOR).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
+
+#include <cstdio>
+#include <cstdlib>
 
 #include <algorithm>
 #include <array>
@@ -186,7 +190,7 @@ int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* 
         double total_a = 0;
         for (int T = 0; T < nblk; T++)
             for (int B = 0; B <= T; B++) total_a += std::min(64 * B + 63, U);
-        ca = (int)std::floor(total_a / (4096.0 * world));
+        ca = (int)std::floor(total_a / (4096.0 * world));  // exact-variant kernel (k_sweep<3, true>)
         ca = std::max(1, std::min(64, ca));
         for (int T = 0; T < nblk; T++) {
             if (64 * T >= U) break;
@@ -288,7 +292,23 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     double total_a = 0;
     for (int C = 0; C < nblk; C++)
         for (int K = 0; K <= C; K++) total_a += std::max(0, 64 * K + 63 - pad);
-    ca = (int)std::floor(total_a / (4096.0 * world));
+    // a-chunk size: k_sweep3 holds 2 waves per SIMD (233 VGPRs), i.e. 8 unit
+    // slots per CU.  Units cost about the same whatever their masking, so the
+    // last dispatch round is the tail: aim for >= 8 rounds per shard and take
+    // the smallest chunk that gets there (measured on MI355X, syn1000c3:
+    // ca = 2 at world 1, ca = 1 for shards of world >= 2, profiles/).
+    static const double kTarget = [] {  // units per shard the a-chunk is sized for
+        if (const char* v = std::getenv("PSX_K3_UNITS")) return std::atof(v);
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) {
+            hipDeviceProp_t pr;
+            if (hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0)
+                cus = pr.multiProcessorCount;
+        }
+        return 8.0 * (8.0 * cus);
+    }();
+    ca = (int)std::floor(total_a / (kTarget * world));
+    if (const char* v = std::getenv("PSX_K3_CA")) ca = std::atoi(v);
     ca = std::max(1, std::min(64, ca));
     std::vector<PlanUnit> all;
     for (int C = 0; C < nblk; C++) {
@@ -354,6 +374,26 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
                 }
         }
     }
+    // optional (PSX_K3_SPLIT): the last dispatch round runs half units (b-walk
+    // steps [0, 32) and [32, 64) of the same (a-chunk, K, C)).  Measured neutral
+    // on MI355X (world-8 shard 0.350 vs 0.352 ms: the tail is ~9 % of the
+    // launch either way, tools/unit_trace.py), so off by default.  Totals above
+    // are unchanged.
+    const size_t slots = (size_t)(kTarget / 8.0);
+    if (std::getenv("PSX_K3_SPLIT") && mine.size() > 2 * slots) {
+        std::vector<PlanUnit> out(mine.begin(), mine.end() - slots);
+        for (size_t i = mine.size() - slots; i < mine.size(); i++) {
+            PlanUnit h = mine[i];
+            h.work *= 0.5;
+            h.j0 = 0;
+            h.j1 = 32;
+            out.push_back(h);
+            h.j0 = 32;
+            h.j1 = 64;
+            out.push_back(h);
+        }
+        mine.swap(out);
+    }
     return 0;
 }
 
@@ -382,7 +422,10 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     const int pad = variant ? ldg - U : 0;  // record keys of variant 1 are in v space
     // device buffers
     std::vector<int4> hu(P.n_units);
-    for (int i = 0; i < P.n_units; i++) hu[i] = make_int4(mine[i].a0, mine[i].a1, mine[i].B, mine[i].T);
+    // variant 1 packs the b-walk step range of (half) units into the high bits
+    for (int i = 0; i < P.n_units; i++)
+        hu[i] = variant ? make_int4(mine[i].a0, mine[i].a1, mine[i].B | (mine[i].j0 << 16), mine[i].T | (mine[i].j1 << 16))
+                        : make_int4(mine[i].a0, mine[i].a1, mine[i].B, mine[i].T);
     if (P.n_units > 0) {
         SWCHK(hipMalloc(&P.d_units, sizeof(int4) * P.n_units));
         SWCHK(hipMemcpy(P.d_units, hu.data(), sizeof(int4) * P.n_units, hipMemcpyHostToDevice));
@@ -430,6 +473,7 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     packed.insert(packed.end(), rows.begin(), rows.end());
     packed.insert(packed.end(), pos.begin(), pos.end());
     packed.insert(packed.end(), dptr.begin(), dptr.end());
+    P.rec_len = idx.size();
     if (!idx.empty()) SWCHK(hipMalloc(&P.d_rec, sizeof(Acc5) * idx.size()));
     if (!packed.empty()) {
         SWCHK(hipMalloc(&P.d_csr, sizeof(int) * packed.size()));
@@ -564,21 +608,39 @@ static void mark_last(SweepPlanCache& C, SweepPlan& P) {
     if (other != C.plans.end()) other->second.ran = false;  // stats: the last pass only
 }
 
+Acc5* plan_records(SweepPlan& P, int parity) {
+    if (!parity) return P.d_rec;
+    if (parity < 0 || parity > 2) {
+        g_sweep_err = "bad record buffer index";
+        return nullptr;
+    }
+    Acc5*& r = P.d_rec_alt[parity - 1];
+    if (!r && P.rec_len > 0 && hipMalloc(&r, sizeof(Acc5) * P.rec_len) != hipSuccess) {
+        r = nullptr;
+        g_sweep_err = "out of device memory (record buffer)";
+    }
+    return r;
+}
+
 int sweep_kernel(SweepPlanCache& C, SweepPlan& P, hipStream_t st, const SweepArgs& a, SetRec* srec_out, bool exact,
-                 SweepPlan* l2, SetRec* srec2) {
+                 SweepPlan* l2, SetRec* srec2, int parity, int* flag_in, bool timed, hipEvent_t ev0,
+                 hipEvent_t ev1) {
     const int k = P.k, U = P.U, ldg = P.ldg;
     mark_last(C, P);
     P.fused_bytes = P.fused_flops = 0;
     const bool ride = l2 && k == 3 && !exact && l2->k == 2 && l2->n_units > 0;
     if (l2) mark_last(C, *l2);
     if (P.n_units == 0 && !ride) {
-        if (l2 && sweep_kernel(C, *l2, st, a, srec2, exact, nullptr, nullptr)) return -1;
+        if (l2 && sweep_kernel(C, *l2, st, a, srec2, exact, nullptr, nullptr, parity, flag_in, timed)) return -1;
         return 0;
     }
     SetRec* srec = srec_out ? srec_out : P.d_srec;
     const TileArgs A = tile_args(C, a, k, U, ldg);
     if (!C.d_flag && sweep_begin(C, st)) return -1;
-    SWCHK(hipEventRecord(P.ev[0], st));
+    int* const flag = flag_in ? flag_in : C.d_flag;
+    Acc5* const rec = plan_records(P, parity);
+    if (!rec && P.rec_len > 0) return -1;
+    if (timed) SWCHK(hipEventRecord(P.ev[0], st));
     const dim3 g(P.n_units), blk(64);
     if (k == 3 && !exact) {
         Sweep3Args S3;
@@ -594,25 +656,42 @@ int sweep_kernel(SweepPlanCache& C, SweepPlan& P, hipStream_t st, const SweepArg
         S3.U = U; S3.ldg = ldg; S3.Ck = A.Ck;
         Level2Blocks b{0, TileArgs{}, nullptr, nullptr, nullptr, nullptr};
         if (ride) {  // level 2 in the same launch: its units are the first blocks of the grid
-            b = Level2Blocks{l2->n_units, tile_args(C, a, 2, U, ldg), l2->d_units, l2->d_rec,
+            Acc5* rec2 = plan_records(*l2, parity);
+            if (!rec2 && l2->rec_len > 0) return -1;
+            b = Level2Blocks{l2->n_units, tile_args(C, a, 2, U, ldg), l2->d_units, rec2,
                              srec2 ? srec2 : l2->d_srec, l2->d_pos};
             P.fused_bytes = l2->alg_bytes;
             P.fused_flops = l2->flops;
         }
-        if (launch_sweep3(C.allpres, S3, P.n_units, P.d_units, P.d_rec, srec, P.rec_stride, C.d_flag, P.d_pos, st,
-                          ride ? &b : nullptr))
+        static const char* trace_path = std::getenv("PSX_UNIT_TRACE");  // diagnostics: unit timeline dump
+        if (trace_path) SWCHK(hipMalloc(&S3.trace, sizeof(unsigned long long) * 4 * (size_t)P.n_units));
+        if (launch_sweep3(C.allpres, S3, P.n_units, P.d_units, rec, srec, P.rec_stride, flag, P.d_pos, st,
+                          ride ? &b : nullptr, ev0, ev1))
             SWCHK(hipGetLastError());
+        if (trace_path) {
+            std::vector<unsigned long long> h(4 * (size_t)P.n_units);
+            SWCHK(hipStreamSynchronize(st));
+            SWCHK(hipMemcpy(h.data(), S3.trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+            SWCHK(hipFree(S3.trace));
+            if (FILE* f = std::fopen(trace_path, "wb")) {
+                std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+                std::fclose(f);
+            }
+        }
     } else if (k == 3)
-        hipLaunchKernelGGL((k_sweep<3, true>), g, blk, 0, st, A, P.d_units, P.d_rec, srec, P.rec_stride, C.d_flag, P.d_pos);
+        hipLaunchKernelGGL((k_sweep<3, true>), g, blk, 0, st, A, P.d_units, rec, srec, P.rec_stride, flag, P.d_pos);
     else if (!exact)
-        hipLaunchKernelGGL((k_sweep<2, false>), g, blk, 0, st, A, P.d_units, P.d_rec, srec, P.rec_stride, C.d_flag, P.d_pos);
+        hipExtLaunchKernelGGL((k_sweep<2, false>), g, blk, 0, st, ev0, ev1, 0, A, P.d_units, rec, srec, P.rec_stride,
+                              flag, P.d_pos);
     else
-        hipLaunchKernelGGL((k_sweep<2, true>), g, blk, 0, st, A, P.d_units, P.d_rec, srec, P.rec_stride, C.d_flag, P.d_pos);
+        hipLaunchKernelGGL((k_sweep<2, true>), g, blk, 0, st, A, P.d_units, rec, srec, P.rec_stride, flag, P.d_pos);
     SWCHK(hipGetLastError());
-    SWCHK(hipEventRecord(P.ev[1], st));
-    SWCHK(hipEventRecord(P.ev[2], st));  // merges (if any) re-record ev[2]
-    P.ran = true;
-    if (l2 && !ride && sweep_kernel(C, *l2, st, a, srec2, exact, nullptr, nullptr)) return -1;
+    if (timed) {
+        SWCHK(hipEventRecord(P.ev[1], st));
+        SWCHK(hipEventRecord(P.ev[2], st));  // merges (if any) re-record ev[2]
+        P.ran = true;
+    }
+    if (l2 && !ride && sweep_kernel(C, *l2, st, a, srec2, exact, nullptr, nullptr, parity, flag_in, timed)) return -1;
     return 0;
 }
 
@@ -644,7 +723,7 @@ int sweep_stats_plan(SweepPlan& P, int k, SweepStats* stats) {
 void sweep_free(SweepPlanCache& C) {
     for (auto& kv : C.plans) {
         SweepPlan& P = kv.second;
-        hipFree(P.d_units); hipFree(P.d_rec); hipFree(P.d_srec); hipFree(P.d_csr);
+        hipFree(P.d_units); hipFree(P.d_rec); hipFree(P.d_rec_alt[0]); hipFree(P.d_rec_alt[1]); hipFree(P.d_srec); hipFree(P.d_csr);
         for (int i = 0; i < 3; i++) if (P.ev[i]) hipEventDestroy(P.ev[i]);
     }
     C.plans.clear();

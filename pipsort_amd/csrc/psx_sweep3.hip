@@ -31,6 +31,7 @@
 // notSharedLL groups more than ~900 bits below a set's scale raise *flag; the
 // host then reruns the level with k_sweep<3, true> (exact group scaling).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <string>
 
@@ -179,8 +180,10 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
 
     const int unit = blockIdx.x - n2;
     const int t = threadIdx.x;
+    const unsigned long long t_start = A.trace ? wall_clock64() : 0ull;
     const int4 un = units[unit];
-    const int a0 = un.x, a1 = un.y, K = un.z, C = un.w;
+    const int a0 = un.x, a1 = un.y, K = un.z & 0xffff, C = un.w & 0xffff;
+    const int j0 = un.z >> 16, j1 = un.w >> 16;  // b-walk steps of this (half) unit
     const int pad = A.pad, ldg = A.ldg;
     const int tile = C * (C + 1) / 2 + K;
     const double rho = A.rho;
@@ -298,7 +301,7 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
         lacc_zero(accA);
         __syncthreads();  // (a, b) terms visible
 
-        for (int j = 0; j < 64; j++) {
+        for (int j = j0; j < j1; j++) {
             const int bs = (t + j) & 63;
             const int vb = 64 * K + bs;
             const bool act = okc && vb > va && vb < vc;
@@ -467,6 +470,14 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
     sr.npat = npat;
     wave_fold_set(sr);
     if (t == 0) srec[unit] = sr;
+    if (A.trace && t == 0) {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        A.trace[4 * (size_t)unit] = t_start;
+        A.trace[4 * (size_t)unit + 1] = wall_clock64();
+        A.trace[4 * (size_t)unit + 2] = hw;
+        A.trace[4 * (size_t)unit + 3] = (unsigned long long)unit;
+    }
 }
 
 // skewT[tile(K, C)][j][t] = G~[64C + t][64K + ((t + j) & 63)] for K <= C, in the
@@ -489,16 +500,19 @@ int launch_build_skewT(const double* G, int ldg, int pad, double* skew, hipStrea
 }
 
 int launch_sweep3(bool allpres, const Sweep3Args& A, int n_units, const int4* units, Acc5* rec, SetRec* srec,
-                  int rec_stride, int* flag, const int* pos, hipStream_t st, const Level2Blocks* l2) {
+                  int rec_stride, int* flag, const int* pos, hipStream_t st, const Level2Blocks* l2, hipEvent_t ev0,
+                  hipEvent_t ev1) {
     const Level2Blocks none{0, TileArgs{}, nullptr, nullptr, nullptr, nullptr};
     const Level2Blocks& b = l2 ? *l2 : none;
     const dim3 grid(n_units + b.n);
+    // with events: their timestamps / completion ride in the dispatch packet
+    // itself (no marker packets between back-to-back passes)
     if (allpres)
-        hipLaunchKernelGGL((k_sweep3<true>), grid, dim3(64), 0, st, A, units, rec, srec, rec_stride, flag, pos, b.n, b.A,
-                           b.units, b.rec, b.srec, b.pos);
+        hipExtLaunchKernelGGL((k_sweep3<true>), grid, dim3(64), 0, st, ev0, ev1, 0, A, units, rec, srec, rec_stride,
+                              flag, pos, b.n, b.A, b.units, b.rec, b.srec, b.pos);
     else
-        hipLaunchKernelGGL((k_sweep3<false>), grid, dim3(64), 0, st, A, units, rec, srec, rec_stride, flag, pos, b.n,
-                           b.A, b.units, b.rec, b.srec, b.pos);
+        hipExtLaunchKernelGGL((k_sweep3<false>), grid, dim3(64), 0, st, ev0, ev1, 0, A, units, rec, srec, rec_stride,
+                              flag, pos, b.n, b.A, b.units, b.rec, b.srec, b.pos);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

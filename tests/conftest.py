@@ -26,6 +26,9 @@ def _built():
 
 @pytest.fixture(scope="session")
 def gpu():
+    # torch's bundled HIP runtime must load before the engine library (same
+    # SONAME, one runtime for both), as in bench.py
+    import torch  # noqa: F401
     from pipsort_amd import engine
     if engine.device_count() < 1:
         pytest.fail("GPU test on a host without a HIP device")

@@ -1,9 +1,12 @@
-"""Run one shard's exhaustive pass repeatedly (for rocprofv3 --kernel-trace):
+"""Run one shard's step repeatedly (for rocprofv3 --kernel-trace):
     python tools/pass_trace.py --rank 0 --world 8 --steps 20
-then tools/trace_gaps.py on the kernel_trace.csv shows the per-pass timeline."""
+A step is the bench step: asynchronous pass + (world > 1) export, one copy
+kernel standing in for the RCCL all-gather, merge.  tools/trace_gaps.py on the
+kernel_trace.csv shows the per-step timeline."""
 import argparse
 import os
 import sys
+import time
 
 import torch
 
@@ -21,14 +24,32 @@ a = ap.parse_args()
 torch.cuda.set_device(0)
 seam = bench.build_inputs(a.workload)
 pc = E.PostCal(seam, device=0)
+stream = torch.cuda.Stream()
+torch.cuda.set_stream(stream)
+pc.set_stream(stream.cuda_stream)
 pc.set_shard(a.rank, a.world)
-import time
+nb = pc.partials_bytes()
+mine = torch.empty(nb, dtype=torch.uint8, device="cuda")
+gathered = torch.empty(nb * a.world, dtype=torch.uint8, device="cuda")
+
+
+def step():
+    pc.run_exhaustive_async()
+    if a.world > 1:
+        pc.export_partials(mine.data_ptr())
+        gathered.view(a.world, nb).copy_(mine.view(1, nb).expand(a.world, nb))
+        pc.merge_partials(gathered.data_ptr(), a.world)
+
+
 for _ in range(3):
-    pc.run_exhaustive()
+    step()
+torch.cuda.synchronize()
+pc.sync()
 t0 = time.perf_counter()
 for _ in range(a.steps):
-    pc.run_exhaustive()
+    step()
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / a.steps * 1e3
-print(f"world {a.world} rank {a.rank}: {dt:.3f} ms per pass; last timing {pc.timing()}", flush=True)
+assert not pc.sync()
+print(f"world {a.world} rank {a.rank}: {dt:.3f} ms per step; timing {pc.timing()}", flush=True)
 pc.close()

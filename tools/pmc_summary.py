@@ -38,8 +38,16 @@ if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
 if "SQ_INSTS_VALU_FLOPS_FP64" in c:
     out["fp64_flops_per_launch"] = c["SQ_INSTS_VALU_FLOPS_FP64"]
 if "SQ_INSTS_VALU" in c and "GRBM_GUI_ACTIVE" in c:
-    # every wave64 VALU instruction occupies its SIMD for 4 cycles; 1024 SIMDs
-    out["valu_busy"] = 4.0 * c["SQ_INSTS_VALU"] / (1024.0 * c["GRBM_GUI_ACTIVE"])
+    # every wave64 VALU instruction occupies its SIMD for 4 cycles; 1024 SIMDs.
+    # GRBM_GUI_ACTIVE is summed over the 8 XCDs (8 x 2.4 GHz x kernel time), so
+    # the kernel's cycle count is GRBM_GUI_ACTIVE / 8.
+    out["gpu_cycles_per_launch"] = c["GRBM_GUI_ACTIVE"] / 8.0
+    out["valu_busy"] = 4.0 * c["SQ_INSTS_VALU"] / (1024.0 * c["GRBM_GUI_ACTIVE"] / 8.0)
+    f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
+                                      "SQ_INSTS_VALU_TRANS_F64"))
+    if f64:
+        out["fp64_valu_insts_per_launch"] = f64
+        out["fp64_valu_share"] = f64 / c["SQ_INSTS_VALU"]
 for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
     if k in c and "SQ_WAVE_CYCLES" in c:
         out[k.lower() + "_frac"] = c[k] / c["SQ_WAVE_CYCLES"]

@@ -1,0 +1,48 @@
+"""Unit timeline of the k = 3 sweep kernel for one shard (diagnostics):
+    python tools/unit_trace.py --world 8 --rank 3
+Runs synchronous passes with PSX_UNIT_TRACE set (each k_sweep3 unit's lane 0
+records wall_clock64() at start / end, 100 MHz) and prints the kernel span,
+unit durations and how many units run concurrently over time."""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+path = "/tmp/psx_unit_trace.bin"
+os.environ["PSX_UNIT_TRACE"] = path
+import torch  # noqa: E402,F401
+import bench  # noqa: E402
+from pipsort_amd import engine as E  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--workload", default="syn1000c3")
+ap.add_argument("--rank", type=int, default=0)
+ap.add_argument("--world", type=int, default=8)
+a = ap.parse_args()
+pc = E.PostCal(bench.build_inputs(a.workload), device=0)
+pc.set_shard(a.rank, a.world)
+for _ in range(3):
+    pc.run_exhaustive()
+tr = np.fromfile(path, dtype=np.uint64).reshape(-1, 4).astype(np.int64)
+st, en = tr[:, 0], tr[:, 1]
+t0 = st.min()
+span = (en.max() - t0) / 100.0
+dur = (en - st) / 100.0
+print(f"world {a.world} rank {a.rank}: {len(tr)} units, kernel span {span:.1f} us (wall_clock64)")
+print(f"unit duration us: mean {dur.mean():.1f} p10 {np.percentile(dur, 10):.1f} p50 {np.median(dur):.1f} "
+      f"p90 {np.percentile(dur, 90):.1f} max {dur.max():.1f}")
+print(f"first-unit starts: {((st - t0) / 100.0)[:5]}; last start {(st.max() - t0) / 100.0:.1f} us; "
+      f"first end {(en.min() - t0) / 100.0:.1f} us")
+edges = np.linspace(0, span, 21)
+mid = 0.5 * (edges[1:] + edges[:-1])
+conc = [int(((st - t0) / 100.0 <= m).sum() - ((en - t0) / 100.0 <= m).sum()) for m in mid]
+print("concurrent units over time (20 bins):", conc)
+order = np.argsort(st)
+print("start time by unit index decile (us):",
+      [round(float((st[order][int(q * (len(st) - 1))] - t0) / 100.0), 1) for q in np.linspace(0, 1, 11)])
+bu = np.array([d.mean() for d in np.array_split(dur[np.argsort(tr[:, 3])], 10)])
+print("mean duration by unit-index decile:", np.round(bu, 1).tolist())
+pc.close()
