@@ -142,3 +142,29 @@ def test_cli_host_setup_route_still_reproduces_goldens(gpu, tmp_path):
     assert "Time for eigen decomp" in r.stdout
     for f in ("study0_post", "study1_post", "study0_set", "study1_set", "nocausal"):
         assert open(d / f"pipsort_results_{f}.txt").read() == open(d / f"expected_{f}.txt").read(), f
+
+
+def test_example_pipeline_end_to_end(gpu, tmp_path):
+    """tests/example/run_example.sh end to end with the drop-in pieces: PIPSORT
+    (GPU setup + sweep) then global / not-shared PIPs; the post-processed files
+    equal what the reference's utils make from the reference's expected files."""
+    from pipsort_amd import postprocess as PP
+    d = tmp_path / "example"
+    shutil.copytree(os.path.join(loci.GOLDEN, "example"), d)
+    r = subprocess.run([E.PIPSORT_BIN, "-c", "2", "-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "snp_map", "-n",
+                        "334324,6771", "-p", "0.25", "-o", "pipsort_results"], cwd=d, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    PP.global_pips(str(d / "pipsort_results_study0_post.txt"), str(d / "pipsort_results_study1_post.txt"),
+                   str(d / "pipsort_results_shared_pips.txt"), str(d / "global_pips.txt"))
+    PP.not_shared_pips(str(d / "pipsort_results_shared_pips.txt"), str(d / "global_pips.txt"),
+                       str(d / "not_shared_pips.txt"))
+    gold = os.path.join(loci.GOLDEN, "postprocess")
+    g = [l.split("\t") for l in (d / "global_pips.txt").read_text().splitlines()]
+    e = [l.split("\t") for l in open(os.path.join(gold, "example_global_pips.txt")).read().splitlines()]
+    assert [x[0] for x in g] == [x[0] for x in e]
+    # global PIPs column: from byte-identical post / shared-PIP files -> identical
+    assert [x[3] for x in g] == [x[3] for x in e]
+    # LL columns: race-affected in the reference (postcal.cpp:1012-1017), 1 line may differ
+    bad = sum(1 for x, y in zip(g[1:], e[1:]) if x[1:3] != y[1:3])
+    assert bad <= 1
