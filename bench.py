@@ -122,6 +122,46 @@ def cpu_baseline(seam, budget_s=15.0, threads=None):
                       f"{dt:.1f} s"}
 
 
+def sss_probe(reps=20):
+    """BASELINE configs[4]: the SSS path (sss_postcal.cpp:102-380) on SYN-v1
+    M = 2000, -c 5 — the walk itself, and the throughput of one SSS proposal
+    batch (the neighbourhood of a 4-SNP configuration, sss_postcal.cpp:20-99:
+    4 x 1996 swaps, 4 removals, 1996 additions) through psx_eval_union_batch
+    with accumulation, inputs resident on the device."""
+    M = 2000
+    ld, z, _, _, u2l = synth.syn_v1(M)
+    mi = E.model_inputs(ld, z, u2l, (10000, 8000), max_causal=5, sharing_param=0.25)
+    pc = E.PostCal(mi)
+    setup_ms = pc.setup_info["setup_ms"]
+    t0 = time.perf_counter()
+    iters = pc.run_sss()
+    walk_ms = (time.perf_counter() - t0) * 1e3
+    walk_configs = pc.accum().n_configs
+    cur = [M // 4 - 1, M // 4, 3 * M // 4, 3 * M // 4 + 1]
+    rest = [u for u in range(M) if u not in cur]
+    sets = []
+    for i in range(4):  # swaps (nbdzero)
+        keep = [c for j, c in enumerate(cur) if j != i]
+        sets += [sorted(keep + [u]) + [-1] for u in rest]
+    sets += [sorted([c for j, c in enumerate(cur) if j != i]) + [-1, -1] for i in range(4)]  # nbdminus
+    sets += [sorted(cur + [u]) for u in rest]  # nbdplus
+    arr = np.array(sets, dtype=np.int32)
+    npat = int(sum(3 ** int((r >= 0).sum()) for r in arr))
+    pc.eval_union_batch(arr, accumulate=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        pc.eval_union_batch(arr, accumulate=True)
+    batch_ms = (time.perf_counter() - t0) * 1e3 / reps
+    pc.close()
+    return {"workload": "SYN-v1 2-study locus, M=2000 SNPs, -c 5 -p 0.25 -n 10000,8000 (BASELINE configs[4])",
+            "gpu_model_setup_and_create_ms": setup_ms, "walk_iterations": iters, "walk_configs": walk_configs,
+            "walk_ms": walk_ms, "batch_sets": len(sets), "batch_configs": npat, "batch_ms": batch_ms,
+            "batch_configs_per_s": npat / (batch_ms / 1e3),
+            "multi_gpu": "replicas only: the walk is serial (host mt19937 sampling between batches) and one "
+                         "batch is sub-millisecond on one GPU"}
+
+
 def example_wall():
     """Wall-clock of the drop-in PIPSORT CLI on tests/example (-c 2 -p 0.25)."""
     import loci
@@ -296,6 +336,7 @@ def main():
             "configs_checked": int(acc.n_configs) if acc is not None else None,
         }
         if world == 1:
+            out["sss"] = sss_probe()
             w, same = example_wall()
             out["example_wall_s"] = w
             out["example_outputs_match_reference"] = same
