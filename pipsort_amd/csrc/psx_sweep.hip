@@ -317,7 +317,10 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
             const int amax = 64 * K + 63;  // a < b <= 64K + 63
             for (int a0 = pad; a0 < amax; a0 += ca) {
                 const int a1 = std::min(a0 + ca, amax);
-                all.push_back({a0, a1, K, C, (double)(a1 - a0)});
+                // a diagonal tile (K == C) runs its folded walk: half the steps
+                // plus the same per-unit / per-a work (measured 0.55 of an
+                // off-diagonal unit, tools/unit_trace.py)
+                all.push_back({a0, a1, K, C, (double)(a1 - a0) * (K == C ? 0.55 : 1.0)});
             }
         }
     }
@@ -664,12 +667,12 @@ int sweep_kernel(SweepPlanCache& C, SweepPlan& P, hipStream_t st, const SweepArg
             P.fused_flops = l2->flops;
         }
         static const char* trace_path = std::getenv("PSX_UNIT_TRACE");  // diagnostics: unit timeline dump
-        if (trace_path) SWCHK(hipMalloc(&S3.trace, sizeof(unsigned long long) * 4 * (size_t)P.n_units));
+        if (trace_path) SWCHK(hipMalloc(&S3.trace, sizeof(unsigned long long) * 8 * (size_t)P.n_units));
         if (launch_sweep3(C.allpres, S3, P.n_units, P.d_units, rec, srec, P.rec_stride, flag, P.d_pos, st,
                           ride ? &b : nullptr, ev0, ev1))
             SWCHK(hipGetLastError());
         if (trace_path) {
-            std::vector<unsigned long long> h(4 * (size_t)P.n_units);
+            std::vector<unsigned long long> h(8 * (size_t)P.n_units);
             SWCHK(hipStreamSynchronize(st));
             SWCHK(hipMemcpy(h.data(), S3.trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
             SWCHK(hipFree(S3.trace));

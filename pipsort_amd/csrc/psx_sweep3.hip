@@ -183,7 +183,14 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
     const unsigned long long t_start = A.trace ? wall_clock64() : 0ull;
     const int4 un = units[unit];
     const int a0 = un.x, a1 = un.y, K = un.z & 0xffff, C = un.w & 0xffff;
-    const int j0 = un.z >> 16, j1 = un.w >> 16;  // b-walk steps of this (half) unit
+    // b-walk steps of this (half) unit.  A diagonal tile (K == C) is walked
+    // folded: at step j lane t pairs with slot (t + j) & 63 whichever of the two
+    // is larger, so steps 1..31 (+ step 32 on lanes < 32) visit every pair of
+    // the block once — half the steps of the triangular walk, no idle lanes.
+    // The set {a, slot, t} is factored in the order (a, slot, t) either way.
+    const bool diag = K == C;
+    const int j0 = diag ? 1 + (un.z >> 17) : un.z >> 16;
+    const int j1 = diag ? 1 + (un.w >> 17) : un.w >> 16;
     const int pad = A.pad, ldg = A.ldg;
     const int tile = C * (C + 1) / 2 + K;
     const double rho = A.rho;
@@ -235,6 +242,8 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
     const double* sk0 = A.skewT[0] + (size_t)tile * 4096 + t;
     const double* sk1 = A.skewT[1] + (size_t)tile * 4096 + t;
 
+    unsigned long long t_ph[4] = {0ull, 0ull, 0ull, 0ull};  // diagnostics: phases of the first a
+    if (A.trace) t_ph[0] = wall_clock64();
     for (int ai = 0; ai < a1 - a0; ai++) {
         const int va = a0 + ai, ua = va - pad;  // a0 >= pad: a is always a real SNP
         const unsigned pa = A.pres[ua];
@@ -300,11 +309,12 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
         LAcc accA;
         lacc_zero(accA);
         __syncthreads();  // (a, b) terms visible
+        if (A.trace && ai == 0) t_ph[1] = wall_clock64();
 
         for (int j = j0; j < j1; j++) {
             const int bs = (t + j) & 63;
             const int vb = 64 * K + bs;
-            const bool act = okc && vb > va && vb < vc;
+            const bool act = diag ? (vb > va && vc > va && (j < 32 || t < 32)) : (okc && vb > va && vb < vc);
             if (act) {
                 double E[2][8];
                 int nb[2];
@@ -442,9 +452,11 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
             // compiler must keep program order (no lgkmcnt drain per step)
             __builtin_amdgcn_wave_barrier();
         }
+        if (A.trace && ai == 0) t_ph[2] = wall_clock64();
         Acc5 ra = lacc_rec(accA, A.Ck, A.pit0);
         wave_fold_acc(ra);
         if (t == 0) put_rec(rec, pos, (size_t)unit * rec_stride + 128 + ai, ra);
+        if (A.trace && ai == 0) t_ph[3] = wall_clock64();
     }
     __syncthreads();
     put_rec(rec, pos, (size_t)unit * rec_stride + t, lacc_rec(accC, A.Ck, A.pit0));
@@ -473,10 +485,12 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
     if (A.trace && t == 0) {
         unsigned hw;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        A.trace[4 * (size_t)unit] = t_start;
-        A.trace[4 * (size_t)unit + 1] = wall_clock64();
-        A.trace[4 * (size_t)unit + 2] = hw;
-        A.trace[4 * (size_t)unit + 3] = (unsigned long long)unit;
+        unsigned long long* tr = A.trace + 8 * (size_t)unit;
+        tr[0] = t_start;
+        tr[1] = wall_clock64();
+        tr[2] = hw;
+        tr[3] = (unsigned long long)unit | ((unsigned long long)diag << 32) | ((unsigned long long)(a1 - a0) << 33);
+        for (int i = 0; i < 4; i++) tr[4 + i] = t_ph[i];
     }
 }
 

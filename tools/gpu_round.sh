@@ -9,6 +9,6 @@ rc=$?
 echo "pytest rc=$rc" >> $OUT/pytest_gpu.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit $?
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline > $OUT/prof.log 2>&1 || exit $?
 if [ -n "${PMC:-}" ]; then TAG=${TAG:-r01} bash tools/gpu_pmc.sh || exit $?; fi
 exit 0

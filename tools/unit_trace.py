@@ -26,7 +26,7 @@ pc = E.PostCal(bench.build_inputs(a.workload), device=0)
 pc.set_shard(a.rank, a.world)
 for _ in range(3):
     pc.run_exhaustive()
-tr = np.fromfile(path, dtype=np.uint64).reshape(-1, 4).astype(np.int64)
+tr = np.fromfile(path, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
 st, en = tr[:, 0], tr[:, 1]
 t0 = st.min()
 span = (en.max() - t0) / 100.0
@@ -43,6 +43,23 @@ print("concurrent units over time (20 bins):", conc)
 order = np.argsort(st)
 print("start time by unit index decile (us):",
       [round(float((st[order][int(q * (len(st) - 1))] - t0) / 100.0), 1) for q in np.linspace(0, 1, 11)])
-bu = np.array([d.mean() for d in np.array_split(dur[np.argsort(tr[:, 3])], 10)])
+uid = tr[:, 3] & 0xffffffff
+diag = (tr[:, 3] >> 32) & 1
+na = tr[:, 3] >> 33
+for dflag in (0, 1):
+    for k in sorted(set(na[diag == dflag].tolist())):
+        m = (diag == dflag) & (na == k)
+        print(f"{'diagonal' if dflag else 'off-diag'} units with {k} a: n={m.sum()} mean {dur[m].mean():.1f} us")
+ph = tr[:, 4:8]
+pro = (ph[:, 0] - st) / 100.0
+apro = (ph[:, 1] - ph[:, 0]) / 100.0
+steps = (ph[:, 2] - ph[:, 1]) / 100.0
+fold = (ph[:, 3] - ph[:, 2]) / 100.0
+for dflag in (0, 1):
+    m = diag == dflag
+    print(f"{'diagonal' if dflag else 'off-diag'} first-a phases (us, mean): unit prologue {pro[m].mean():.1f}, "
+          f"a prologue {apro[m].mean():.1f}, steps {steps[m].mean():.1f}, a fold+record {fold[m].mean():.1f}, "
+          f"rest {((en - ph[:, 3]) / 100.0)[m].mean():.1f}")
+bu = np.array([d.mean() for d in np.array_split(dur[np.argsort(uid)], 10)])
 print("mean duration by unit-index decile:", np.round(bu, 1).tolist())
 pc.close()
