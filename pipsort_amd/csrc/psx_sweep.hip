@@ -291,12 +291,12 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     auto cls = [&](int v) { return v >= pad ? (int)pres_host[v - pad] : 0; };
     double total_a = 0;
     for (int C = 0; C < nblk; C++)
-        for (int K = 0; K <= C; K++) total_a += std::max(0, 64 * K + 63 - pad);
+        for (int K = 0; K <= C; K++) total_a += (K < C) ? std::max(0, 64 * K - pad) : U;  // a-range per tile
     // a-chunk size: k_sweep3 holds 2 waves per SIMD (233 VGPRs), i.e. 8 unit
-    // slots per CU.  Units cost about the same whatever their masking, so the
-    // last dispatch round is the tail: aim for >= 8 rounds per shard and take
-    // the smallest chunk that gets there (measured on MI355X, syn1000c3:
-    // ca = 2 at world 1, ca = 1 for shards of world >= 2, profiles/).
+    // slots per CU.  Larger chunks amortise the per-unit prologue / records,
+    // smaller ones shorten the last dispatch round: aim for >= 6 rounds of the
+    // wave slots per shard (measured on MI355X, syn1000c3, tools/ca_sweep.sh:
+    // ca = 2..4 best at world 1, 2 at world 2, 1 at worlds 4 and 8).
     static const double kTarget = [] {  // units per shard the a-chunk is sized for
         if (const char* v = std::getenv("PSX_K3_UNITS")) return std::atof(v);
         int dev = 0, cus = 256;
@@ -305,22 +305,31 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
             if (hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0)
                 cus = pr.multiProcessorCount;
         }
-        return 8.0 * (8.0 * cus);
+        return 6.0 * (8.0 * cus);
     }();
     ca = (int)std::floor(total_a / (kTarget * world));
     if (const char* v = std::getenv("PSX_K3_CA")) ca = std::atoi(v);
     ca = std::max(1, std::min(64, ca));
+    // Every union triple x < y < z belongs to exactly one unit family, by which
+    // of its members share a 64-block:
+    //   all in different blocks      -> off-diagonal tile (K = blk y, C = blk z), a = x
+    //   x, y in one block, z later   -> diagonal tile (K = C = blk x), a = z (after the block)
+    //   y, z in one block, x earlier -> diagonal tile (K = C = blk y), a = x (before the block)
+    //   all three in one block       -> diagonal tile, a = x (in the block, below the pair)
+    // so off-diagonal tiles only see a < 64K (every lane active every step) and
+    // the triangular pair structure only occurs in diagonal tiles, which walk
+    // it folded (psx_sweep3.hip): no in-block masking waste.
     std::vector<PlanUnit> all;
     for (int C = 0; C < nblk; C++) {
         if (64 * C + 64 <= pad) continue;
         for (int K = 0; K <= C; K++) {
-            const int amax = 64 * K + 63;  // a < b <= 64K + 63
+            const int amax = (K < C) ? 64 * K : ldg;
             for (int a0 = pad; a0 < amax; a0 += ca) {
                 const int a1 = std::min(a0 + ca, amax);
-                // a diagonal tile (K == C) runs its folded walk: half the steps
-                // plus the same per-unit / per-a work (measured 0.55 of an
-                // off-diagonal unit, tools/unit_trace.py)
-                all.push_back({a0, a1, K, C, (double)(a1 - a0) * (K == C ? 0.55 : 1.0)});
+                // a diagonal tile runs its folded walk: half the steps plus the
+                // same per-unit / per-a work (0.68 of an off-diagonal unit, fitted to the
+                // per-shard times of the 8-way rehearsal, profiles/)
+                all.push_back({a0, a1, K, C, (double)(a1 - a0) * (K == C ? 0.68 : 1.0)});
             }
         }
     }
@@ -346,35 +355,32 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
         pref[x].assign(ldg + 1, 0);
         for (int v = 0; v < ldg; v++) pref[x][v + 1] = pref[x][v] + (cls(v) == x);
     }
+    auto cnt = [&](int x, int v0, int v1) { return (double)(pref[x][v1] - pref[x][v0]); };
     sets = 0; bytes = 0; configs = 0;
+    auto add = [&](double n, int x, int y, int z) {
+        if (n == 0) return;
+        sets += n;
+        bytes += n * bytes_cls[x][y][z];
+        configs += n * wcls[x] * wcls[y] * wcls[z];
+    };
     for (auto& u : mine) {
-        // T[x][y]: number of (a, b) pairs, a of class x in [a0, min(a1, b)), b of class y,
-        // accumulated over b in block K in increasing order; c must exceed b
-        double Tcum[4][4] = {{0}};
-        std::vector<std::array<double, 16>> upto(65);  // upto[i]: T over the first i b's of the block
-        for (int i = 0; i <= 64; i++) {
-            for (int x = 0; x < 4; x++)
-                for (int y = 0; y < 4; y++) upto[i][4 * x + y] = Tcum[x][y];
-            if (i == 64) break;
-            const int b = 64 * u.B + i, y = cls(b);
-            if (y == 0) continue;
-            const int ahi = std::min(u.a1, b);
-            if (ahi <= u.a0) continue;
-            for (int x = 1; x < 4; x++) Tcum[x][y] += pref[x][ahi] - pref[x][u.a0];
+        const int b0 = 64 * u.B, c0 = 64 * u.T;
+        if (u.B < u.T) {  // a < block K < block C: every (a, b, c) of the tile
+            for (int x = 1; x < 4; x++) {
+                const double na = cnt(x, u.a0, u.a1);
+                if (na == 0) continue;
+                for (int y = 1; y < 4; y++)
+                    for (int z = 1; z < 4; z++) add(na * cnt(y, b0, b0 + 64) * cnt(z, c0, c0 + 64), x, y, z);
+            }
+            continue;
         }
-        for (int t = 0; t < 64; t++) {
-            const int c = 64 * u.T + t, z = cls(c);
-            if (z == 0) continue;
-            // b < c: all of block K when K < C, else the first t b's
-            const auto& T = upto[u.B < u.T ? 64 : t];
-            for (int x = 1; x < 4; x++)
-                for (int y = 1; y < 4; y++) {
-                    const double n = T[4 * x + y];
-                    if (n == 0) continue;
-                    sets += n;
-                    bytes += n * bytes_cls[x][y][z];
-                    configs += n * wcls[x] * wcls[y] * wcls[z];
-                }
+        for (int a = u.a0; a < u.a1; a++) {  // diagonal tile: pairs of the block (above a if a is in it)
+            const int x = cls(a);
+            if (x == 0) continue;
+            const int lo_v = (a >= b0 && a < b0 + 64) ? a + 1 : b0;
+            double n[4] = {0, cnt(1, lo_v, b0 + 64), cnt(2, lo_v, b0 + 64), cnt(3, lo_v, b0 + 64)};
+            for (int y = 1; y < 4; y++)
+                for (int z = y; z < 4; z++) add(y == z ? n[y] * (n[y] - 1) / 2 : n[y] * n[z], x, y, z);
         }
     }
     // optional (PSX_K3_SPLIT): the last dispatch round runs half units (b-walk
@@ -382,7 +388,7 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // on MI355X (world-8 shard 0.350 vs 0.352 ms: the tail is ~9 % of the
     // launch either way, tools/unit_trace.py), so off by default.  Totals above
     // are unchanged.
-    const size_t slots = (size_t)(kTarget / 8.0);
+    const size_t slots = (size_t)(kTarget / 6.0);
     if (std::getenv("PSX_K3_SPLIT") && mine.size() > 2 * slots) {
         std::vector<PlanUnit> out(mine.begin(), mine.end() - slots);
         for (size_t i = mine.size() - slots; i < mine.size(); i++) {

@@ -314,7 +314,11 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
         for (int j = j0; j < j1; j++) {
             const int bs = (t + j) & 63;
             const int vb = 64 * K + bs;
-            const bool act = diag ? (vb > va && vc > va && (j < 32 || t < 32)) : (okc && vb > va && vb < vc);
+            // diagonal tile: the pair {slot, t} of the block with a below both,
+            // or any real pair when a lies after the block
+            const bool act = diag ? (((vb > va && vc > va) || (va >= 64 * K + 64 && vb >= pad && vc >= pad)) &&
+                                     (j < 32 || t < 32))
+                                  : (okc && vb > va && vb < vc);
             if (act) {
                 double E[2][8];
                 int nb[2];

@@ -14,7 +14,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libpipsort_engine.so")
+# PSX_ENGINE_LIB: an alternative build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("PSX_ENGINE_LIB") or os.path.join(_HERE, "lib", "libpipsort_engine.so")
 PIPSORT_BIN = os.path.join(_HERE, "bin", "PIPSORT")
 
 PSX_OK = 0
