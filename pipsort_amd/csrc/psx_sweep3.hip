@@ -311,7 +311,14 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
         __syncthreads();  // (a, b) terms visible
         if (A.trace && ai == 0) t_ph[1] = wall_clock64();
 
+        // the skewed Sigma~ row of the next step is loaded one step ahead
+        double gnx0 = sk0[j0 * 64], gnx1 = sk1[j0 * 64];
         for (int j = j0; j < j1; j++) {
+            const double gcur0 = gnx0, gcur1 = gnx1;
+            if (j + 1 < j1) {
+                gnx0 = sk0[(j + 1) * 64];
+                gnx1 = sk1[(j + 1) * 64];
+            }
             const int bs = (t + j) & 63;
             const int vb = 64 * K + bs;
             // diagonal tile: the pair {slot, t} of the block with a below both,
@@ -324,7 +331,7 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
                 int nb[2];
 #pragma unroll
                 for (int s = 0; s < 2; s++) {
-                    const double Gbc = (s ? sk1 : sk0)[j * 64];
+                    const double Gbc = s ? gcur1 : gcur0;
                     // {b, c}
                     const double l2 = Gbc * bI[s][bs];
                     const double D2 = fma(-l2, Gbc, Acc[s]);
