@@ -147,13 +147,13 @@ union SweepSmem {  // a block runs either a k = 3 unit or a level-2 unit
 template <bool ALLPRES>
 __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __restrict__ units,
                                                   Acc5* __restrict__ rec, SetRec* __restrict__ srec, int rec_stride,
-                                                  int* __restrict__ flag, const int* __restrict__ pos, int n2,
+                                                  int* __restrict__ flag, const int* __restrict__ pos, int nk3,
                                                   TileArgs A2, const int4* __restrict__ units2,
                                                   Acc5* __restrict__ rec2, SetRec* __restrict__ srec2,
                                                   const int* __restrict__ pos2) {
     __shared__ SweepSmem sm;
-    if ((int)blockIdx.x < n2) {  // level-2 units ride in the same launch (dispatched first)
-        sweep_unit<2, false>(A2, blockIdx.x, units2, rec2, srec2, 128, flag, pos2, sm.u2);
+    if ((int)blockIdx.x >= nk3) {  // level-2 units ride in the same launch, after the k = 3 units
+        sweep_unit<2, false>(A2, blockIdx.x - nk3, units2, rec2, srec2, 128, flag, pos2, sm.u2);
         return;
     }
     double (&tab)[256] = sm.s3.tab;
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
     double (&sNs)[64] = sm.s3.sNs;
     int (&sM)[64] = sm.s3.sM;
 
-    const int unit = blockIdx.x - n2;
+    const int unit = blockIdx.x;  // grid position = unit index: XCD = unit % 8 (plan_units3c)
     const int t = threadIdx.x;
     const unsigned long long t_start = A.trace ? wall_clock64() : 0ull;
     const int4 un = units[unit];
@@ -534,10 +534,10 @@ int launch_sweep3(bool allpres, const Sweep3Args& A, int n_units, const int4* un
     // itself (no marker packets between back-to-back passes)
     if (allpres)
         hipExtLaunchKernelGGL((k_sweep3<true>), grid, dim3(64), 0, st, ev0, ev1, 0, A, units, rec, srec, rec_stride,
-                              flag, pos, b.n, b.A, b.units, b.rec, b.srec, b.pos);
+                              flag, pos, n_units, b.A, b.units, b.rec, b.srec, b.pos);
     else
         hipExtLaunchKernelGGL((k_sweep3<false>), grid, dim3(64), 0, st, ev0, ev1, 0, A, units, rec, srec, rec_stride,
-                              flag, pos, b.n, b.A, b.units, b.rec, b.srec, b.pos);
+                              flag, pos, n_units, b.A, b.units, b.rec, b.srec, b.pos);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
