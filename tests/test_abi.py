@@ -80,6 +80,23 @@ def test_shards_partition_every_level(world):
         assert abs(tot_cfg - e[k]) < 0.5
 
 
+@pytest.mark.parametrize("U", [3, 63, 64, 65, 129, 1000])
+@pytest.mark.parametrize("world", [1, 8])
+def test_k3_block_pattern_plan_counts(U, world):
+    """The k = 3 plan (off-diagonal tiles + folded diagonal tiles with a before,
+    after or inside the block) covers C(U, 3) sets and sum 27 configurations
+    per set for a fully shared locus, at block-boundary sizes."""
+    u2l = np.stack([np.arange(U), np.arange(U)]).astype(np.int32)
+    seam = _count_seam(u2l, 3)
+    sets, cfg = 0, 0.0
+    for r in range(world):
+        s, c = seam.shard_stats(3, r, world)
+        sets += s
+        cfg += c
+    assert sets == math.comb(U, 3)
+    assert abs(cfg - 27 * math.comb(U, 3)) < 0.5
+
+
 def test_partial_fold_is_associative_and_order_fixed():
     rng = np.random.default_rng(0)
     ldg = 128

@@ -314,3 +314,39 @@ def test_cli_configs_file_matches_oracle_cli(gpu, tmp_path):
     _cli_pair(tmp_path, "test_optional_configs",
               ["-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "eur_afr_small_test_snp_map", "-n", "7000,7000",
                "-b", "all_configs_int16", "-d", "72", "-e", "5", "-o", "out"])
+
+
+def test_max_size_m2000_c3_properties(gpu):
+    """M = 2000, c = 3 (35,917,996,001 configurations; U = 2000 is the largest
+    locus of BASELINE configs), built through the GPU Model setup: exact
+    configuration count, PIP ranges, sharded exchange = single pass.  (Values
+    are pinned against the oracle at sizes it finishes in seconds, above.)"""
+    import torch
+    M = 2000
+    ld, z, _, _, u2l = synth.syn_v1(M)
+    mi = E.model_inputs(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    pc = E.PostCal(mi)
+    pc.run_exhaustive()
+    a = pc.accum()
+    assert a.n_configs == mi.count_configs() == 1 + 3 * M + 9 * (M * (M - 1) // 2) + 27 * (M * (M - 1) * (M - 2) // 6)
+    post, noc, sh = a.pips()
+    assert np.all(post >= 0) and np.all(post <= 1 + 1e-12) and np.all(sh <= 1 + 1e-12)
+    gpip = post[:M] + post[M:] - sh
+    assert np.all(gpip <= 1 + 1e-6) and np.all(gpip >= -1e-6)
+    assert post[M // 4] > 0.5 and post[M + M // 4] > 0.5
+    # two shards merged == the single pass (to rounding of the fold order)
+    nb = pc.partials_bytes()
+    buf = torch.empty(2 * nb, dtype=torch.uint8, device="cuda")
+    for r in range(2):
+        x = E.PostCal(mi)
+        x.set_shard(r, 2)
+        x.run_exhaustive()
+        x.export_partials(buf.data_ptr() + r * nb)
+        x.close()
+    torch.cuda.synchronize()
+    m = E.PostCal(mi)
+    m.merge_partials(buf.data_ptr(), 2)
+    g = m.accum()
+    assert g.n_configs == a.n_configs
+    d = np.abs(_sexp(g.post, g.total) - _sexp(a.post, a.total)).max()
+    assert d <= 1e-12
