@@ -66,6 +66,8 @@ struct Sweep3Args {
     const double* Ad[2];       // diag(A_s) = 1/d_s + diag(Sigma~_s), by u
     const double* ys[2];       // y_s * sqrt(log2(e) / 2), by u
     const double* skewT[2];    // skewed Sigma~ tiles in v space, tile(K, C), K <= C
+    const double* bcmu[2];     // {b, c} subset weights mu per [tile][step][lane] (a-independent)
+    const int2* bcn;           // their base-2 exponents, both studies
     const double* muS[2];      // singleton weights {c}, by u
     const int* nS[2];
     const unsigned char* pres; // bit s: SNP present in study s, by u
@@ -81,11 +83,16 @@ int launch_sweep3(bool allpres, const Sweep3Args& A, int n_units, const int4* un
                   hipEvent_t ev1 = nullptr);
 int launch_scale_y(const double* y, int n, double* ys, hipStream_t st);
 int launch_build_skewT(const double* G, int ldg, int pad, double* skew, hipStream_t st);
+// {b, c} subset weights of every skewT entry (the a-independent half of a k = 3
+// step), computed once per locus with the sweep kernel's own arithmetic
+int launch_build_bc3(const Sweep3Args& A, int ntile, double* mu0, double* mu1, int2* n, hipStream_t st);
 
 struct SweepPlanCache {
     std::map<std::tuple<int, int, int, int, int>, SweepPlan> plans;  // (k, U, rank, world, variant)
     double* d_skew[2] = {nullptr, nullptr};  // skewed Sigma~ tiles (B <= T), k = 2 and exact k = 3
     double* d_skewT[2] = {nullptr, nullptr}; // lane-owns-c tiles in v space (k = 3 fast kernel)
+    double* d_bcmu[2] = {nullptr, nullptr};  // {b, c} weights per skewT entry (k = 3 fast kernel)
+    int2* d_bcn = nullptr;
     double* d_muS[2] = {nullptr, nullptr};   // singleton subset weights
     int* d_nS[2] = {nullptr, nullptr};
     double* d_ys[2] = {nullptr, nullptr};    // scaled y (k = 3 fast kernel)

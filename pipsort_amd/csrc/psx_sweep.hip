@@ -327,9 +327,9 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
             for (int a0 = pad; a0 < amax; a0 += ca) {
                 const int a1 = std::min(a0 + ca, amax);
                 // a diagonal tile runs its folded walk: half the steps plus the
-                // same per-unit / per-a work (0.68 of an off-diagonal unit, fitted to the
+                // same per-unit / per-a work (0.71 of an off-diagonal unit, fitted to the
                 // per-shard times of the 8-way rehearsal, profiles/)
-                all.push_back({a0, a1, K, C, (double)(a1 - a0) * (K == C ? 0.68 : 1.0)});
+                all.push_back({a0, a1, K, C, (double)(a1 - a0) * (K == C ? 0.71 : 1.0)});
             }
         }
     }
@@ -496,16 +496,39 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     return 0;
 }
 
+static TileArgs tile_args(const SweepPlanCache& C, const SweepArgs& a, int k, int U, int ldg);
+
+// arguments of the k = 3 fast kernel (and of its {b, c} precompute)
+static Sweep3Args sweep3_args(const SweepPlanCache& C, const SweepArgs& a, int U, int ldg) {
+    const TileArgs A = tile_args(C, a, 3, U, ldg);
+    Sweep3Args S3;
+    for (int s = 0; s < 2; s++) {
+        S3.G[s] = A.G[s]; S3.Ad[s] = A.Ad[s]; S3.ys[s] = C.d_ys[s]; S3.skewT[s] = C.d_skewT[s];
+        S3.bcmu[s] = C.d_bcmu[s];
+        S3.muS[s] = A.muS[s]; S3.nS[s] = A.nS[s]; S3.rsd[s] = A.rsd[s];
+    }
+    S3.bcn = C.d_bcn;
+    S3.pad = ldg - U;
+    S3.pres = A.pres;
+    S3.tab = C.d_tab;
+    S3.pit0 = A.pit[0];
+    S3.rho = A.pit[0] > 0 ? A.pit[1] / A.pit[0] : 0.0;
+    S3.U = U; S3.ldg = ldg; S3.Ck = A.Ck;
+    return S3;
+}
+
 static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hipStream_t st) {
     if (C.d_skew[0] && C.skew_ldg == ldg && C.skew_src[0] == a.G0 && C.skew_src[1] == a.G1) return 0;
     for (int s = 0; s < 2; s++) {
         hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
         hipFree(C.d_skewT[s]); C.d_skewT[s] = nullptr;
+        hipFree(C.d_bcmu[s]); C.d_bcmu[s] = nullptr;
         hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
         hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
         hipFree(C.d_ys[s]); C.d_ys[s] = nullptr;
     }
     hipFree(C.d_tab); C.d_tab = nullptr;
+    hipFree(C.d_bcn); C.d_bcn = nullptr;
     {
         // 2^(i/256) correctly rounded (long double on the host)
         double tab[256];
@@ -535,6 +558,12 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
         SWCHK(hipMalloc(&C.d_skew[s], sizeof(double) * (size_t)ntile * 4096));
         hipLaunchKernelGGL(k_build_skew, dim3(ntile, 64), dim3(64), 0, st, s ? a.G1 : a.G0, ldg, nblk, C.d_skew[s]);
         SWCHK(hipGetLastError());
+    }
+    {  // the a-independent {b, c} weights of every k = 3 step
+        Sweep3Args S3 = sweep3_args(C, a, U, ldg);
+        for (int s = 0; s < 2; s++) SWCHK(hipMalloc(&C.d_bcmu[s], sizeof(double) * (size_t)ntile * 4096));
+        SWCHK(hipMalloc(&C.d_bcn, sizeof(int2) * (size_t)ntile * 4096));
+        if (launch_build_bc3(S3, ntile, C.d_bcmu[0], C.d_bcmu[1], C.d_bcn, st)) SWCHK(hipGetLastError());
     }
     C.skew_ldg = ldg;
     C.skew_src[0] = a.G0;
@@ -655,17 +684,7 @@ int sweep_kernel(SweepPlanCache& C, SweepPlan& P, hipStream_t st, const SweepArg
     if (timed) SWCHK(hipEventRecord(P.ev[0], st));
     const dim3 g(P.n_units), blk(64);
     if (k == 3 && !exact) {
-        Sweep3Args S3;
-        for (int s = 0; s < 2; s++) {
-            S3.G[s] = A.G[s]; S3.Ad[s] = A.Ad[s]; S3.ys[s] = C.d_ys[s]; S3.skewT[s] = C.d_skewT[s];
-            S3.muS[s] = A.muS[s]; S3.nS[s] = A.nS[s]; S3.rsd[s] = A.rsd[s];
-        }
-        S3.pad = ldg - U;
-        S3.pres = A.pres;
-        S3.tab = C.d_tab;
-        S3.pit0 = A.pit[0];
-        S3.rho = A.pit[0] > 0 ? A.pit[1] / A.pit[0] : 0.0;
-        S3.U = U; S3.ldg = ldg; S3.Ck = A.Ck;
+        Sweep3Args S3 = sweep3_args(C, a, U, ldg);
         Level2Blocks b{0, TileArgs{}, nullptr, nullptr, nullptr, nullptr};
         if (ride) {  // level 2 in the same launch: its units are the first blocks of the grid
             Acc5* rec2 = plan_records(*l2, parity);
@@ -742,11 +761,13 @@ void sweep_free(SweepPlanCache& C) {
     for (int s = 0; s < 2; s++) {
         hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
         hipFree(C.d_skewT[s]); C.d_skewT[s] = nullptr;
+        hipFree(C.d_bcmu[s]); C.d_bcmu[s] = nullptr;
         hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
         hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
         hipFree(C.d_ys[s]); C.d_ys[s] = nullptr;
     }
     hipFree(C.d_tab); C.d_tab = nullptr;
+    hipFree(C.d_bcn); C.d_bcn = nullptr;
     if (C.own_flag) hipFree(C.d_flag);
     C.d_flag = nullptr;
 }

@@ -118,6 +118,69 @@ __device__ __forceinline__ Acc5 lacc_rec(const LAcc& a, int Ck, double pit0) {
     return r;
 }
 
+// b-block terms of SNP v (v space) in study s: 1/A_bb, y_b / 2, the {b}
+// quadratic form and its pivot factor (x the c step's rsd / 2)
+struct BTerms {
+    double I, Yh, H, R, chi;
+};
+template <bool ALLPRES>
+__device__ __forceinline__ BTerms b_terms(const Sweep3Args& A, int s, int v) {
+    const int u = v - A.pad;
+    const bool ok = v >= A.pad;
+    const unsigned p = ok ? A.pres[u] : 0u;
+    BTerms b;
+    b.chi = (ok && (ALLPRES || ((p >> s) & 1u))) ? 1.0 : 0.0;
+    const double Abb = ok ? A.Ad[s][u] : 1.0;
+    const double yb = ok ? A.ys[s][u] : 0.0;
+    const double r = rsqrt_nr(Abb);
+    b.I = r * r;
+    b.Yh = 0.5 * yb;
+    b.H = yb * yb * r * r;
+    b.R = r * A.rsd[s] * b.chi * (0.5 * A.rsd[s]);  // {b} factor x (c's rsd / 2)
+    return b;
+}
+
+// the {b, c} subset weight 2^n2 * mu2 (LDL^T of {b, c}, c extending b)
+__device__ __forceinline__ void bc_weight(double Gbc, const BTerms& b, double Acc, double ych, double chic,
+                                          const double* tab, int& n2, double& mu2) {
+    const double l2 = Gbc * b.I;
+    const double D2 = fma(-l2, Gbc, Acc);
+    const double w2 = fma(-l2, b.Yh, ych);
+    const double r2 = rsq2x(D2);
+    const double t2 = w2 * r2;
+    const double h2 = fma(t2, t2, b.H);
+    split3(h2, b.R * r2 * chic, tab, n2, mu2);
+}
+
+// bcmu[s][tile][j][t], bcn[tile][j][t]: the {b, c} weights of the k = 3 walk,
+// b = 64K + ((t + j) & 63), c = 64C + t (the folded diagonal walk uses the same
+// (slot, lane) pairs).  One block per (tile, step), lane t.
+template <bool ALLPRES>
+__global__ void k_build_bc3(Sweep3Args A, double* __restrict__ mu0, double* __restrict__ mu1,
+                            int2* __restrict__ nn) {
+    const int tile = blockIdx.x, j = blockIdx.y, t = threadIdx.x;
+    int C = 0;
+    while ((C + 1) * (C + 2) / 2 <= tile) C++;
+    const int K = tile - C * (C + 1) / 2;
+    const int vb = 64 * K + ((t + j) & 63), vc = 64 * C + t, uc = vc - A.pad;
+    const bool okc = vc >= A.pad;
+    const unsigned pcm = okc ? A.pres[uc] : 0u;
+    const size_t o = (size_t)tile * 4096 + j * 64 + t;
+    int n[2];
+    double mu[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        const BTerms b = b_terms<ALLPRES>(A, s, vb);
+        const double chic = (okc && (ALLPRES || ((pcm >> s) & 1u))) ? 1.0 : 0.0;
+        const double Acc = okc ? A.Ad[s][uc] : 1.0;
+        const double ych = 0.5 * (okc ? A.ys[s][uc] : 0.0);
+        bc_weight(A.skewT[s][o], b, Acc, ych, chic, A.tab, n[s], mu[s]);
+    }
+    mu0[o] = mu[0];
+    mu1[o] = mu[1];
+    nn[o] = make_int2(n[0], n[1]);
+}
+
 // Unit = (a-chunk [a0, a1), b-block K, c-chunk C), K <= C, in the padded index
 // space v = u + pad (the partial 64-block is the lowest one, where the sweep
 // has the least work).  Lane t owns c = 64C + t for the whole unit; at step j
@@ -132,7 +195,7 @@ __device__ __forceinline__ Acc5 lacc_rec(const LAcc& a, int Ck, double pit0) {
 // indexed [study][b slot], the exp2 table and the rotating b-slot accumulators
 struct Sweep3Smem {
     double tab[256];
-    double bI[2][64], bYh[2][64], bH[2][64], bR[2][64];
+    double bH[2][64], bR[2][64];
     double abG[2][64], abD[2][64], abI[2][64], abW[2][64], abH[2][64], abR[2][64], abMu[2][64], abMuB[2][64];
     int abN[2][64];
     double bW[64];
@@ -157,8 +220,6 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
         return;
     }
     double (&tab)[256] = sm.s3.tab;
-    double (&bI)[2][64] = sm.s3.bI;
-    double (&bYh)[2][64] = sm.s3.bYh;
     double (&bH)[2][64] = sm.s3.bH;
     double (&bR)[2][64] = sm.s3.bR;
     double (&abG)[2][64] = sm.s3.abG;
@@ -201,17 +262,11 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
     const int vbl = 64 * K + t, ubl = vbl - pad;
     const bool okb = vbl >= pad;
     const unsigned pbl = okb ? A.pres[ubl] : 0u;
-    double chib[2];
 #pragma unroll
     for (int s = 0; s < 2; s++) {
-        chib[s] = (okb && (ALLPRES || ((pbl >> s) & 1u))) ? 1.0 : 0.0;
-        const double Abb = okb ? A.Ad[s][ubl] : 1.0;
-        const double yb = okb ? A.ys[s][ubl] : 0.0;
-        const double r = rsqrt_nr(Abb);
-        bI[s][t] = r * r;
-        bYh[s][t] = 0.5 * yb;
-        bH[s][t] = yb * yb * r * r;
-        bR[s][t] = r * A.rsd[s] * chib[s] * (0.5 * A.rsd[s]);  // {b} factor x (c's rsd / 2)
+        const BTerms b = b_terms<ALLPRES>(A, s, vbl);
+        bH[s][t] = b.H;
+        bR[s][t] = b.R;
     }
     bW[t] = memb_weight(pbl);
     sM[t] = EMPTY;
@@ -241,6 +296,9 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
     double nc0 = 0.0, nc1 = 0.0, npat = 0.0;
     const double* sk0 = A.skewT[0] + (size_t)tile * 4096 + t;
     const double* sk1 = A.skewT[1] + (size_t)tile * 4096 + t;
+    const double* bm0 = A.bcmu[0] + (size_t)tile * 4096 + t;
+    const double* bm1 = A.bcmu[1] + (size_t)tile * 4096 + t;
+    const int2* bnn = A.bcn + (size_t)tile * 4096 + t;
 
     unsigned long long t_ph[4] = {0ull, 0ull, 0ull, 0ull};  // diagnostics: phases of the first a
     if (A.trace) t_ph[0] = wall_clock64();
@@ -271,7 +329,9 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
                 const double rab = rsqrt_nr(Dab);
                 const double wab = fma(-l, ya, yb);
                 const double hab = fma(wab * wab, rab * rab, ha);
-                const double rPab = rPa * rab * A.rsd[s] * chib[s];
+                // this lane's b absent from study s (or padding): the {a, b} weight is 0
+                const bool chib = okb && (ALLPRES || ((pbl >> s) & 1u));
+                const double rPab = chib ? rPa * rab * A.rsd[s] : 0.0;
                 int nAB, nB;
                 double muAB, muB;
                 split3(hab, rPab, tab, nAB, muAB);
@@ -311,13 +371,19 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
         __syncthreads();  // (a, b) terms visible
         if (A.trace && ai == 0) t_ph[1] = wall_clock64();
 
-        // the skewed Sigma~ row of the next step is loaded one step ahead
-        double gnx0 = sk0[j0 * 64], gnx1 = sk1[j0 * 64];
+        // the next step's skewed Sigma~ entries and {b, c} weights are loaded one
+        // step ahead (L2 / MALL latency is longer than the VALU work between)
+        double gnx0 = sk0[j0 * 64], gnx1 = sk1[j0 * 64], mnx0 = bm0[j0 * 64], mnx1 = bm1[j0 * 64];
+        int2 nnx = bnn[j0 * 64];
         for (int j = j0; j < j1; j++) {
-            const double gcur0 = gnx0, gcur1 = gnx1;
+            const double gcur0 = gnx0, gcur1 = gnx1, mcur0 = mnx0, mcur1 = mnx1;
+            const int2 ncur = nnx;
             if (j + 1 < j1) {
                 gnx0 = sk0[(j + 1) * 64];
                 gnx1 = sk1[(j + 1) * 64];
+                mnx0 = bm0[(j + 1) * 64];
+                mnx1 = bm1[(j + 1) * 64];
+                nnx = bnn[(j + 1) * 64];
             }
             const int bs = (t + j) & 63;
             const int vb = 64 * K + bs;
@@ -332,13 +398,9 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
 #pragma unroll
                 for (int s = 0; s < 2; s++) {
                     const double Gbc = s ? gcur1 : gcur0;
-                    // {b, c}
-                    const double l2 = Gbc * bI[s][bs];
-                    const double D2 = fma(-l2, Gbc, Acc[s]);
-                    const double w2 = fma(-l2, bYh[s][bs], ych[s]);
-                    const double r2 = rsq2x(D2);
-                    const double t2 = w2 * r2;
-                    const double h2 = fma(t2, t2, bH[s][bs]);
+                    // {b, c}: precomputed (k_build_bc3, a-independent)
+                    const int n2 = s ? ncur.y : ncur.x;
+                    const double mu2 = s ? mcur1 : mcur0;
                     // {a, b, c}: extend the (a, b) factor by the c row
                     const double lcb = fma(-l1[s], abG[s][bs], Gbc) * abI[s][bs];
                     const double u3 = lcb * abD[s][bs];
@@ -347,14 +409,10 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
                     const double r3 = rsq2x(D3);
                     const double t3 = w3 * r3;
                     const double h3 = fma(t3, t3, abH[s][bs]);
-                    double rP2 = bR[s][bs] * r2, rP3 = abR[s][bs] * r3;
-                    if (!ALLPRES) {
-                        rP2 *= chic[s];
-                        rP3 *= chic[s];
-                    }
-                    int n2, n3;
-                    double mu2, mu3;
-                    split3(h2, rP2, tab, n2, mu2);
+                    double rP3 = abR[s][bs] * r3;
+                    if (!ALLPRES && !((pcm >> s) & 1u)) rP3 = 0.0;  // c absent from study s
+                    int n3;
+                    double mu3;
                     split3(h3, rP3, tab, n3, mu3);
                     nb[s] = n3;
                     // subset weights relative to 2^n_abc (bit 0 = a, bit 1 = b, bit 2 = c)
@@ -521,6 +579,12 @@ __global__ void k_build_skewT(const double* __restrict__ G, int ldg, int pad, do
 int launch_build_skewT(const double* G, int ldg, int pad, double* skew, hipStream_t st) {
     const int nblk = ldg / 64;
     hipLaunchKernelGGL(k_build_skewT, dim3(nblk * (nblk + 1) / 2, 64), dim3(64), 0, st, G, ldg, pad, skew);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_build_bc3(const Sweep3Args& A, int ntile, double* mu0, double* mu1, int2* n, hipStream_t st) {
+    // a non-ALLPRES build is exact for every locus (chi factors of present SNPs are 1)
+    hipLaunchKernelGGL((k_build_bc3<false>), dim3(ntile, 64), dim3(64), 0, st, A, mu0, mu1, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
