@@ -308,8 +308,13 @@ def main():
                     "kernel_ms": avg_kernel_s * 1e3,
                     "alg_bytes_per_launch": alg_bytes}
         fp64 = {"achieved": tm["flops"] / avg_kernel_s / 1e12 if avg_kernel_s > 0 else 0.0,
-                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s"}
+                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "note": "FP64 flops per set calibrated from PMC instruction counts (FMA = 2); the kernel is "
+                        "VALU-issue bound, not FMA bound: see valu_busy"}
         fp64["frac"] = fp64["achieved"] / FP64_PEAK_TFLOPS
+        if pmc and "valu_busy" in pmc:
+            fp64["valu_busy"] = pmc["valu_busy"]
+            fp64["valu_busy_source"] = "profiles/pmc_latest.json (rocprofv3 --pmc, same workload)"
         out = {
             "metric": "causal configurations evaluated/sec (whole node)",
             "value": value,

@@ -428,9 +428,11 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     P.n_units = (int)mine.size();
     P.union_sets = (uint64_t)sets;
     P.alg_bytes = bytes;
-    // FP64 operation estimate per union set (prefix, c-row
-    // extension, split-exps, 3^k assignment folds and record folds)
-    P.flops = sets * (k == 3 ? 900.0 : 260.0);
+    // FP64 operations per union set (FMA = 2), calibrated from the PMC FP64
+    // instruction counts of the k = 3 fast kernel (profiles/pmc_latest.json:
+    // 64 x (2 FMA + MUL + ADD + TRANS) / sets = 281); k = 2 by the same ratio of
+    // VALU work per set
+    P.flops = sets * (k == 3 ? 281.0 : 110.0);
     const int pad = variant ? ldg - U : 0;  // record keys of variant 1 are in v space
     // device buffers
     std::vector<int4> hu(P.n_units);
