@@ -227,7 +227,7 @@ def main():
     pc.set_shard(rank, world)
     # one stream for torch (collectives, copies) and the engine: the exchange is
     # ordered by the stream, no host synchronisation between export and merge
-    stream = torch.cuda.Stream()
+    stream = torch.cuda.Stream(priority=-1)  # high: merges + exchange ahead of the sweeps
     torch.cuda.set_stream(stream)
     pc.set_stream(stream.cuda_stream)
     nbytes = pc.partials_bytes()

@@ -383,6 +383,12 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
                 for (int z = y; z < 4; z++) add(y == z ? n[y] * (n[y] - 1) / 2 : n[y] * n[z], x, y, z);
         }
     }
+    // Longest units first (LPT): the off-diagonal units, then the folded
+    // diagonal ones (0.71), so the launch's last dispatch round is made of the
+    // shorter units (the in-launch level-2 units follow them).  The unit
+    // timeline (tools/unit_trace.py) showed a ~60 us tail of full-length units
+    // on a world-8 shard in tile order.  Stable: tile order kept within a class.
+    std::stable_sort(mine.begin(), mine.end(), [](const PlanUnit& x, const PlanUnit& y) { return x.work > y.work; });
     // (An XCD-aware order — whole tiles binned per XCD so each 4 MB L2 serves
     // ~1/8 of the skewed tiles — measured 4 % slower than this natural order
     // once the next step's tile row is prefetched; not used.)

@@ -24,7 +24,7 @@ a = ap.parse_args()
 torch.cuda.set_device(0)
 seam = bench.build_inputs(a.workload)
 pc = E.PostCal(seam, device=0)
-stream = torch.cuda.Stream()
+stream = torch.cuda.Stream(priority=-1)
 torch.cuda.set_stream(stream)
 pc.set_stream(stream.cuda_stream)
 pc.set_shard(a.rank, a.world)

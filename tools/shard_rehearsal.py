@@ -32,7 +32,7 @@ def main():
     torch.cuda.set_device(0)
     seam = bench.build_inputs(args.workload)
     pc = E.PostCal(seam, device=0)
-    stream = torch.cuda.Stream()
+    stream = torch.cuda.Stream(priority=-1)  # high: merges + exchange ahead of the sweeps
     torch.cuda.set_stream(stream)
     pc.set_stream(stream.cuda_stream)
     nb = pc.partials_bytes()
