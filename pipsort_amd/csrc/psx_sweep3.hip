@@ -1,16 +1,23 @@
 // psx_sweep3.hip — the k = 3 exhaustive level (postcal.cpp:716-1092 for
 // |union set| = 3), the dominant kernel of the sweep.
 //
-// Same tiling as k_sweep (psx_sweep.hip): a unit is (a-chunk, B, T), lane t
-// owns b = 64B + t and walks c = 64T + ((t + j) & 63) diagonally, so the 64
-// per-c accumulators rotate through LDS without atomics.  This kernel is
-// VALU-issue bound (every wave64 VALU op costs ~4 cycles, FP64 or integer
-// alike; HBM traffic is negligible), so it is built to minimise the VALU
-// instruction count per union set:
+// A unit is (a-chunk, b-block K, c-block C), K <= C, in the padded index space:
+// lane t owns c = 64C + t and at step j takes b-slot (t + j) & 63 of block K,
+// so the 64 b-slot accumulators rotate through LDS without atomics.  Triples
+// are routed by block pattern (plan_units3c): off-diagonal tiles (K < C) only
+// see a before block K, so every lane is active every step; triples with two
+// members in one block go to that block's diagonal tile (K == C), walked
+// folded (steps 1..32, each pair of the block once) with a before, after or
+// inside the block.  This kernel is VALU-issue bound (every wave64 VALU op
+// costs ~4 cycles, FP64 or integer alike; HBM traffic is negligible), so it is
+// built to minimise the VALU instruction count per union set:
 //
-//  * everything indexed by c (A diag, scaled y, singleton weights, presence
-//    factors) and the Sigma~ row of a are staged in LDS once per unit / per a
-//    and read with immediate offsets — no per-step address arithmetic;
+//  * per step only the {a, b, c} extension is computed: the a-independent
+//    {b, c} weights come precomputed (k_build_bc3, once per locus) and are
+//    streamed with the tile row of Sigma~, both one step ahead of use;
+//  * the (a, c) terms (lane-owned) and (a, b) terms (lane-parallel, into LDS)
+//    are hoisted per a; everything else indexed by b is staged in LDS once per
+//    unit and read with immediate offsets;
 //  * y is pre-scaled by sqrt(log2(e)/2), so every quadratic form is directly
 //    the base-2 exponent h_T of the subset weight;
 //  * 1/sqrt(pivot) is v_rsq_f64 (5e-8 relative on gfx950, tools/rsq_acc.hip)
@@ -22,9 +29,9 @@
 //    row / column partial sums and pit0 is applied once per record;
 //  * accumulators keep a lazy shift: a contribution at shift G is added with
 //    one power-of-two scale and the shift only moves (rarely, in one
-//    wave-uniform branch) when G exceeds it by > 960 bits.  Contributions more than ~1022 bits below
-//    an accumulator's own running maximum vanish, exactly as in the
-//    branch-free fold they replace.
+//    wave-uniform branch) when G exceeds it by > 960 bits.  Contributions more
+//    than ~1022 bits below an accumulator's own running maximum vanish,
+//    exactly as in the branch-free fold they replace.
 //
 // Absent members (mixed loci) are masked by zeroing their pivot factor, which
 // zeroes every subset weight containing them (checkOR of postcal.cpp:907-955).
