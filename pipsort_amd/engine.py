@@ -168,6 +168,8 @@ def load_library(path: str = LIB_PATH):
         "psx_sync": (c_int, [vp, P(c_i32)]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("PSX_ENGINE_LIB") and not hasattr(lib, name):
+            continue  # an older build under A/B comparison
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -25,8 +25,22 @@ def _sexp(v, t):
     return r
 
 
+BIG_LOCUS = 10_000_000  # configurations: above this the reference's normaliser drifts (see below)
+
+
 def assert_parity(got: E.Accumulators, ref: dict, pip_tol=1e-9, ll_rtol=1e-10):
+    """Engine vs oracle.  Above BIG_LOCUS configurations the reference's serial
+    addlogSpace accumulation of the normaliser (postcal.h:102-112, restated by
+    the oracle) drifts by up to ~2e-7 log units (profiles/r01w_total_drift.txt:
+    the engine matches an exact fsum of the oracle's own per-configuration L to
+    4e-12), which scales every PIP: there PIPs are held to the north star's
+    1e-6 and the per-SNP log accumulators themselves to 1e-9 relative."""
     assert got.n_configs == ref["n_configs"]
+    if got.n_configs > BIG_LOCUS:
+        pip_tol = max(pip_tol, PIP_TOL)
+        for name in ("post", "no_causal", "shared"):
+            g, r = getattr(got, name), ref[name]
+            np.testing.assert_allclose(g[r != 0], r[r != 0], rtol=1e-9, atol=0, err_msg=name)
     assert abs(got.total - ref["total"]) <= 1e-9 * max(1.0, abs(ref["total"]))
     for name in ("post", "no_causal", "shared"):
         g, r = getattr(got, name), ref[name]
@@ -156,9 +170,19 @@ def test_union_batch_scores(gpu):
     np.testing.assert_allclose(got, ref, rtol=1e-12)
 
 
-@pytest.mark.parametrize("M0,M1,shared,c", [(90, 110, 60, 3), (64, 64, 64, 3), (130, 70, 5, 2), (1, 3, 1, 3)])
+@pytest.mark.parametrize("M0,M1,shared,c", [(90, 110, 60, 3), (64, 64, 64, 3), (130, 70, 5, 2), (1, 3, 1, 3),
+                                              (100, 37, 30, 3), (200, 190, 150, 3)])
 def test_mixed_membership_loci(gpu, M0, M1, shared, c):
-    """Union SNPs present in one study only, U not a multiple of 64, tiny loci."""
+    """Union SNPs present in one study only, U not a multiple of 64, tiny loci.
+
+    (200, 190, 150, 3) has 26M configurations: there the reference's serial
+    log-space accumulation of the normaliser (addlogSpace, postcal.h:102-112,
+    restated by the oracle) drifts by 1.9e-7 log units, while the engine's
+    total matches an exact fsum of the oracle's own per-configuration values
+    to 4e-12 (profiles/r01w_total_drift.txt).  Every PIP then differs by that
+    factor, so this case is held to the north star's 1e-6 and its per-SNP log
+    accumulators to 1e-9 relative (they agree to 1e-13); assert_parity applies
+    that rule to every locus above BIG_LOCUS configurations."""
     ld, z, _, _, u2l = synth.mixed_locus(M0, M1, shared, seed=M0 + M1)
     seam = E.seam_from_arrays(ld, z, u2l, (5000, 9000), max_causal=c, sharing_param=0.5)
     pc = E.PostCal(seam)
@@ -166,7 +190,7 @@ def test_mixed_membership_loci(gpu, M0, M1, shared, c):
     assert_parity(pc.accum(), O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-9)
 
 
-@pytest.mark.parametrize("M,c", [(100, 3), (200, 2), (130, 3)])
+@pytest.mark.parametrize("M,c", [(100, 3), (200, 2), (130, 3), (3, 3), (63, 3), (64, 3), (65, 3), (129, 3), (192, 3)])
 def test_synthetic_vs_oracle(gpu, M, c):
     ld, z, _, _, u2l = synth.syn_v1(M)
     seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=c, sharing_param=0.25)
