@@ -292,11 +292,13 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     double total_a = 0;
     for (int C = 0; C < nblk; C++)
         for (int K = 0; K <= C; K++) total_a += (K < C) ? std::max(0, 64 * K - pad) : U;  // a-range per tile
-    // a-chunk size: k_sweep3 holds 2 waves per SIMD (233 VGPRs), i.e. 8 unit
+    // a-chunk size: k_sweep3 holds 2 waves per SIMD (~245 VGPRs), i.e. 8 unit
     // slots per CU.  Larger chunks amortise the per-unit prologue / records,
-    // smaller ones shorten the last dispatch round: aim for >= 6 rounds of the
-    // wave slots per shard (measured on MI355X, syn1000c3, tools/ca_sweep.sh:
-    // ca = 2..4 best at world 1, 2 at world 2, 1 at worlds 4 and 8).
+    // smaller ones shorten the last dispatch round (the longest-first order
+    // below leaves the short folded-diagonal units for it): about 3.5 rounds of
+    // the wave slots per shard, at most 4 a per unit (measured on MI355X,
+    // syn1000c3, tools/ca_sweep.sh: ca = 4 at world 1, 2 at worlds 2 and 4, 1 at
+    // world 8).
     static const double kTarget = [] {  // units per shard the a-chunk is sized for
         if (const char* v = std::getenv("PSX_K3_UNITS")) return std::atof(v);
         int dev = 0, cus = 256;
@@ -305,9 +307,10 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
             if (hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0)
                 cus = pr.multiProcessorCount;
         }
-        return 6.0 * (8.0 * cus);
+        return 3.5 * (8.0 * cus);
     }();
-    ca = (int)std::floor(total_a / (kTarget * world));
+    ca = (int)std::lround(total_a / (kTarget * world));
+    ca = std::min(ca, 4);
     if (const char* v = std::getenv("PSX_K3_CA")) ca = std::atoi(v);
     ca = std::max(1, std::min(64, ca));
     // Every union triple x < y < z belongs to exactly one unit family, by which
@@ -326,10 +329,11 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
             const int amax = (K < C) ? 64 * K : ldg;
             for (int a0 = pad; a0 < amax; a0 += ca) {
                 const int a1 = std::min(a0 + ca, amax);
-                // a diagonal tile runs its folded walk: half the steps plus the
-                // same per-unit / per-a work (0.71 of an off-diagonal unit, fitted to the
-                // per-shard times of the 8-way rehearsal, profiles/)
-                all.push_back({a0, a1, K, C, (double)(a1 - a0) * (K == C ? 0.71 : 1.0)});
+                // unit cost in off-diagonal-a units: a fixed per-unit part and a
+                // per-a part; a diagonal tile's folded walk has half the steps.
+                // Fitted to unit durations (tools/unit_trace.py, MI355X):
+                // off-diagonal 3.3 + 81.8 ca us, diagonal 3.0 + 48.4 ca us.
+                all.push_back({a0, a1, K, C, 0.04 + (double)(a1 - a0) * (K == C ? 0.59 : 1.0)});
             }
         }
     }
@@ -397,7 +401,7 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // on MI355X (world-8 shard 0.350 vs 0.352 ms: the tail is ~9 % of the
     // launch either way, tools/unit_trace.py), so off by default.  Totals above
     // are unchanged.
-    const size_t slots = (size_t)(kTarget / 6.0);
+    const size_t slots = (size_t)(kTarget / 3.5);
     if (std::getenv("PSX_K3_SPLIT") && mine.size() > 2 * slots) {
         std::vector<PlanUnit> out(mine.begin(), mine.end() - slots);
         for (size_t i = mine.size() - slots; i < mine.size(); i++) {
