@@ -7,6 +7,7 @@
 // same input formats and the same output files.
 #include <fcntl.h>
 #include <getopt.h>
+#include <thread>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -67,7 +68,32 @@ vector<int> read_sigma(const string& s) {
 }
 
 // util.cpp:86-96 importData: doubles separated by whitespace, stopping at the
-// first token `istream >> double` would reject.  mmap + strtod for speed.
+// first token `istream >> double` would reject.  mmap + strtod, parsed in
+// parallel chunks cut at whitespace: each chunk parses until its own first
+// rejected token, and the result is the chunks in order up to the first chunk
+// that stopped — exactly the sequential parse (an M = 2000 LD file is 150 MB).
+namespace {
+struct ParsedChunk {
+    vector<double> v;
+    bool stopped = false;
+};
+
+void parse_chunk(const char* s, const char* end, ParsedChunk& out) {
+    out.v.reserve((size_t)(end - s) / 8 + 1);
+    while (s < end) {
+        while (s < end && isspace((unsigned char)*s)) s++;
+        if (s >= end) break;
+        char c = *s;
+        if (!(isdigit((unsigned char)c) || c == '-' || c == '+' || c == '.')) { out.stopped = true; return; }
+        char* e = nullptr;
+        double v = strtod(s, &e);
+        if (e == s) { out.stopped = true; return; }
+        out.v.push_back(v);
+        s = e;
+    }
+}
+}  // namespace
+
 bool import_data(const string& fn, vector<double>& out) {
     int fd = open(fn.c_str(), O_RDONLY);
     if (fd < 0) {
@@ -85,17 +111,29 @@ bool import_data(const string& fn, vector<double>& out) {
     munmap(p, len + 1);
     const char* s = buf.c_str();
     const char* end = s + len;
-    out.reserve(len / 8);
-    while (s < end) {
-        while (s < end && isspace((unsigned char)*s)) s++;
-        if (s >= end) break;
-        char c = *s;
-        if (!(isdigit((unsigned char)c) || c == '-' || c == '+' || c == '.')) break;
-        char* e = nullptr;
-        double v = strtod(s, &e);
-        if (e == s) break;
-        out.push_back(v);
-        s = e;
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const size_t nt = len < (size_t)(1 << 20) ? 1 : hw;
+    // chunk boundaries at whitespace, so no token is split
+    vector<const char*> cut(nt + 1);
+    cut[0] = s;
+    cut[nt] = end;
+    for (size_t i = 1; i < nt; i++) {
+        const char* c = s + len * i / nt;
+        if (c < cut[i - 1]) c = cut[i - 1];
+        while (c < end && !isspace((unsigned char)*c)) c++;
+        cut[i] = c;
+    }
+    vector<ParsedChunk> parts(nt);
+    vector<std::thread> th;
+    for (size_t i = 1; i < nt; i++) th.emplace_back(parse_chunk, cut[i], cut[i + 1], std::ref(parts[i]));
+    parse_chunk(cut[0], cut[1], parts[0]);
+    for (auto& t : th) t.join();
+    size_t total = 0;
+    for (auto& c : parts) total += c.v.size();
+    out.reserve(out.size() + total);
+    for (auto& c : parts) {
+        out.insert(out.end(), c.v.begin(), c.v.end());
+        if (c.stopped) break;
     }
     return true;
 }

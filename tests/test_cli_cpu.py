@@ -63,3 +63,29 @@ def test_no_gpu_fails_loudly(ex):
     r = run(["-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "eur_afr_small_test_snp_map", "-n", "7000,7000",
              "-o", "out"], ex)
     assert r.returncode == 1 and "no HIP device" in r.stdout
+
+
+@pytest.mark.parametrize("stop_at", [None, 1, 250_000, 999_999])
+def test_ld_parser_stops_at_first_rejected_token(tmp_path, stop_at):
+    """util.cpp:86-96 semantics of the chunk-parallel LD parser: parsing stops at
+    the first token `istream >> double` rejects, wherever the parallel chunks
+    are cut (a 1000 x 1000 file is ~20 MB, several chunks).  The CLI then
+    reports the size it parsed (model.h:98-103) before touching the engine."""
+    import numpy as np
+    from pipsort_amd import synth
+    M = 1000
+    ld, z, names, rows, _ = synth.syn_v1(M)
+    d = synth.write_locus(str(tmp_path / "loc"), ld, z, names, rows)
+    if stop_at is not None:
+        p = os.path.join(d, "syn0.ld")
+        toks = open(p).read().split()
+        toks[stop_at] = "x" + toks[stop_at]
+        open(p, "w").write(" ".join(toks) + "\n")
+    r = run(["-c", "2", "-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "snp_map", "-n", "10000,8000", "-o", "out"], d)
+    if stop_at is None:
+        assert "LD matrix is size" not in r.stdout
+        assert "pushing back num snps 0 for study %d" % M in r.stdout
+    else:
+        m = int(np.sqrt(stop_at))
+        assert r.returncode == 1
+        assert f"LD matrix is size {m} x {m} but zscores has {M} snps" in r.stdout
