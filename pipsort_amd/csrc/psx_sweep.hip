@@ -307,7 +307,7 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
             if (hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0)
                 cus = pr.multiProcessorCount;
         }
-        return 3.5 * (8.0 * cus);
+        return 3.5 * (4.0 * PSX_K3_WAVES * cus);
     }();
     ca = (int)std::lround(total_a / (kTarget * world));
     ca = std::min(ca, 4);
@@ -396,24 +396,43 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // (An XCD-aware order — whole tiles binned per XCD so each 4 MB L2 serves
     // ~1/8 of the skewed tiles — measured 4 % slower than this natural order
     // once the next step's tile row is prefetched; not used.)
-    // optional (PSX_K3_SPLIT): the last dispatch round runs half units (b-walk
-    // steps [0, 32) and [32, 64) of the same (a-chunk, K, C)).  Measured neutral
-    // on MI355X (world-8 shard 0.350 vs 0.352 ms: the tail is ~9 % of the
-    // launch either way, tools/unit_trace.py), so off by default.  Totals above
-    // are unchanged.
-    const size_t slots = (size_t)(kTarget / 3.5);
-    if (std::getenv("PSX_K3_SPLIT") && mine.size() > 2 * slots) {
-        std::vector<PlanUnit> out(mine.begin(), mine.end() - slots);
-        for (size_t i = mine.size() - slots; i < mine.size(); i++) {
-            PlanUnit h = mine[i];
-            h.work *= 0.5;
-            h.j0 = 0;
-            h.j1 = 32;
-            out.push_back(h);
-            h.j0 = 32;
-            h.j1 = 64;
-            out.push_back(h);
+    // Tail split (PSX_K3_TAIL="frac:q"): the units that make up the last `frac`
+    // of this shard's work are cut into q b-walk ranges (steps [64i/q, 64(i+1)/q);
+    // a folded diagonal unit halves them), so the launch's last dispatch rounds
+    // are made of short pieces and the 2048 wave slots drain together.  Each
+    // piece repeats the unit prologue and writes its own records (the merge
+    // folds them like any other unit's).  Totals above are unchanged.
+    double tail_frac = 0.0;
+    int tail_q = 1;
+    if (const char* v = std::getenv("PSX_K3_TAIL")) {
+        tail_frac = std::atof(v);
+        if (const char* c = std::strchr(v, ':')) tail_q = std::atoi(c + 1);
+    } else if (std::getenv("PSX_K3_SPLIT")) {  // former option: last round in halves
+        tail_frac = -1.0;
+        tail_q = 2;
+    }
+    tail_q = std::max(1, std::min(32, tail_q));
+    if (tail_q > 1 && tail_frac != 0.0 && !mine.empty()) {
+        size_t cut = mine.size();
+        if (tail_frac < 0) {
+            const size_t slots = (size_t)(kTarget / 3.5);
+            cut = mine.size() > 2 * slots ? mine.size() - slots : mine.size();
+        } else {
+            double tot = 0, run = 0;
+            for (auto& u : mine) tot += u.work;
+            while (cut > 0 && run + mine[cut - 1].work <= tail_frac * tot) run += mine[--cut].work;
         }
+        std::vector<PlanUnit> out(mine.begin(), mine.begin() + cut);
+        for (size_t i = cut; i < mine.size(); i++)
+            for (int p = 0; p < tail_q; p++) {
+                PlanUnit h = mine[i];
+                h.work /= tail_q;
+                h.j0 = 64 * p / tail_q;
+                h.j1 = 64 * (p + 1) / tail_q;
+                out.push_back(h);
+            }
+        std::stable_sort(out.begin() + cut, out.end(),
+                         [](const PlanUnit& x, const PlanUnit& y) { return x.work > y.work; });
         mine.swap(out);
     }
     return 0;

@@ -208,6 +208,8 @@ struct Sweep3Smem {
     double bW[64];
     double sP0[64], sP1[64], sSh[64], sSl[64], sNs[64];
     int sM[64];
+    double g1ab[2][64], g1ac[2][64];  // the first a's Sigma~ row entries
+    int sPos[3][64];                   // record positions: c, b slot, a
 };
 union SweepSmem {  // a block runs either a k = 3 unit or a level-2 unit
     Sweep3Smem s3;
@@ -215,7 +217,7 @@ union SweepSmem {  // a block runs either a k = 3 unit or a level-2 unit
 };
 
 template <bool ALLPRES>
-__global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __restrict__ units,
+__global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const int4* __restrict__ units,
                                                   Acc5* __restrict__ rec, SetRec* __restrict__ srec, int rec_stride,
                                                   int* __restrict__ flag, const int* __restrict__ pos, int nk3,
                                                   TileArgs A2, const int4* __restrict__ units2,
@@ -245,6 +247,9 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
     double (&sSl)[64] = sm.s3.sSl;
     double (&sNs)[64] = sm.s3.sNs;
     int (&sM)[64] = sm.s3.sM;
+    double (&g1ab)[2][64] = sm.s3.g1ab;
+    double (&g1ac)[2][64] = sm.s3.g1ac;
+    int (&sPos)[3][64] = sm.s3.sPos;
 
     const int unit = blockIdx.x;  // grid position = unit index: XCD = unit % 8 (plan_units3c)
     const int t = threadIdx.x;
@@ -307,6 +312,22 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
     const double* bm1 = A.bcmu[1] + (size_t)tile * 4096 + t;
     const int2* bnn = A.bcn + (size_t)tile * 4096 + t;
 
+    // record positions (CSR map) of this unit's c / b-slot / a records, and the
+    // first a's Sigma~ row entries, loaded with the unit prologue into LDS: no
+    // dependent global-load round trip later at the first a or at the record
+    // writes, and no registers held across the walk
+    {
+        const size_t rbase = (size_t)unit * rec_stride;
+        sPos[0][t] = pos[rbase + t];
+        sPos[1][t] = pos[rbase + 64 + t];
+        sPos[2][t] = (t < a1 - a0) ? pos[rbase + 128 + t] : -1;
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            g1ab[s][t] = okb ? A.G[s][(size_t)(a0 - pad) * ldg + ubl] : 0.0;
+            g1ac[s][t] = okc ? A.G[s][(size_t)(a0 - pad) * ldg + uc] : 0.0;
+        }
+    }
+
     unsigned long long t_ph[4] = {0ull, 0ull, 0ull, 0ull};  // diagnostics: phases of the first a
     if (A.trace) t_ph[0] = wall_clock64();
     for (int ai = 0; ai < a1 - a0; ai++) {
@@ -328,7 +349,7 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
             split3(ha, rPa, tab, nA, muA);
             {
                 // {a, b} and {b} for this lane's b, into LDS
-                const double Gab = okb ? A.G[s][(size_t)ua * ldg + ubl] : 0.0;
+                const double Gab = ai ? (okb ? A.G[s][(size_t)ua * ldg + ubl] : 0.0) : g1ab[s][t];
                 const double Abb = okb ? A.Ad[s][ubl] : 1.0;
                 const double yb = okb ? A.ys[s][ubl] : 0.0;
                 const double l = Gab * iAaa;
@@ -354,7 +375,7 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
                 abN[s][t] = nAB;
             }
             // {a, c}: lane-owned
-            const double Gac = okc ? A.G[s][(size_t)ua * ldg + uc] : 0.0;
+            const double Gac = ai ? (okc ? A.G[s][(size_t)ua * ldg + uc] : 0.0) : g1ac[s][t];
             l1[s] = Gac * iAaa;
             D1[s] = fma(-l1[s], Gac, Acc[s]);
             const double w1 = fma(-l1[s], ya, yc[s]);
@@ -531,11 +552,12 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
         if (A.trace && ai == 0) t_ph[2] = wall_clock64();
         Acc5 ra = lacc_rec(accA, A.Ck, A.pit0);
         wave_fold_acc(ra);
-        if (t == 0) put_rec(rec, pos, (size_t)unit * rec_stride + 128 + ai, ra);
+        const int qa = sPos[2][ai];
+        if (t == 0 && qa >= 0) rec[qa] = ra;
         if (A.trace && ai == 0) t_ph[3] = wall_clock64();
     }
     __syncthreads();
-    put_rec(rec, pos, (size_t)unit * rec_stride + t, lacc_rec(accC, A.Ck, A.pit0));
+    if (sPos[0][t] >= 0) rec[sPos[0][t]] = lacc_rec(accC, A.Ck, A.pit0);
     {
         LAcc sl;
         sl.m = sM[t];
@@ -544,7 +566,7 @@ __global__ __launch_bounds__(64, 2) void k_sweep3(Sweep3Args A, const int4* __re
         sl.sh = sSh[t];
         sl.sl = sSl[t];
         sl.ns = sNs[t];
-        put_rec(rec, pos, (size_t)unit * rec_stride + 64 + t, lacc_rec(sl, A.Ck, A.pit0));
+        if (sPos[1][t] >= 0) rec[sPos[1][t]] = lacc_rec(sl, A.Ck, A.pit0);
     }
     SetRec sr;
     sr.tot = totC * A.pit0;
