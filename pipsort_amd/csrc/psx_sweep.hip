@@ -393,9 +393,10 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // timeline (tools/unit_trace.py) showed a ~60 us tail of full-length units
     // on a world-8 shard in tile order.  Stable: tile order kept within a class.
     std::stable_sort(mine.begin(), mine.end(), [](const PlanUnit& x, const PlanUnit& y) { return x.work > y.work; });
-    // (An XCD-aware order — whole tiles binned per XCD so each 4 MB L2 serves
-    // ~1/8 of the skewed tiles — measured 4 % slower than this natural order
-    // once the next step's tile row is prefetched; not used.)
+    // (An XCD-aware order — runs of one tile's units packed onto the 8 XCDs,
+    // workgroup i running on XCD (i + launch offset) % 8, so each 4 MB L2 serves
+    // ~1/8 of the tile rows — measured neutral (r01y, worlds 1-8) once the next
+    // step's tile row is prefetched; not used.)
     // Tail split (PSX_K3_TAIL="frac:q"): the units that make up the last `frac`
     // of this shard's work are cut into q b-walk ranges (steps [64i/q, 64(i+1)/q);
     // a folded diagonal unit halves them), so the launch's last dispatch rounds

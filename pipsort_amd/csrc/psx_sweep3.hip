@@ -581,12 +581,13 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
     wave_fold_set(sr);
     if (t == 0) srec[unit] = sr;
     if (A.trace && t == 0) {
-        unsigned hw;
+        unsigned hw, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         unsigned long long* tr = A.trace + 8 * (size_t)unit;
         tr[0] = t_start;
         tr[1] = wall_clock64();
-        tr[2] = hw;
+        tr[2] = hw | ((unsigned long long)xcc << 32);
         tr[3] = (unsigned long long)unit | ((unsigned long long)diag << 32) | ((unsigned long long)(a1 - a0) << 33);
         for (int i = 0; i < 4; i++) tr[4 + i] = t_ph[i];
     }

@@ -62,4 +62,16 @@ for dflag in (0, 1):
           f"rest {((en - ph[:, 3]) / 100.0)[m].mean():.1f}")
 bu = np.array([d.mean() for d in np.array_split(dur[np.argsort(uid)], 10)])
 print("mean duration by unit-index decile:", np.round(bu, 1).tolist())
+
+# first-a walk time and unit duration by start-time decile (cold-start effects)
+sdec = np.array_split(np.argsort(st), 10)
+print("first-a steps (us) by start-time decile:", [round(float(steps[i].mean()), 1) for i in sdec])
+print("unit duration (us) by start-time decile:", [round(float(dur[i].mean()), 1) for i in sdec])
+print("units with 4 a: later-a time per a (us) by start decile:",
+      [round(float(((en[i] - ph[i, 3]) / 100.0)[na[i] == 4].mean() / 3.0), 1) if (na[i] == 4).any() else None
+       for i in sdec])
+
+xcc = (tr[:, 2] >> 32) & 0xf
+print("XCC of unit index (first 16):", xcc[:16].tolist(), "; fraction with XCC == index % 8:",
+      round(float((xcc == (np.arange(len(xcc)) % 8)).mean()), 3))
 pc.close()
