@@ -162,6 +162,51 @@ def sss_probe(reps=20):
                          "batch is sub-millisecond on one GPU"}
 
 
+def torch_allgather(backend):
+    """psx_allgather_fn over torch.distributed (RCCL for nccl, host for gloo)."""
+    world = dist.get_world_size()
+
+    def ag(b: bytes) -> bytes:
+        dev = "cuda" if backend == "nccl" else "cpu"
+        x = torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+        out = torch.empty(len(b) * world, dtype=torch.uint8, device=dev)
+        dist.all_gather_into_tensor(out, x)
+        return out.cpu().numpy().tobytes()
+    return ag
+
+
+def sss_probe_sharded(rank, world, backend):
+    """BASELINE configs[4] on `world` GPUs: the walk with every iteration's
+    batch split across the ranks (psx_run_sss_sharded, one all-gather of the
+    slices' scores per iteration), then the accumulator exchange."""
+    M = 2000
+    ld, z, _, _, u2l = synth.syn_v1(M)
+    mi = E.model_inputs(ld, z, u2l, (10000, 8000), max_causal=5, sharing_param=0.25)
+    pc = E.PostCal(mi)
+    pc.set_shard(rank, world)
+    ag = torch_allgather(backend)
+    pc.run_sss_sharded(ag)  # warm-up (allocations, collective setup)
+    dist.barrier()
+    t0 = time.perf_counter()
+    iters = pc.run_sss_sharded(ag)
+    nb = pc.partials_bytes()
+    mine = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    pc.export_partials(mine.data_ptr())
+    torch.cuda.synchronize()
+    allp = torch.frombuffer(bytearray(ag(mine.cpu().numpy().tobytes())), dtype=torch.uint8).cuda()
+    pc.merge_partials(allp.data_ptr(), world)
+    torch.cuda.synchronize()
+    walk_ms = (time.perf_counter() - t0) * 1e3
+    x = torch.tensor([walk_ms], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+    dist.all_reduce(x, op=dist.ReduceOp.MAX)
+    n = pc.accum().n_configs
+    pc.close()
+    return {"workload": "SYN-v1 2-study locus, M=2000 SNPs, -c 5 -p 0.25 -n 10000,8000 (BASELINE configs[4])",
+            "walk_iterations": iters, "walk_configs": n, "walk_ms_incl_exchange": float(x.item()),
+            "multi_gpu": f"batch split over {world} ranks, one all-gather of scores per iteration "
+                         "(psx_run_sss_sharded) + one accumulator exchange"}
+
+
 def example_wall():
     """Wall-clock of the drop-in PIPSORT CLI on tests/example (-c 2 -p 0.25)."""
     import loci
@@ -295,6 +340,7 @@ def main():
     torch.cuda.synchronize()
     acc = pc.accum() if (world == 1 or rank == 0) else None
 
+    sss_line = sss_probe_sharded(rank, world, backend) if world > 1 else None
     if rank == 0:
         value = configs_per_step * args.steps / elapsed
         avg_kernel_s = (kms / max(launches, 1)) / 1e3
@@ -340,6 +386,8 @@ def main():
             "pass_mode": "async (no host sync per step)" if use_async else "synchronous",
             "configs_checked": int(acc.n_configs) if acc is not None else None,
         }
+        if world > 1:
+            out["sss"] = sss_line
         if world == 1:
             out["sss"] = sss_probe()
             w, same = example_wall()

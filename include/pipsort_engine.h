@@ -33,6 +33,7 @@ extern "C" {
 #define PSX_ESINGULAR (-4) /* postcal.cpp:291-294 "matrix is singular" (ref exits 0) */
 #define PSX_EORDER (-5)    /* postcal.cpp:587-590 "This did not work as expected" */
 #define PSX_ERANGE (-6)    /* sweep too large to index / unsupported c        */
+#define PSX_EEXCHANGE (-7) /* the caller's all-gather callback failed            */
 
 typedef struct psx_engine psx_engine;
 
@@ -157,6 +158,22 @@ int psx_run_configs(psx_engine *e, const int16_t *rows, int64_t n_rows, int32_t 
 /* PostCal::sss_computeTotalLikelihood (sss_postcal.cpp:102-380): stochastic
  * shotgun search, host random walk (mt19937(12345)) + GPU neighbour batches. */
 int psx_run_sss(psx_engine *e, int32_t *iterations_out);
+
+/* All-gather callback of the sharded SSS walk: gather `bytes` host bytes from
+ * every rank into recv (world * bytes, rank order).  Returns 0 on success.  The
+ * caller binds it to its collective (torch.distributed / RCCL, MPI, ...). */
+typedef int (*psx_allgather_fn)(void *ctx, const void *send, void *recv, int64_t bytes);
+
+/* sss_computeTotalLikelihood (sss_postcal.cpp:102-380) across the ranks of
+ * psx_set_shard (the reference runs it on one host, OpenMP inside).  Every
+ * rank runs the same walk (same neighbourhoods, hash map and mt19937 draws);
+ * each evaluates and accumulates a contiguous slice of every iteration's batch
+ * (the null configuration on rank 0), and one all-gather per iteration shares
+ * the slices' scores and the ranks' running normalisers (the :265-270 stop
+ * test).  The accumulators are then merged like a sharded exhaustive sweep
+ * (psx_export_partials / all-gather / psx_merge_partials).  With world 1 it
+ * is psx_run_sss. */
+int psx_run_sss_sharded(psx_engine *e, psx_allgather_fn allgather, void *ctx, int32_t *iterations_out);
 
 /* PostCal::expand_and_compute_lkl (sss_postcal.cpp:447-685), batched: evaluate
  * n_sets union sets (ascending union indices, -1 padded to `stride`), return the

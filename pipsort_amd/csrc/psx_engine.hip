@@ -1524,8 +1524,10 @@ struct VecHash {  // postcal.h:43-56
 };
 }  // namespace
 
-int psx_run_sss(psx_engine* e, int32_t* iterations_out) {
+namespace {
+static int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* iterations_out) {
     HIPCHK(hipSetDevice(e->dev));
+    const int rank = allgather ? e->rank : 0, world = allgather ? e->world : 1;
     int rc;
     if ((rc = reset_acc(e))) return rc;
     std::memset(&e->timing, 0, sizeof(e->timing));
@@ -1596,6 +1598,7 @@ int psx_run_sss(psx_engine* e, int32_t* iterations_out) {
         flat.reserve(batch.size() * stride);
         for (auto& v : batch) for (int j = 0; j < stride; j++) flat.push_back(j < (int)v.size() ? v[j] : -1);
         std::vector<double> sc(batch.size());
+        double gsum = 0.0;  // the running normaliser over all ranks (world > 1)
         {
             std::vector<int> vv;
             std::vector<size_t> wh;
@@ -1605,15 +1608,46 @@ int psx_run_sss(psx_engine* e, int32_t* iterations_out) {
                 wh.push_back(i);
                 vv.insert(vv.end(), flat.begin() + i * stride, flat.begin() + (i + 1) * stride);
             }
-            std::vector<double> s2(wh.size());
-            if ((rc = eval_generic(e, vv, stride, wh.size(), nullptr, true, s2.data(), &kms))) return rc;
-            for (size_t i = 0; i < wh.size(); i++) sc[wh[i]] = s2[i];
-            if (nulls > 0 && (rc = fold_null(e, nulls))) return rc;
+            // this rank's contiguous slice of the batch (all of it at world 1)
+            const size_t nw = wh.size();
+            const size_t lo = nw * rank / world, hi = nw * (rank + 1) / world;
+            std::vector<double> s2(nw);
+            std::vector<int> mine(vv.begin() + lo * stride, vv.begin() + hi * stride);
+            if ((rc = eval_generic(e, mine, stride, hi - lo, nullptr, true, s2.data() + lo, &kms))) return rc;
+            if (nulls > 0 && rank == 0 && (rc = fold_null(e, nulls))) return rc;
+            if (world > 1) {
+                // one all-gather: [slice length, normaliser (m, s), slice scores]
+                const size_t per = (nw + world - 1) / world, w = 3 + per;
+                std::vector<double> snd(w, 0.0), rcv(w * world, 0.0);
+                SetRec t;
+                HIPCHK(hipMemcpy(&t, e->dsacc, sizeof(SetRec), hipMemcpyDeviceToHost));
+                snd[0] = (double)(hi - lo);
+                snd[1] = (double)t.m;
+                snd[2] = t.tot;
+                std::copy(s2.begin() + lo, s2.begin() + hi, snd.begin() + 3);
+                if (allgather(ctx, snd.data(), rcv.data(), (int64_t)(w * sizeof(double))))
+                    return fail(PSX_EEXCHANGE, "SSS all-gather callback failed");
+                double mx = -INFINITY;
+                std::vector<double> part(world, 0.0);
+                for (int r = 0; r < world; r++) {
+                    const double* q = rcv.data() + (size_t)r * w;
+                    const size_t rlo = nw * r / world, rn = nw * (r + 1) / world - rlo;
+                    if ((size_t)q[0] != rn) return fail(PSX_EEXCHANGE, "SSS all-gather: ranks disagree on the batch");
+                    std::copy(q + 3, q + 3 + rn, s2.begin() + rlo);
+                    part[r] = logval(e, (int32_t)q[1], q[2]);
+                    if (part[r] != 0.0) mx = std::max(mx, part[r]);
+                }
+                double acc = 0.0;  // the ranks' normalisers, combined in rank order
+                for (int r = 0; r < world; r++)
+                    if (part[r] != 0.0) acc += std::exp(part[r] - mx);
+                gsum = acc > 0 ? mx + std::log(acc) : 0.0;
+            }
+            for (size_t i = 0; i < nw; i++) sc[wh[i]] = s2[i];
         }
         for (size_t i = 0; i < batch.size(); i++)
             if (batch_pos[i] >= 0) lk[batch_pos[i]] = sc[i];
-        double sss_sum;
-        if ((rc = sss_total(sss_sum))) return rc;
+        double sss_sum = gsum;
+        if (world == 1 && (rc = sss_total(sss_sum))) return rc;
         if (not_done.empty()) break;                                                       // :260-263
         if (iter >= 100 && (1 - std::exp(old_sum - sss_sum)) <= 0.001) break;             // :265-270
         for (int i : not_done) hm[nbd[i]] = lk[i];                                         // :280-284
@@ -1648,6 +1682,14 @@ int psx_run_sss(psx_engine* e, int32_t* iterations_out) {
     HIPCHK(hipMemcpy(&s, e->dsacc, sizeof(SetRec), hipMemcpyDeviceToHost));
     e->timing.configs = (uint64_t)(s.npat + 0.5);
     return 0;
+}
+}  // namespace
+
+int psx_run_sss(psx_engine* e, int32_t* iterations_out) { return run_sss(e, nullptr, nullptr, iterations_out); }
+
+int psx_run_sss_sharded(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* iterations_out) {
+    if (!allgather && e->world > 1) return fail(PSX_EINVAL, "psx_run_sss_sharded: no all-gather callback");
+    return run_sss(e, allgather, ctx, iterations_out);
 }
 
 int psx_get_accum(psx_engine* e, psx_accum* out) {

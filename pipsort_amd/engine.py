@@ -25,6 +25,7 @@ PSX_EHIP = -3
 PSX_ESINGULAR = -4
 PSX_EORDER = -5
 PSX_ERANGE = -6
+PSX_EEXCHANGE = -7
 
 # Every symbol declared in include/pipsort_engine.h and include/pipsort_model.h
 EXPORTED = [
@@ -35,8 +36,11 @@ EXPORTED = [
     "psx_fold_partials_host", "psx_shard_stats", "psx_set_stream",
     "psx_psd_shift", "psx_lowrank_study", "psx_sym_eigen", "psx_lu_det",
     "psx_create_from_ld", "psx_psd_shift_gpu", "psx_lu_det_gpu",
-    "psx_run_exhaustive_async", "psx_sync",
+    "psx_run_exhaustive_async", "psx_sync", "psx_run_sss_sharded",
 ]
+
+# psx_allgather_fn (include/pipsort_engine.h): int (*)(void *ctx, const void *send, void *recv, int64_t bytes)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
 
 
 class EngineError(RuntimeError):
@@ -166,6 +170,7 @@ def load_library(path: str = LIB_PATH):
         "psx_lu_det_gpu": (c_int, [P(dbl), c_i32, c_int, P(dbl)]),
         "psx_run_exhaustive_async": (c_int, [vp]),
         "psx_sync": (c_int, [vp, P(c_i32)]),
+        "psx_run_sss_sharded": (c_int, [vp, ALLGATHER_FN, vp, P(c_i32)]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("PSX_ENGINE_LIB") and not hasattr(lib, name):
@@ -492,6 +497,30 @@ class PostCal:
         """sss_postcal.cpp:102 sss_computeTotalLikelihood; returns iterations."""
         it = ctypes.c_int32(0)
         _check(self.lib.psx_run_sss(self.h, ctypes.byref(it)))
+        return it.value
+
+    def run_sss_sharded(self, allgather) -> int:
+        """The SSS walk across the ranks of set_shard (psx_run_sss_sharded).
+        allgather(send: bytes) -> bytes gathers every rank's equal-sized `send`
+        in rank order (e.g. torch.distributed.all_gather_into_tensor).  Merge
+        the accumulators afterwards with export_partials / merge_partials."""
+        err = []
+
+        def cb(_ctx, send, recv, nbytes):
+            try:
+                out = allgather(ctypes.string_at(send, nbytes))
+                ctypes.memmove(recv, out, len(out))
+                return 0
+            except BaseException as ex:  # reported through the engine's error code
+                err.append(ex)
+                return 1
+
+        fn = ALLGATHER_FN(cb)
+        it = ctypes.c_int32(0)
+        rc = self.lib.psx_run_sss_sharded(self.h, fn, None, ctypes.byref(it))
+        if err:
+            raise err[0]
+        _check(rc)
         return it.value
 
     def eval_union_batch(self, sets: np.ndarray, accumulate: bool = False) -> np.ndarray:

@@ -35,3 +35,6 @@ def test_bench_sharded_two_ranks(gpu, world):
     assert out["n_gpus"] == world
     # every rank's shard folded into rank 0's accumulators: all configurations counted once
     assert out["configs_checked"] == out["config"]["configs_per_step"] == 179_701
+    # the SSS walk with its batches split across the ranks (psx_run_sss_sharded):
+    # the same walk and configuration count as one GPU (bench sss line, r01x)
+    assert out["sss"]["walk_iterations"] == 2 and out["sss"]["walk_configs"] == 23_993
