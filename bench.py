@@ -340,7 +340,12 @@ def main():
     torch.cuda.synchronize()
     acc = pc.accum() if (world == 1 or rank == 0) else None
 
-    sss_line = sss_probe_sharded(rank, world, backend) if world > 1 else None
+    sss_line = None
+    if world > 1:  # after the timed region; a failure here must not lose the bench line
+        try:
+            sss_line = sss_probe_sharded(rank, world, backend)
+        except Exception as ex:  # noqa: BLE001
+            sss_line = {"error": f"{type(ex).__name__}: {ex}"}
     if rank == 0:
         value = configs_per_step * args.steps / elapsed
         avg_kernel_s = (kms / max(launches, 1)) / 1e3
