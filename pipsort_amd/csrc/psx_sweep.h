@@ -72,7 +72,8 @@ struct Sweep3Args {
     const double* Ad[2];       // diag(A_s) = 1/d_s + diag(Sigma~_s), by u
     const double* ys[2];       // y_s * sqrt(log2(e) / 2), by u
     const double* skewT[2];    // skewed Sigma~ tiles in v space, tile(K, C), K <= C
-    const double* bcmu[2];     // {b, c} subset weights mu per [tile][step][lane] (a-independent)
+    const double2* g01;        // skewT of both studies interleaved (one 16-byte load per step)
+    const double2* mu01;       // {b, c} subset weights mu per [tile][step][lane], both studies (a-independent)
     const int2* bcn;           // their base-2 exponents, both studies
     const double* muS[2];      // singleton weights {c}, by u
     const int* nS[2];
@@ -91,13 +92,16 @@ int launch_scale_y(const double* y, int n, double* ys, hipStream_t st);
 int launch_build_skewT(const double* G, int ldg, int pad, double* skew, hipStream_t st);
 // {b, c} subset weights of every skewT entry (the a-independent half of a k = 3
 // step), computed once per locus with the sweep kernel's own arithmetic
-int launch_build_bc3(const Sweep3Args& A, int ntile, double* mu0, double* mu1, int2* n, hipStream_t st);
+int launch_build_bc3(const Sweep3Args& A, int ntile, double2* mu01, int2* n, hipStream_t st);
+// out[i] = (a[i], b[i])
+int launch_interleave2(const double* a, const double* b, size_t n, double2* out, hipStream_t st);
 
 struct SweepPlanCache {
     std::map<std::tuple<int, int, int, int, int>, SweepPlan> plans;  // (k, U, rank, world, variant)
     double* d_skew[2] = {nullptr, nullptr};  // skewed Sigma~ tiles (B <= T), k = 2 and exact k = 3
     double* d_skewT[2] = {nullptr, nullptr}; // lane-owns-c tiles in v space (k = 3 fast kernel)
-    double* d_bcmu[2] = {nullptr, nullptr};  // {b, c} weights per skewT entry (k = 3 fast kernel)
+    double2* d_g01 = nullptr;                // skewT of both studies interleaved (k = 3 fast kernel)
+    double2* d_mu01 = nullptr;               // {b, c} weights per skewT entry, both studies
     int2* d_bcn = nullptr;
     double* d_muS[2] = {nullptr, nullptr};   // singleton subset weights
     int* d_nS[2] = {nullptr, nullptr};

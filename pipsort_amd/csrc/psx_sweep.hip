@@ -536,10 +536,11 @@ static Sweep3Args sweep3_args(const SweepPlanCache& C, const SweepArgs& a, int U
     Sweep3Args S3;
     for (int s = 0; s < 2; s++) {
         S3.G[s] = A.G[s]; S3.Ad[s] = A.Ad[s]; S3.ys[s] = C.d_ys[s]; S3.skewT[s] = C.d_skewT[s];
-        S3.bcmu[s] = C.d_bcmu[s];
         S3.muS[s] = A.muS[s]; S3.nS[s] = A.nS[s]; S3.rsd[s] = A.rsd[s];
     }
     S3.bcn = C.d_bcn;
+    S3.g01 = C.d_g01;
+    S3.mu01 = C.d_mu01;
     S3.pad = ldg - U;
     S3.pres = A.pres;
     S3.tab = C.d_tab;
@@ -554,13 +555,14 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
     for (int s = 0; s < 2; s++) {
         hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
         hipFree(C.d_skewT[s]); C.d_skewT[s] = nullptr;
-        hipFree(C.d_bcmu[s]); C.d_bcmu[s] = nullptr;
         hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
         hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
         hipFree(C.d_ys[s]); C.d_ys[s] = nullptr;
     }
     hipFree(C.d_tab); C.d_tab = nullptr;
     hipFree(C.d_bcn); C.d_bcn = nullptr;
+    hipFree(C.d_g01); C.d_g01 = nullptr;
+    hipFree(C.d_mu01); C.d_mu01 = nullptr;
     {
         // 2^(i/256) correctly rounded (long double on the host)
         double tab[256];
@@ -593,9 +595,11 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
     }
     {  // the a-independent {b, c} weights of every k = 3 step
         Sweep3Args S3 = sweep3_args(C, a, U, ldg);
-        for (int s = 0; s < 2; s++) SWCHK(hipMalloc(&C.d_bcmu[s], sizeof(double) * (size_t)ntile * 4096));
+        SWCHK(hipMalloc(&C.d_mu01, sizeof(double2) * (size_t)ntile * 4096));
         SWCHK(hipMalloc(&C.d_bcn, sizeof(int2) * (size_t)ntile * 4096));
-        if (launch_build_bc3(S3, ntile, C.d_bcmu[0], C.d_bcmu[1], C.d_bcn, st)) SWCHK(hipGetLastError());
+        if (launch_build_bc3(S3, ntile, C.d_mu01, C.d_bcn, st)) SWCHK(hipGetLastError());
+        SWCHK(hipMalloc(&C.d_g01, sizeof(double2) * (size_t)ntile * 4096));
+        if (launch_interleave2(C.d_skewT[0], C.d_skewT[1], (size_t)ntile * 4096, C.d_g01, st)) SWCHK(hipGetLastError());
     }
     C.skew_ldg = ldg;
     C.skew_src[0] = a.G0;
@@ -793,13 +797,14 @@ void sweep_free(SweepPlanCache& C) {
     for (int s = 0; s < 2; s++) {
         hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
         hipFree(C.d_skewT[s]); C.d_skewT[s] = nullptr;
-        hipFree(C.d_bcmu[s]); C.d_bcmu[s] = nullptr;
         hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
         hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
         hipFree(C.d_ys[s]); C.d_ys[s] = nullptr;
     }
     hipFree(C.d_tab); C.d_tab = nullptr;
     hipFree(C.d_bcn); C.d_bcn = nullptr;
+    hipFree(C.d_g01); C.d_g01 = nullptr;
+    hipFree(C.d_mu01); C.d_mu01 = nullptr;
     if (C.own_flag) hipFree(C.d_flag);
     C.d_flag = nullptr;
 }

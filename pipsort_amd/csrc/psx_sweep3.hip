@@ -159,12 +159,11 @@ __device__ __forceinline__ void bc_weight(double Gbc, const BTerms& b, double Ac
     split3(h2, b.R * r2 * chic, tab, n2, mu2);
 }
 
-// bcmu[s][tile][j][t], bcn[tile][j][t]: the {b, c} weights of the k = 3 walk,
+// mu01[tile][j][t] (both studies), bcn[tile][j][t]: the {b, c} weights of the k = 3 walk,
 // b = 64K + ((t + j) & 63), c = 64C + t (the folded diagonal walk uses the same
 // (slot, lane) pairs).  One block per (tile, step), lane t.
 template <bool ALLPRES>
-__global__ void k_build_bc3(Sweep3Args A, double* __restrict__ mu0, double* __restrict__ mu1,
-                            int2* __restrict__ nn) {
+__global__ void k_build_bc3(Sweep3Args A, double2* __restrict__ mu01, int2* __restrict__ nn) {
     const int tile = blockIdx.x, j = blockIdx.y, t = threadIdx.x;
     int C = 0;
     while ((C + 1) * (C + 2) / 2 <= tile) C++;
@@ -183,8 +182,7 @@ __global__ void k_build_bc3(Sweep3Args A, double* __restrict__ mu0, double* __re
         const double ych = 0.5 * (okc ? A.ys[s][uc] : 0.0);
         bc_weight(A.skewT[s][o], b, Acc, ych, chic, A.tab, n[s], mu[s]);
     }
-    mu0[o] = mu[0];
-    mu1[o] = mu[1];
+    mu01[o] = make_double2(mu[0], mu[1]);
     nn[o] = make_int2(n[0], n[1]);
 }
 
@@ -306,10 +304,10 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
     double totC = 0.0;
     int m0 = EMPTY, m1 = EMPTY;
     double nc0 = 0.0, nc1 = 0.0, npat = 0.0;
-    const double* sk0 = A.skewT[0] + (size_t)tile * 4096 + t;
-    const double* sk1 = A.skewT[1] + (size_t)tile * 4096 + t;
-    const double* bm0 = A.bcmu[0] + (size_t)tile * 4096 + t;
-    const double* bm1 = A.bcmu[1] + (size_t)tile * 4096 + t;
+    // the tile row: both studies' skewed Sigma~ entries and {b, c} weights as
+    // 16-byte pairs (three loads per step)
+    const double2* g01 = A.g01 + (size_t)tile * 4096 + t;
+    const double2* m01 = A.mu01 + (size_t)tile * 4096 + t;
     const int2* bnn = A.bcn + (size_t)tile * 4096 + t;
 
     // record positions (CSR map) of this unit's c / b-slot / a records, and the
@@ -401,16 +399,18 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
 
         // the next step's skewed Sigma~ entries and {b, c} weights are loaded one
         // step ahead (L2 / MALL latency is longer than the VALU work between)
-        double gnx0 = sk0[j0 * 64], gnx1 = sk1[j0 * 64], mnx0 = bm0[j0 * 64], mnx1 = bm1[j0 * 64];
+        double2 gnx = g01[j0 * 64], mnx = m01[j0 * 64];
         int2 nnx = bnn[j0 * 64];
         for (int j = j0; j < j1; j++) {
-            const double gcur0 = gnx0, gcur1 = gnx1, mcur0 = mnx0, mcur1 = mnx1;
+            const double gcur0 = gnx.x, gcur1 = gnx.y, mcur0 = mnx.x, mcur1 = mnx.y;
             const int2 ncur = nnx;
+#ifndef PSX_K3_NOLOAD_EXPERIMENT
             if (j + 1 < j1) {
-                gnx0 = sk0[(j + 1) * 64];
-                gnx1 = sk1[(j + 1) * 64];
-                mnx0 = bm0[(j + 1) * 64];
-                mnx1 = bm1[(j + 1) * 64];
+#else
+            if (false) {  // timing experiment only: results invalid
+#endif
+                gnx = g01[(j + 1) * 64];
+                mnx = m01[(j + 1) * 64];
                 nnx = bnn[(j + 1) * 64];
             }
             const int bs = (t + j) & 63;
@@ -612,9 +612,20 @@ int launch_build_skewT(const double* G, int ldg, int pad, double* skew, hipStrea
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_build_bc3(const Sweep3Args& A, int ntile, double* mu0, double* mu1, int2* n, hipStream_t st) {
+int launch_build_bc3(const Sweep3Args& A, int ntile, double2* mu01, int2* n, hipStream_t st) {
     // a non-ALLPRES build is exact for every locus (chi factors of present SNPs are 1)
-    hipLaunchKernelGGL((k_build_bc3<false>), dim3(ntile, 64), dim3(64), 0, st, A, mu0, mu1, n);
+    hipLaunchKernelGGL((k_build_bc3<false>), dim3(ntile, 64), dim3(64), 0, st, A, mu01, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+__global__ void k_interleave2(const double* __restrict__ a, const double* __restrict__ b, size_t n,
+                              double2* __restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = make_double2(a[i], b[i]);
+}
+
+int launch_interleave2(const double* a, const double* b, size_t n, double2* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_interleave2, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, b, n, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
