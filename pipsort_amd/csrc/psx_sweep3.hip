@@ -333,6 +333,9 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
         const unsigned pa = A.pres[ua];
         double l1[2], D1[2], w1h[2], Ep[2][4];  // Ep: {}, {a}, {c}, {a,c} relative to 2^{n_ac}
         int R[2];
+        // step j0 of the tile row: issued before the a prologue, whose work hides it
+        double2 gnx = g01[j0 * 64], mnx = m01[j0 * 64];
+        int2 nnx = bnn[j0 * 64];
         __syncthreads();  // previous a's (a, b) terms fully consumed
 #pragma unroll
         for (int s = 0; s < 2; s++) {
@@ -399,8 +402,6 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
 
         // the next step's skewed Sigma~ entries and {b, c} weights are loaded one
         // step ahead (L2 / MALL latency is longer than the VALU work between)
-        double2 gnx = g01[j0 * 64], mnx = m01[j0 * 64];
-        int2 nnx = bnn[j0 * 64];
         for (int j = j0; j < j1; j++) {
             const double gcur0 = gnx.x, gcur1 = gnx.y, mcur0 = mnx.x, mcur1 = mnx.y;
             const int2 ncur = nnx;
