@@ -130,36 +130,82 @@ __global__ void k_to_union(const double* __restrict__ S, int M, const int* __res
 // batches, the -b configs path, levels the tiled sweep does not cover.
 // forced[set] = (C0 mask, C1 mask) restricts a set to one pattern (configs rows).
 // ---------------------------------------------------------------------------
+// Register-resident: the set's Sigma~ sub-blocks, Ad and y are gathered into
+// LDS in one round trip; every loop runs over PSX_KMAX with `j < k` guards so
+// the per-lane arrays stay in VGPRs (no scratch); members outside a lane's
+// subset enter its LDL^T as zero rows, which leaves the in-subset arithmetic
+// (and its rounding) exactly that of psx::ldlt_terms.
 __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restrict__ sets, int stride,
                                                   const int* __restrict__ forced, SetRec* __restrict__ srec,
-                                                  Acc5* __restrict__ mrec) {
+                                                  Acc5* __restrict__ mrec, double* __restrict__ score) {
+    constexpr int KM = PSX_KMAX;
+    __shared__ double s_g[2][KM][KM];
+    __shared__ double s_ad[2][KM], s_y[2][KM];
     __shared__ double s_mu[2][64];
     __shared__ double s_f[2][64];
     __shared__ int s_n[2][64];
+    __shared__ int s_mem[KM];
     const int set = blockIdx.x;
     const int lane = threadIdx.x;
     const int* S = sets + (size_t)set * stride;
-    int mem[PSX_KMAX];
-    int k = 0;
-    for (int i = 0; i < stride && i < PSX_KMAX; i++) {
-        int v = S[i];
-        if (v >= 0) mem[k++] = v;
+    const int v = lane < stride && lane < KM ? S[lane] : -1;
+    const unsigned long long bal = __ballot(v >= 0);
+    const int k = __popcll(bal);
+    if (v >= 0) s_mem[__popcll(bal & ((1ull << lane) - 1ull))] = v;
+    __syncthreads();
+    for (int e = lane; e < 2 * KM * KM; e += 64) {
+        const int s = e / (KM * KM), i = (e / KM) % KM, j = e % KM;
+        if (i < k && j < i) s_g[s][i][j] = P.G[s][(size_t)s_mem[i] * P.ldg + s_mem[j]];
+    }
+    if (lane < 2 * KM) {
+        const int s = lane / KM, i = lane % KM;
+        if (i < k) {
+            s_ad[s][i] = P.Ad[s][s_mem[i]];
+            s_y[s][i] = P.y[s][s_mem[i]];
+        }
     }
     int pmask[2] = {0, 0};
-    for (int j = 0; j < k; j++) {
-        unsigned char pr = P.pres[mem[j]];
-        if (pr & 1) pmask[0] |= 1 << j;
-        if (pr & 2) pmask[1] |= 1 << j;
+#pragma unroll
+    for (int j = 0; j < KM; j++) {
+        if (j < k) {
+            const unsigned char pr = P.pres[s_mem[j]];
+            if (pr & 1) pmask[0] |= 1 << j;
+            if (pr & 2) pmask[1] |= 1 << j;
+        }
     }
+    __syncthreads();
     const int nsub = 1 << k;
     if (lane < nsub) {
+#pragma unroll
         for (int s = 0; s < 2; s++) {
-            int idx[PSX_KMAX];
-            int t = 0;
-            for (int j = 0; j < k; j++)
-                if (lane & (1 << j)) idx[t++] = mem[j];
-            double q, Pd;
-            psx::ldlt_terms(P.G[s], P.ldg, P.Ad[s], P.y[s], P.dval[s], idx, t, q, Pd);
+            double L[KM][KM], D[KM], w[KM];
+            double q = 0.0, Pd = 1.0;
+#pragma unroll
+            for (int i = 0; i < KM; i++) {
+                const bool in = i < k && ((lane >> i) & 1);
+                double di = 1.0, wi = 0.0;
+#pragma unroll
+                for (int j = 0; j < i; j++) {
+                    double acc = s_g[s][i][j];
+#pragma unroll
+                    for (int m = 0; m < j; m++) acc -= L[i][m] * L[j][m] * D[m];
+                    // L[j][*] = 0 and D[j] = 1 for j outside the subset
+                    L[i][j] = in && ((lane >> j) & 1) ? acc / D[j] : 0.0;
+                }
+                if (in) {
+                    di = s_ad[s][i];
+                    wi = s_y[s][i];
+#pragma unroll
+                    for (int m = 0; m < i; m++) {
+                        di -= L[i][m] * L[i][m] * D[m];
+                        wi -= L[i][m] * w[m];
+                    }
+                    q += wi * wi / di;
+                    Pd *= P.dval[s] * di;
+                }
+                D[i] = di;
+                w[i] = wi;
+            }
             int n;
             double mu;
             psx::split_exp(0.5 * q * PSX_LOG2E, 1.0 / sqrt(Pd), n, mu);
@@ -171,14 +217,16 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
     __syncthreads();
     const int S0 = pmask[0], S1 = pmask[1];
     const int Gll = s_n[0][S0] + s_n[1][S1] + 2;
-    int GN[PSX_KMAX];
-    for (int j = 0; j < k; j++) {
-        int bj = 1 << j;
-        int g1 = s_n[0][S0] + s_n[1][S1 & ~bj];
-        int g2 = s_n[0][S0 & ~bj] + s_n[1][S1];
+    int GN[KM];
+#pragma unroll
+    for (int j = 0; j < KM; j++) {
+        const int bj = 1 << j;
+        const int g1 = s_n[0][S0] + s_n[1][S1 & ~bj];
+        const int g2 = s_n[0][S0 & ~bj] + s_n[1][S1];
         GN[j] = psx::imax(g1, g2) + 2;
     }
-    const int GS = Gll + P.Ck[k];
+    const int Ck = P.Ck[k];
+    const int GS = Gll + Ck;
     int npat = 1;
     for (int j = 0; j < k; j++) npat *= 3;
     int fc0 = -1, fc1 = -1;
@@ -186,40 +234,56 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
         fc0 = forced[2 * set];
         fc1 = forced[2 * set + 1];
     }
+    double pit[KM + 1], pri[KM + 1];
+#pragma unroll
+    for (int j = 0; j <= KM; j++) {
+        pit[j] = P.pit[k][j];
+        pri[j] = P.prior[k][j];
+    }
     double tot = 0, nc0 = 0, nc1 = 0, smin = 1e300, npatv = 0;
     // noCausal[s] terms live on their own shifts (C_s empty => the other study is full)
-    const int Gnc0 = s_n[1][S1] + P.Ck[k], Gnc1 = s_n[0][S0] + P.Ck[k];
-    double p0[PSX_KMAX], p1[PSX_KMAX], sh[PSX_KMAX], sl[PSX_KMAX], ns[PSX_KMAX];
-    for (int j = 0; j < PSX_KMAX; j++) p0[j] = p1[j] = sh[j] = sl[j] = ns[j] = 0.0;
+    const int Gnc0 = s_n[1][S1] + Ck, Gnc1 = s_n[0][S0] + Ck;
+    double p0[KM], p1[KM], sh[KM], sl[KM], ns[KM];
+#pragma unroll
+    for (int j = 0; j < KM; j++) p0[j] = p1[j] = sh[j] = sl[j] = ns[j] = 0.0;
     for (int p = lane; p < npat; p += 64) {
-        int c0 = 0, c1 = 0, x[PSX_KMAX];
+        int c0 = 0, c1 = 0, x[KM];
         int r = p;
-        for (int j = 0; j < k; j++) {
-            x[j] = r % 3 + 1;
-            r /= 3;
-            if (x[j] & 1) c0 |= 1 << j;
-            if (x[j] & 2) c1 |= 1 << j;
+#pragma unroll
+        for (int j = 0; j < KM; j++) {
+            x[j] = 0;
+            if (j < k) {
+                x[j] = r % 3 + 1;
+                r /= 3;
+                if (x[j] & 1) c0 |= 1 << j;
+                if (x[j] & 2) c1 |= 1 << j;
+            }
         }
         if ((c0 & ~S0) || (c1 & ~S1)) continue;  // (study, SNP) pair not present: no mask bit
         if (fc0 >= 0 && (c0 != fc0 || c1 != fc1)) continue;
-        int nsh = __popc(c0 & c1);
-        double mup = s_mu[0][c0] * s_mu[1][c1];
-        int np = s_n[0][c0] + s_n[1][c1];
-        double wll = ldexp(mup, np - Gll);
-        double w = wll * P.pit[k][nsh];
+        const int nsh = __popc(c0 & c1);
+        double pitv = pit[0], priv = pri[0];
+#pragma unroll
+        for (int j = 1; j <= KM; j++)
+            if (nsh == j) { pitv = pit[j]; priv = pri[j]; }
+        const double mup = s_mu[0][c0] * s_mu[1][c1];
+        const int np = s_n[0][c0] + s_n[1][c1];
+        const double wll = ldexp(mup, np - Gll);
+        const double w = wll * pitv;
         npatv += 1.0;
         tot += w;
         // value = 2^{np} mup 2^{prior log2e}; pit carries 2^{-Ck}, the shift +Ck
-        if (c0 == 0) nc0 += ldexp(mup * P.pit[k][0], np - (Gnc0 - P.Ck[k]));
-        if (c1 == 0) nc1 += ldexp(mup * P.pit[k][0], np - (Gnc1 - P.Ck[k]));
-        smin = fmin(smin, s_f[0][c0] + s_f[1][c1] + P.prior[k][nsh]);
-        for (int j = 0; j < k; j++) {
+        if (c0 == 0) nc0 += ldexp(mup * pit[0], np - (Gnc0 - Ck));
+        if (c1 == 0) nc1 += ldexp(mup * pit[0], np - (Gnc1 - Ck));
+        smin = fmin(smin, s_f[0][c0] + s_f[1][c1] + priv);
+#pragma unroll
+        for (int j = 0; j < KM; j++) {
             if (x[j] & 1) p0[j] += w;
             if (x[j] & 2) p1[j] += w;
             if (x[j] == 3) {
                 sh[j] += w;
                 sl[j] += wll;
-            } else {
+            } else if (x[j]) {
                 ns[j] += ldexp(mup, np - GN[j]);
             }
         }
@@ -229,35 +293,37 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
     nc1 = wave_sum(nc1);
     npatv = wave_sum(npatv);
     smin = wave_min(smin);
-    for (int j = 0; j < k; j++) {
-        p0[j] = wave_sum(p0[j]);
-        p1[j] = wave_sum(p1[j]);
-        sh[j] = wave_sum(sh[j]);
-        sl[j] = wave_sum(sl[j]);
-        ns[j] = wave_sum(ns[j]);
+    double vp0 = 0, vp1 = 0, vsh = 0, vsl = 0, vns = 0;
+#pragma unroll
+    for (int j = 0; j < KM; j++) {
+        if (j < k) {
+            const double a0 = wave_sum(p0[j]), a1 = wave_sum(p1[j]), a2 = wave_sum(sh[j]), a3 = wave_sum(sl[j]),
+                         a4 = wave_sum(ns[j]);
+            if (j == lane) { vp0 = a0; vp1 = a1; vsh = a2; vsl = a3; vns = a4; }
+        }
     }
     if (lane == 0) {
-        SetRec r = psx::set_zero();
-        r.m = GS;
-        r.m0 = Gnc0;
-        r.m1 = Gnc1;
-        r.tot = tot;
-        r.nc0 = nc0;
-        r.nc1 = nc1;
-        r.score = smin;
-        r.npat = npatv;
-        srec[set] = r;
+        SetRec rr = psx::set_zero();
+        rr.m = GS;
+        rr.m0 = Gnc0;
+        rr.m1 = Gnc1;
+        rr.tot = tot;
+        rr.nc0 = nc0;
+        rr.nc1 = nc1;
+        rr.score = smin;
+        rr.npat = npatv;
+        srec[set] = rr;
+        if (score) score[set] = smin;
     }
     if (lane < k && mrec) {
         Acc5 a;
         a.mP = GS;
         a.mS = Gll;
-        a.mN = GN[lane];
+        a.mN = GN[0];
+#pragma unroll
+        for (int j = 1; j < KM; j++)
+            if (j == lane) a.mN = GN[j];
         a.pad = 0;
-        // dynamic index into the per-lane arrays happens once; keep it simple
-        double vp0 = 0, vp1 = 0, vsh = 0, vsl = 0, vns = 0;
-        for (int j = 0; j < k; j++)
-            if (j == lane) { vp0 = p0[j]; vp1 = p1[j]; vsh = sh[j]; vsl = sl[j]; vns = ns[j]; }
         a.post0 = vp0;
         a.post1 = vp1;
         a.shared = vsh;
@@ -458,16 +524,21 @@ struct psx_engine {
     // sweep workspace (tiled kernel)
     psx::SweepPlanCache plans;
     // generic workspace
-    int* dsets = nullptr;
-    size_t cap_sets = 0;
-    int* dforced = nullptr;
-    size_t cap_forced = 0;
+    // sets | forced | CSR of one batch, uploaded with one copy from pinned staging
+    int* dgen = nullptr;
+    size_t cap_gen = 0;
+    int* hstage = nullptr;
+    size_t cap_stage = 0;
+    hipEvent_t stage_ev = nullptr;  // last upload out of hstage (reuse waits on it)
+    bool stage_rec = false;
+    double* dscore = nullptr;       // per-set scores (SSS), read back compactly
+    size_t cap_score = 0;
+    double* hscore = nullptr;
+    size_t cap_hscore = 0;
     SetRec* dsrec = nullptr;
     size_t cap_srec = 0;
     Acc5* dmrec = nullptr;
     size_t cap_mrec = 0;
-    int* dcsr = nullptr;
-    size_t cap_csr = 0;
     // cached generic exhaustive levels (level 1, levels > 3 when small): (k, rank, world)
     struct GenLevel {
         int* d_sets = nullptr;
@@ -508,7 +579,10 @@ psx_engine::~psx_engine() {
     for (int s = 0; s < 2; s++) { hipFree(dG[s]); hipFree(dAd[s]); hipFree(dy[s]); }
     hipFree(dpres); hipFree(dacc);
     if (hstat) hipHostFree(hstat);
-    hipFree(dsets); hipFree(dforced); hipFree(dsrec); hipFree(dmrec); hipFree(dcsr); hipFree(dpass);
+    if (stage_ev) { hipEventSynchronize(stage_ev); hipEventDestroy(stage_ev); }
+    if (hstage) hipHostFree(hstage);
+    if (hscore) hipHostFree(hscore);
+    hipFree(dgen); hipFree(dscore); hipFree(dsrec); hipFree(dmrec); hipFree(dpass);
     psx::sweep_free(plans);
     for (auto& kv : glevels) {
         GenLevel& g = kv.second;
@@ -533,6 +607,19 @@ int ensure(T*& p, size_t& cap, size_t n) {
     p = nullptr;
     size_t nc = std::max(n, cap * 2);
     HIPCHK(hipMalloc(&p, nc * sizeof(T)));
+    cap = nc;
+    return 0;
+}
+
+// pinned host buffer of at least n elements (contents not preserved)
+template <typename T>
+int ensure_host(T*& p, size_t& cap, size_t n) {
+    if (n <= cap) return 0;
+    const size_t nc = std::max(n, cap * 2);
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&p), nc * sizeof(T)));
     cap = nc;
     return 0;
 }
@@ -584,33 +671,41 @@ int eval_generic(psx_engine* e, const std::vector<int>& sets, int stride, size_t
     if (nsets == 0) return 0;
     if (stride > PSX_KMAX) return fail(PSX_ERANGE, "union set larger than PSX_KMAX");
     int rc;
-    if ((rc = ensure(e->dsets, e->cap_sets, nsets * stride))) return rc;
+    std::vector<int> ptr, idx, rows;
+    if (accumulate) build_csr(sets, stride, nsets, e->U, ptr, idx, rows);
+    const size_t n_sets = nsets * stride, n_forced = forced ? nsets * 2 : 0;
+    const size_t n_csr = ptr.size() + idx.size() + rows.size();
+    const size_t total = n_sets + n_forced + n_csr;
+    if ((rc = ensure(e->dgen, e->cap_gen, total))) return rc;
     if ((rc = ensure(e->dsrec, e->cap_srec, nsets))) return rc;
     if ((rc = ensure(e->dmrec, e->cap_mrec, nsets * stride))) return rc;
-    HIPCHK(hipMemcpyAsync(e->dsets, sets.data(), nsets * stride * sizeof(int), hipMemcpyHostToDevice, e->stream));
-    int* dforced = nullptr;
-    if (forced) {
-        if ((rc = ensure(e->dforced, e->cap_forced, nsets * 2))) return rc;
-        HIPCHK(hipMemcpyAsync(e->dforced, forced, nsets * 2 * sizeof(int), hipMemcpyHostToDevice, e->stream));
-        dforced = e->dforced;
+    if (scores && (rc = ensure(e->dscore, e->cap_score, nsets))) return rc;
+    // one upload: the staging buffer is reused once its previous upload is done
+    if (e->stage_rec) HIPCHK(hipEventSynchronize(e->stage_ev));
+    if ((rc = ensure_host(e->hstage, e->cap_stage, total))) return rc;
+    int* h = e->hstage;
+    std::memcpy(h, sets.data(), n_sets * sizeof(int));
+    if (forced) std::memcpy(h + n_sets, forced, n_forced * sizeof(int));
+    int* hc = h + n_sets + n_forced;
+    if (accumulate) {
+        std::memcpy(hc, ptr.data(), ptr.size() * sizeof(int));
+        std::memcpy(hc + ptr.size(), idx.data(), idx.size() * sizeof(int));
+        std::memcpy(hc + ptr.size() + idx.size(), rows.data(), rows.size() * sizeof(int));
     }
+    HIPCHK(hipMemcpyAsync(e->dgen, h, total * sizeof(int), hipMemcpyHostToDevice, e->stream));
+    if (!e->stage_ev) HIPCHK(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(e->stage_ev, e->stream));
+    e->stage_rec = true;
+    const int* dsets = e->dgen;
+    const int* dforced = forced ? e->dgen + n_sets : nullptr;
+    const int* dcsr = e->dgen + n_sets + n_forced;
     if (kernel_ms) HIPCHK(hipEventRecord(e->ev[2], e->stream));
-    hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)nsets), dim3(64), 0, e->stream, e->dp, e->dsets, stride, dforced,
-                       e->dsrec, e->dmrec);
+    hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)nsets), dim3(64), 0, e->stream, e->dp, dsets, stride, dforced,
+                       e->dsrec, e->dmrec, scores ? e->dscore : nullptr);
     HIPCHK(hipGetLastError());
     if (kernel_ms) HIPCHK(hipEventRecord(e->ev[3], e->stream));
     if (accumulate) {
-        std::vector<int> ptr, idx, rows;
-        build_csr(sets, stride, nsets, e->U, ptr, idx, rows);
-        size_t need = ptr.size() + idx.size() + rows.size();
-        if ((rc = ensure(e->dcsr, e->cap_csr, need))) return rc;
-        std::vector<int> packed;
-        packed.reserve(need);
-        packed.insert(packed.end(), ptr.begin(), ptr.end());
-        packed.insert(packed.end(), idx.begin(), idx.end());
-        packed.insert(packed.end(), rows.begin(), rows.end());
-        HIPCHK(hipMemcpyAsync(e->dcsr, packed.data(), need * sizeof(int), hipMemcpyHostToDevice, e->stream));
-        if (psx::launch_merge_members(e->dmrec, e->dcsr, e->dcsr + ptr.size(), e->dcsr + ptr.size() + idx.size(),
+        if (psx::launch_merge_members(e->dmrec, dcsr, dcsr + ptr.size(), dcsr + ptr.size() + idx.size(),
                                       (int)rows.size(), e->dacc, e->stream))
             return fail(PSX_EHIP, psx::sweep_error());
         SetRec none = psx::set_zero();
@@ -618,10 +713,10 @@ int eval_generic(psx_engine* e, const std::vector<int>& sets, int stride, size_t
             return fail(PSX_EHIP, psx::sweep_error());
     }
     if (scores) {
-        std::vector<SetRec> sr(nsets);
-        HIPCHK(hipMemcpyAsync(sr.data(), e->dsrec, nsets * sizeof(SetRec), hipMemcpyDeviceToHost, e->stream));
+        if ((rc = ensure_host(e->hscore, e->cap_hscore, nsets))) return rc;
+        HIPCHK(hipMemcpyAsync(e->hscore, e->dscore, nsets * sizeof(double), hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
-        for (size_t i = 0; i < nsets; i++) scores[i] = e->K + sr[i].score;
+        for (size_t i = 0; i < nsets; i++) scores[i] = e->K + e->hscore[i];
     }
     if (kernel_ms) {
         HIPCHK(hipStreamSynchronize(e->stream));
@@ -764,7 +859,7 @@ int enqueue_generic_level(psx_engine* e, int k) {
     if (g.nsets == 0) return 0;
     HIPCHK(hipEventRecord(g.ev[0], e->stream));
     hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)g.nsets), dim3(64), 0, e->stream, e->dp, g.d_sets, k,
-                       (const int*)nullptr, g.d_srec, g.d_mrec);
+                       (const int*)nullptr, g.d_srec, g.d_mrec, (double*)nullptr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(g.ev[1], e->stream));
     if (psx::launch_merge_members(g.d_mrec, g.d_csr, g.d_csr + g.ptr_len, g.d_csr + g.ptr_len + g.idx_len,
@@ -810,7 +905,7 @@ int enqueue_level1(psx_engine* e, const SetRec& extra) {
     HIPCHK(hipEventRecord(g.ev[0], e->stream));
     if (g.nsets)
         hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)g.nsets), dim3(64), 0, e->stream, e->dp, g.d_sets, 1,
-                           (const int*)nullptr, g.d_srec, e->dacc + g.lo);
+                           (const int*)nullptr, g.d_srec, e->dacc + g.lo, (double*)nullptr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(g.ev[1], e->stream));
     if (psx::launch_merge_sets(g.d_srec, (long)g.nsets, extra, e->dsacc, e->stream, true, e->dflag))

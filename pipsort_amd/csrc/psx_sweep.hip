@@ -84,18 +84,36 @@ __global__ void k_build_skew(const double* __restrict__ G, int ldg, int nblk, do
 // ---------------------------------------------------------------------------
 // Deterministic record merges (shared with the generic evaluator path)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_merge_members(const Acc5* __restrict__ rec, const int* __restrict__ ptr,
-                                                      const int* __restrict__ idx, const int* __restrict__ row_snp,
-                                                      Acc5* __restrict__ acc) {
+// Gathered records (generic evaluator: SSS batches, configs rows, levels >= 4).
+// A row can hold thousands of records (an SSS neighbourhood repeats the current
+// configuration's members in every swap set), so 256 threads fold it and each
+// thread issues MERGE_R index loads, then MERGE_R record loads, before folding:
+// two dependent round trips per MERGE_R * 256 records instead of per 64.
+constexpr int MERGE_R = 8;
+__global__ __launch_bounds__(256) void k_merge_members(const Acc5* __restrict__ rec, const int* __restrict__ ptr,
+                                                       const int* __restrict__ idx, const int* __restrict__ row_snp,
+                                                       Acc5* __restrict__ acc) {
+    __shared__ Acc5 sh[4];
     const int row = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int b = ptr[row], e = ptr[row + 1];
     Acc5 a = acc_zero();
-    for (int i = ptr[row] + lane; i < ptr[row + 1]; i += 64) fold_acc(a, rec[idx[i]]);
+    for (int i0 = b + (int)threadIdx.x; i0 < e; i0 += 256 * MERGE_R) {
+        int ix[MERGE_R];
+#pragma unroll
+        for (int r = 0; r < MERGE_R; r++) ix[r] = i0 + 256 * r < e ? idx[i0 + 256 * r] : -1;
+        Acc5 v[MERGE_R];
+#pragma unroll
+        for (int r = 0; r < MERGE_R; r++) v[r] = ix[r] >= 0 ? rec[ix[r]] : acc_zero();
+#pragma unroll
+        for (int r = 0; r < MERGE_R; r++) fold_acc(a, v[r]);
+    }
     wave_fold_acc(a);
-    if (lane == 0) {
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
         const int u = row_snp[row];
         Acc5 g = acc[u];
-        fold_acc(g, a);
+        for (int w = 0; w < 4; w++) fold_acc(g, sh[w]);
         acc[u] = g;
     }
 }
@@ -126,7 +144,14 @@ __global__ __launch_bounds__(512) void k_merge_sets(const SetRec* __restrict__ r
                                                     SetRec* __restrict__ acc, int init, int* __restrict__ zero_flag) {
     __shared__ SetRec sh[8];
     SetRec a = set_zero();
-    for (long i = threadIdx.x; i < n; i += 512) fold_set(a, rec[i]);
+    // MERGE_R loads in flight per thread before folding them (fold order fixed)
+    for (long i0 = threadIdx.x; i0 < n; i0 += 512 * MERGE_R) {
+        SetRec v[MERGE_R];
+#pragma unroll
+        for (int r = 0; r < MERGE_R; r++) v[r] = i0 + 512 * r < n ? rec[i0 + 512 * r] : set_zero();
+#pragma unroll
+        for (int r = 0; r < MERGE_R; r++) fold_set(a, v[r]);
+    }
     wave_fold_set(a);
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = a;
     __syncthreads();
@@ -142,7 +167,7 @@ __global__ __launch_bounds__(512) void k_merge_sets(const SetRec* __restrict__ r
 int launch_merge_members(const Acc5* rec, const int* ptr, const int* idx, const int* rows, int n_rows, Acc5* acc,
                          hipStream_t st) {
     if (n_rows <= 0) return 0;
-    hipLaunchKernelGGL(k_merge_members, dim3(n_rows), dim3(64), 0, st, rec, ptr, idx, rows, acc);
+    hipLaunchKernelGGL(k_merge_members, dim3(n_rows), dim3(256), 0, st, rec, ptr, idx, rows, acc);
     SWCHK(hipGetLastError());
     return 0;
 }
