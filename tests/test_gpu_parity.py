@@ -208,6 +208,42 @@ def test_exhaustive_c4_generic_levels(gpu):
     assert_parity(pc.accum(), O.postcal(seam))
 
 
+@pytest.mark.parametrize("M0,M1,shared,c", [(10, 9, 5, 6), (12, 12, 6, 5), (14, 8, 8, 6)])
+def test_exhaustive_generic_high_levels_mixed(gpu, M0, M1, shared, c):
+    """Levels 4..6 run through the generic evaluator (k_eval_sets, up to
+    PSX_KMAX = 6 members and 3^6 assignments) on loci where members are
+    absent from one study (no mask bit, postcal.cpp:930-942)."""
+    ld, z, _, _, u2l = synth.mixed_locus(M0, M1, shared, seed=M0 + M1)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=c, sharing_param=0.25)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    a = pc.accum()
+    assert a.n_configs == seam.count_configs()
+    assert_parity(a, O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-9)
+
+
+def test_union_batch_heavy_rows(gpu):
+    """An SSS neighbourhood repeats the current members in thousands of sets:
+    SNP 0 below sits in 3,160 sets (several 256 x 8 rounds of the member
+    merge).  One batch must fold to the same accumulators as the same sets fed
+    in chunks of 50 (different fold trees: equal to rounding), and its scores
+    must not depend on the batching at all."""
+    ld, z, _, _, u2l = synth.syn_v1(120)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    sets = np.array([[0, a, b] for a in range(1, 81) for b in range(a + 1, 81)], dtype=np.int32)
+    one, many = E.PostCal(seam), E.PostCal(seam)
+    s1 = one.eval_union_batch(sets, accumulate=True)
+    s2 = np.concatenate([many.eval_union_batch(sets[i:i + 50], accumulate=True) for i in range(0, len(sets), 50)])
+    assert np.array_equal(s1, s2)
+    a, b = one.accum(), many.accum()
+    assert a.n_configs == b.n_configs == 27 * len(sets)
+    for x, y in ((a.post, b.post), (a.shared, b.shared), (a.shared_ll, b.shared_ll),
+                 (a.notshared_ll, b.notshared_ll), (a.no_causal, b.no_causal)):
+        assert np.array_equal(x == 0, y == 0)
+        np.testing.assert_allclose(x, y, rtol=1e-12, atol=0)
+    assert abs(a.total - b.total) <= 1e-12 * abs(a.total)
+
+
 def test_deterministic_and_reusable(gpu):
     ld, z, _, _, u2l = synth.syn_v1(300)
     seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
