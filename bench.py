@@ -239,6 +239,13 @@ def load_pmc(workload):
 
 
 def main():
+    # the bench line must be the only thing on stdout: native libraries print
+    # banners there (RCCL prints its version block at communicator init), so
+    # fd 1 is pointed at stderr for the whole run and the line is written to a
+    # saved copy of the original stdout
+    sys.stdout.flush()
+    line_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -256,9 +263,13 @@ def main():
     # PSX_DIST_BACKEND=gloo lets a multi-rank run share one GPU for validation
     # (host-staged exchange); the real path is nccl = RCCL over xGMI.
     backend = os.environ.get("PSX_DIST_BACKEND", "nccl")
+    # PSX_FORCE_DIST=1 takes the multi-rank code path even at world 1 (under
+    # torch.distributed.run): the RCCL calls of the exchange then run on a
+    # one-GPU box, as a check of the N > 1 path (not a bench line)
+    use_dist = world > 1 or bool(os.environ.get("PSX_FORCE_DIST"))
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    if world > 1:
+    if use_dist:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -289,7 +300,7 @@ def main():
             pc.run_exhaustive_async()
         else:
             pc.run_exhaustive()
-        if world > 1:
+        if use_dist:
             pc.export_partials(mine.data_ptr())  # enqueued on torch's current stream
             if backend == "nccl":
                 dist.all_gather_into_tensor(gathered, mine)  # the one exchange step (RCCL over xGMI)
@@ -305,7 +316,7 @@ def main():
             step()
         torch.cuda.synchronize()
         pc.sync()
-        if world > 1:
+        if use_dist:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -316,7 +327,7 @@ def main():
                 kms += t["kernel_ms"]
                 launches += t["kernel_launches"]
         torch.cuda.synchronize()
-        if world > 1:
+        if use_dist:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         exact = pc.sync()  # EXACT flag of any pass (OR-ed over ranks by the merge)
@@ -332,7 +343,7 @@ def main():
         print("bench: EXACT rerun needed, timing the synchronous path", file=sys.stderr)
         use_async = False
         elapsed, kms, launches, _ = timed()
-    if world > 1:
+    if use_dist:
         x = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         elapsed = float(x.item())
@@ -341,7 +352,7 @@ def main():
     acc = pc.accum() if (world == 1 or rank == 0) else None
 
     sss_line = None
-    if world > 1:  # after the timed region; a failure here must not lose the bench line
+    if use_dist:  # after the timed region; a failure here must not lose the bench line
         try:
             sss_line = sss_probe_sharded(rank, world, backend)
         except Exception as ex:  # noqa: BLE001
@@ -382,7 +393,7 @@ def main():
             "config": {"workload": WORKLOADS[args.workload][4], "union_snps": seam.n_union,
                        "max_causal": int(seam.max_causal), "configs_per_step": configs_per_step,
                        "parallelism": (f"config-shard x{world} + 1 {'RCCL' if backend == 'nccl' else backend} all-gather"
-                            if world > 1 else "single GPU")},
+                            if use_dist else "single GPU")},
             "roofline": roofline,
             "fp64": fp64,
             "setup_s": setup_s,
@@ -391,9 +402,9 @@ def main():
             "pass_mode": "async (no host sync per step)" if use_async else "synchronous",
             "configs_checked": int(acc.n_configs) if acc is not None else None,
         }
-        if world > 1:
+        if use_dist:
             out["sss"] = sss_line
-        if world == 1:
+        else:
             out["sss"] = sss_probe()
             w, same = example_wall()
             out["example_wall_s"] = w
@@ -401,9 +412,10 @@ def main():
             if not args.no_cpu_baseline:
                 # the reference's N x N likelihood needs B and S': host eigen route
                 out["cpu_baseline"] = cpu_baseline(build_seam(args.workload), budget_s=args.cpu_budget)
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(line_fd, (json.dumps(out) + "\n").encode())
     pc.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

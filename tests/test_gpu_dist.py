@@ -29,12 +29,33 @@ def test_bench_sharded_two_ranks(gpu, world):
            "--gpus", str(world), "--steps", "2", "--warmup", "1", "--workload", "syn200c2", "--no-cpu-baseline"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]  # the bench line alone on stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == world
     # every rank's shard folded into rank 0's accumulators: all configurations counted once
     assert out["configs_checked"] == out["config"]["configs_per_step"] == 179_701
     # the SSS walk with its batches split across the ranks (psx_run_sss_sharded):
     # the same walk and configuration count as one GPU (bench sss line, r01x)
+    assert out["sss"]["walk_iterations"] == 2 and out["sss"]["walk_configs"] == 23_993
+
+
+def test_bench_rccl_path_world1(gpu):
+    """The N > 1 code path with the nccl (= RCCL) backend, on the one GPU of a
+    test box (PSX_FORCE_DIST=1 at world 1): RCCL communicator, all-gather of
+    the partial images on the engine stream, barrier / max-over-ranks timing,
+    sharded SSS walk.  RCCL prints a version banner at init; stdout must still
+    hold the bench line alone."""
+    env = dict(os.environ, PSX_FORCE_DIST="1")
+    env.pop("PSX_DIST_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--steps", "3", "--warmup", "1", "--workload", "syn200c2", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert "RCCL" in out["config"]["parallelism"]
+    assert out["configs_checked"] == out["config"]["configs_per_step"] == 179_701
     assert out["sss"]["walk_iterations"] == 2 and out["sss"]["walk_configs"] == 23_993
