@@ -222,6 +222,32 @@ def test_exhaustive_generic_high_levels_mixed(gpu, M0, M1, shared, c):
     assert_parity(a, O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-9)
 
 
+TINY = [(1, 1, 1, 3), (2, 1, 1, 3), (3, 3, 0, 3), (2, 2, 2, 2), (4, 3, 2, 3), (5, 4, 3, 1), (3, 2, 1, 6)]
+
+
+@pytest.mark.parametrize("M0,M1,shared,c", TINY)
+def test_tiny_loci_edges(gpu, M0, M1, shared, c):
+    """Degenerate loci: one or two union SNPs under c = 3 (c > U: the tiled
+    sweep does not apply), no SNP shared by the studies, c = 1, c = 6 over four
+    SNPs.  Exhaustive (synchronous and asynchronous passes) and SSS against the
+    oracle."""
+    ld, z, _, _, u2l = synth.mixed_locus(M0, M1, shared, seed=M0 + M1)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=c, sharing_param=0.25)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    a = pc.accum()
+    assert a.n_configs == seam.count_configs()
+    assert_parity(a, O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-9)
+    pc.run_exhaustive_async()
+    pc.sync()
+    b = pc.accum()
+    for x, y in ((a.post, b.post), (a.shared_ll, b.shared_ll), (a.notshared_ll, b.notshared_ll)):
+        assert np.array_equal(x, y)
+    assert a.total == b.total
+    pc.run_sss()
+    assert_parity(pc.accum(), O.postcal(seam, "sss"), ll_rtol=1e-11)
+
+
 def test_union_batch_heavy_rows(gpu):
     """An SSS neighbourhood repeats the current members in thousands of sets:
     SNP 0 below sits in 3,160 sets (several 256 x 8 rounds of the member
