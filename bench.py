@@ -207,6 +207,28 @@ def sss_probe_sharded(rank, world, backend):
                          "(psx_run_sss_sharded) + one accumulator exchange"}
 
 
+def pcie_inclusive(mi, configs, device, reps=3):
+    """Whole-locus rate from host buffers to host results: the GPU Model setup
+    from the host LD / z arrays (H2D included), one synchronous exhaustive
+    pass, and the accumulators read back to the host (psx_get_accum, D2H).
+    Not the bench value (inputs are not resident): reported beside it."""
+    best = None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pc = E.PostCal(mi, device=device)
+        pc.run_exhaustive()
+        pc.accum()
+        dt = time.perf_counter() - t0
+        setup_ms = pc.setup_info["setup_ms"]
+        pc.close()
+        if best is None or dt < best[0]:
+            best = (dt, setup_ms)
+    return {"value": configs / best[0], "unit": "configs/s", "s": best[0], "setup_ms": best[1],
+            "note": "host LD/z -> GPU Model setup (H2D) -> one synchronous pass -> accumulators on the host "
+                    "(D2H); best of %d" % reps}
+
+
 def example_wall():
     """Wall-clock of the drop-in PIPSORT CLI on tests/example (-c 2 -p 0.25)."""
     import loci
@@ -405,6 +427,7 @@ def main():
         if use_dist:
             out["sss"] = sss_line
         else:
+            out["pcie_inclusive"] = pcie_inclusive(seam, configs_per_step, local)
             out["sss"] = sss_probe()
             w, same = example_wall()
             out["example_wall_s"] = w

@@ -15,6 +15,7 @@ struct LdStudyResult {
     int sigma_host_needed;    // path 1: the caller rebuilds Sigma' = LD + added I on the host
     double min_pivot_ratio;   // min L D L^T pivot / max |diag|
     double spsq;              // path 0: ||S'_s||^2 = z^T Sigma'^-1 z
+    int fused_route;          // 1: swap-free LU of a symmetric LD carried step 2 (one elimination)
 };
 
 // Partial-pivot LU determinant of the device matrix dA (n x n row-major,

@@ -125,6 +125,90 @@ __global__ __launch_bounds__(kElimCols) void k_elim(double* __restrict__ A, int 
     }
 }
 
+// Fused step j of the partial-pivot elimination for matrices that need no row
+// swap (LD matrices: the diagonal stays the column maximum).  Column j sits
+// contiguous in col[j & 1] (written by step j - 1's owners of column j), so
+// every block reduces it to GSL's pivot (first row of maximal |a_ij|, NaNs never
+// chosen; the same decision k_lu_pivot makes).  If that pivot is row j the
+// block eliminates exactly as k_elim (same operations, same rounding) and the
+// owners of column j + 1 publish its new entries to col[(j + 1) & 1]; else the
+// step raises *flag and this and every later step do nothing (the caller then
+// reruns the pivoting path from a fresh copy).  One launch per column instead
+// of a pivot launch plus an update launch.
+__global__ __launch_bounds__(kElimCols) void k_lu_step(double* __restrict__ A, int n, int j,
+                                                       double* __restrict__ col, int* __restrict__ flag,
+                                                       double* __restrict__ z) {
+#pragma clang fp contract(off)
+    __shared__ double sv[kElimCols];
+    __shared__ int si[kElimCols];
+    __shared__ double sl[kElimRows];
+    if (*flag) return;
+    const int t = threadIdx.x;
+    const double* cj = col + (size_t)(j & 1) * n;
+    double mx = -1.0;
+    int ip = n;
+    for (int i = j + t; i < n; i += kElimCols) {
+        const double v = fabs(cj[i]);
+        if (v > mx) { mx = v; ip = i; }
+    }
+    sv[t] = mx;
+    si[t] = ip;
+    __syncthreads();
+    for (int w = kElimCols / 2; w > 0; w >>= 1) {
+        if (t < w) {
+            const double v2 = sv[t + w];
+            const int i2 = si[t + w];
+            if (v2 > sv[t] || (v2 == sv[t] && i2 < si[t])) { sv[t] = v2; si[t] = i2; }
+        }
+        __syncthreads();
+    }
+    const double ajj = cj[j];
+    const int p = (ajj != ajj || si[0] >= n) ? j : si[0];
+    if (p != j) {
+        if (t == 0) *flag = 1;
+        return;
+    }
+    const int i0 = j + 1 + blockIdx.y * kElimRows;
+    const int nr = min(kElimRows, n - i0);
+    const int k = j + 1 + blockIdx.x * kElimCols + t;
+    double* cn = col + (size_t)((j + 1) & 1) * n;
+    if (ajj == 0.0) {  // GSL skips the column: column j + 1 is published unchanged
+        if (k == j + 1)
+            for (int r = 0; r < nr; r++) cn[i0 + r] = A[(size_t)(i0 + r) * n + k];
+        return;
+    }
+    if (t < nr) sl[t] = A[(size_t)(i0 + t) * n + j] / ajj;
+    __syncthreads();
+    if (z && blockIdx.x == 0 && t < nr) {
+        const double zj = z[j];
+        z[i0 + t] = z[i0 + t] - sl[t] * zj;
+    }
+    if (k >= n) return;
+    const double ujk = A[(size_t)j * n + k];
+    for (int r = 0; r < nr; r++) {
+        double* q = A + (size_t)(i0 + r) * n + k;
+        const double prod = sl[r] * ujk;
+        const double v = *q - prod;
+        *q = v;
+        if (k == j + 1) cn[i0 + r] = v;
+    }
+}
+
+// *asym = 1 when L is not exactly symmetric (any L_ik != L_ki, NaNs included)
+__global__ void k_sym_check(const double* __restrict__ L, int n, int* __restrict__ asym) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)n * n) return;
+    const int i = (int)(idx / n), k = (int)(idx % n);
+    if (k > i && !(L[idx] == L[(size_t)k * n + i])) *asym = 1;
+}
+
+// col[0][i] = A[i][0]: column 0 for the first fused step; flag re-armed
+__global__ void k_lu_begin(const double* __restrict__ A, int n, double* __restrict__ col, int* __restrict__ flag) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) col[i] = A[(size_t)i * n];
+    if (i == 0) *flag = 0;
+}
+
 __global__ void k_get_diag(const double* __restrict__ A, int n, double* __restrict__ d) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) d[i] = A[(size_t)i * n + i];
@@ -143,6 +227,18 @@ int enqueue_lu(double* A, int n, int* dswp, hipStream_t st) {
         const int r = n - j - 1;
         hipLaunchKernelGGL(k_elim, dim3((r + kElimCols - 1) / kElimCols, (r + kElimRows - 1) / kElimRows),
                            dim3(kElimCols), 0, st, A, n, j, (double*)nullptr);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// enqueue the fused (swap-free) elimination; *flag != 0 afterwards when some
+// column needed a row swap (A is then partly eliminated: recopy and pivot)
+int enqueue_lu_fused(double* A, int n, double* col, int* flag, double* z, hipStream_t st) {
+    hipLaunchKernelGGL(k_lu_begin, dim3((n + 255) / 256), dim3(256), 0, st, A, n, col, flag);
+    for (int j = 0; j < n - 1; j++) {
+        const int r = n - j - 1;
+        hipLaunchKernelGGL(k_lu_step, dim3((r + kElimCols - 1) / kElimCols, (r + kElimRows - 1) / kElimRows),
+                           dim3(kElimCols), 0, st, A, n, j, col, flag, z);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -173,29 +269,61 @@ int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, dou
                    LdStudyResult* res, std::string* err) {
     std::memset(res, 0, sizeof(*res));
     const size_t nn = (size_t)M * M;
-    double *dL = nullptr, *dA = nullptr, *dz = nullptr, *ddiag = nullptr;
+    double *dL = nullptr, *dA = nullptr, *dz = nullptr, *ddiag = nullptr, *dcol = nullptr;
     int* dswp = nullptr;
-    auto cleanup = [&]() { hipFree(dL); hipFree(dA); hipFree(dz); hipFree(ddiag); hipFree(dswp); };
+    auto cleanup = [&]() { hipFree(dL); hipFree(dA); hipFree(dz); hipFree(ddiag); hipFree(dcol); hipFree(dswp); };
     if (hipMalloc(&dL, nn * sizeof(double)) != hipSuccess || hipMalloc(&dA, nn * sizeof(double)) != hipSuccess ||
         hipMalloc(&dz, M * sizeof(double)) != hipSuccess || hipMalloc(&ddiag, M * sizeof(double)) != hipSuccess ||
-        hipMalloc(&dswp, std::max(M, 1) * sizeof(int)) != hipSuccess) {
+        hipMalloc(&dcol, 2 * (size_t)M * sizeof(double)) != hipSuccess ||
+        hipMalloc(&dswp, (std::max(M, 1) + 2) * sizeof(int)) != hipSuccess) {
         cleanup();
         if (err) *err = "out of device memory (LD setup)";
         return -1;
     }
+    int* const dflag = dswp + std::max(M, 1);
+    // an exactly symmetric LD whose elimination needs no row swap gives step 2's
+    // unpivoted elimination of Sigma' bit for bit (same matrix, same operations):
+    // z's forward solve then rides in step 1 and step 2 is not run again
+    int* const dasym = dflag + 1;
+    int hasym = 1;
     const int cb = 256;
     const unsigned gb = (unsigned)((nn + cb - 1) / cb);
     int rc = 0;
     do {
         if ((rc = chk(hipMemcpyAsync(dL, ld, nn * sizeof(double), hipMemcpyHostToDevice, st), "LD upload", err))) break;
+        if ((rc = chk(hipMemsetAsync(dasym, 0, sizeof(int), st), "memset", err))) break;
+        hipLaunchKernelGGL(k_sym_check, dim3(gb), dim3(cb), 0, st, dL, M, dasym);
+        if ((rc = chk(hipMemcpyAsync(&hasym, dasym, sizeof(int), hipMemcpyDeviceToHost, st), "copy", err))) break;
         // 1. util.cpp:195-226: add 0.01 until det(LU) > 0
         double add = 0.0;
         int it = 0;
+        bool fused = false;  // the last LU ran swap-free with z's forward solve
+        std::vector<double> udiag(M);
         for (;; it++) {
             if (it >= 100000) { rc = -1; if (err) *err = "PSD shift did not terminate"; break; }
             hipLaunchKernelGGL(k_psd_copy, dim3(gb), dim3(cb), 0, st, dL, M, add, dA);
+            if ((rc = chk(hipMemcpyAsync(dz, z, M * sizeof(double), hipMemcpyHostToDevice, st), "z upload", err)))
+                break;
+            if (enqueue_lu_fused(dA, M, dcol, dflag, dz, st)) { rc = chk(hipGetLastError(), "LU launch", err); break; }
+            hipLaunchKernelGGL(k_get_diag, dim3((M + 255) / 256), dim3(256), 0, st, dA, M, ddiag);
+            int hflag = 0;
+            if ((rc = chk(hipMemcpyAsync(udiag.data(), ddiag, M * sizeof(double), hipMemcpyDeviceToHost, st), "copy",
+                          err)) ||
+                (rc = chk(hipMemcpyAsync(&hflag, dflag, sizeof(int), hipMemcpyDeviceToHost, st), "copy", err)) ||
+                (rc = chk(hipStreamSynchronize(st), "LU sync", err)))
+                break;
             double det = 0;
-            if ((rc = lu_det_device(dA, M, dswp, ddiag, st, &det, err))) break;
+            if (!hflag) {
+                // gsl_linalg_LU_det with signum +1: the U_ii multiplied in index order
+                det = 1.0;
+                for (int i = 0; i < M; i++) det *= udiag[i];
+                fused = true;
+            } else {
+                // a row swap is needed: the pivoting elimination from a fresh copy
+                hipLaunchKernelGGL(k_psd_copy, dim3(gb), dim3(cb), 0, st, dL, M, add, dA);
+                if ((rc = lu_det_device(dA, M, dswp, ddiag, st, &det, err))) break;
+                fused = false;
+            }
             if (det > 0) break;
             add += 0.01;
         }
@@ -205,21 +333,32 @@ int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, dou
         // 2. Sigma' (lower triangle, symmetrised) -> dS; elimination without pivoting
         //    of a copy with z's forward solve: pivots D, z~ = L^-1 z
         hipLaunchKernelGGL(k_sym_lower, dim3(gb), dim3(cb), 0, st, dL, M, add, dS);
-        if ((rc = chk(hipMemcpyAsync(dA, dS, nn * sizeof(double), hipMemcpyDeviceToDevice, st), "copy", err))) break;
-        if ((rc = chk(hipMemcpyAsync(dz, z, M * sizeof(double), hipMemcpyHostToDevice, st), "z upload", err))) break;
-        for (int j = 0; j < M - 1; j++) {
-            const int r = M - j - 1;
-            hipLaunchKernelGGL(k_elim, dim3((r + kElimCols - 1) / kElimCols, (r + kElimRows - 1) / kElimRows),
-                               dim3(kElimCols), 0, st, dA, M, j, dz);
-        }
-        hipLaunchKernelGGL(k_get_diag, dim3((M + 255) / 256), dim3(256), 0, st, dA, M, ddiag);
-        if ((rc = chk(hipGetLastError(), "elimination launch", err))) break;
         std::vector<double> piv(M), zt(M), dg(M);
-        hipMemcpyAsync(piv.data(), ddiag, M * sizeof(double), hipMemcpyDeviceToHost, st);
-        hipMemcpyAsync(zt.data(), dz, M * sizeof(double), hipMemcpyDeviceToHost, st);
-        hipLaunchKernelGGL(k_get_diag, dim3((M + 255) / 256), dim3(256), 0, st, dS, M, ddiag);
-        hipMemcpyAsync(dg.data(), ddiag, M * sizeof(double), hipMemcpyDeviceToHost, st);
+        const bool sym = hasym == 0;  // read back with the first LU sync
+        if (fused && sym) {
+            piv = udiag;
+            if ((rc = chk(hipMemcpyAsync(zt.data(), dz, M * sizeof(double), hipMemcpyDeviceToHost, st), "copy", err)))
+                break;
+            for (int i = 0; i < M; i++) dg[i] = ld[(size_t)i * M + i] + add;  // k_sym_lower's diagonal
+        } else {
+            if ((rc = chk(hipMemcpyAsync(dA, dS, nn * sizeof(double), hipMemcpyDeviceToDevice, st), "copy", err)))
+                break;
+            if ((rc = chk(hipMemcpyAsync(dz, z, M * sizeof(double), hipMemcpyHostToDevice, st), "z upload", err)))
+                break;
+            for (int j = 0; j < M - 1; j++) {
+                const int r = M - j - 1;
+                hipLaunchKernelGGL(k_elim, dim3((r + kElimCols - 1) / kElimCols, (r + kElimRows - 1) / kElimRows),
+                                   dim3(kElimCols), 0, st, dA, M, j, dz);
+            }
+            hipLaunchKernelGGL(k_get_diag, dim3((M + 255) / 256), dim3(256), 0, st, dA, M, ddiag);
+            if ((rc = chk(hipGetLastError(), "elimination launch", err))) break;
+            hipMemcpyAsync(piv.data(), ddiag, M * sizeof(double), hipMemcpyDeviceToHost, st);
+            hipMemcpyAsync(zt.data(), dz, M * sizeof(double), hipMemcpyDeviceToHost, st);
+            hipLaunchKernelGGL(k_get_diag, dim3((M + 255) / 256), dim3(256), 0, st, dS, M, ddiag);
+            hipMemcpyAsync(dg.data(), ddiag, M * sizeof(double), hipMemcpyDeviceToHost, st);
+        }
         if ((rc = chk(hipStreamSynchronize(st), "elimination sync", err))) break;
+        res->fused_route = (fused && sym) ? 1 : 0;
         double dmax = 0, pmin = INFINITY;
         for (int i = 0; i < M; i++) {
             dmax = std::max(dmax, std::fabs(dg[i]));

@@ -110,6 +110,37 @@ def test_ld_route_syn1000(gpu):
     assert_parity(got, ref.__dict__, pip_tol=1e-9, ll_rtol=1e-9)
 
 
+def test_ld_route_fused_lu_shift_loop_and_asymmetric(gpu):
+    """The swap-free fused elimination (one launch per column, z's forward
+    solve riding along, step 2 skipped for an exactly symmetric LD):
+    * study 0: AR(1) rho = 0.95, M = 400, whose determinant underflows to 0,
+      so util.cpp:195-226 adds 0.01 several times; the shift must equal the
+      host restatement of GSL's elimination exactly;
+    * study 1: a symmetric LD with one upper entry moved by one ulp (not
+      exactly symmetric: step 2 runs on the lower triangle, as the reference's
+      eigensolver reads it).
+    PIPs against the host eigen route."""
+    M = 400
+    idx = np.arange(M)
+    ar = 0.95 ** np.abs(idx[:, None] - idx[None, :])
+    assert E.lu_det(ar) == 0.0  # the loop must iterate
+    ld1 = 0.5 ** np.abs(idx[:, None] - idx[None, :])
+    ld1[3, 17] = np.nextafter(ld1[3, 17], 1.0)
+    rng = np.random.default_rng(9)
+    z = [rng.standard_normal(M) * 1.5, rng.standard_normal(M) * 1.5]
+    z[0][M // 2] = 5.0
+    z[1][M // 2] = 4.0
+    u2l = np.stack([idx, idx]).astype(np.int32)
+    seam, mi = _both([ar, ld1], z, u2l, (6000, 7000), max_causal=2, sharing_param=0.25)
+    pc, got = _run(mi)
+    info = pc.setup_info
+    assert info["eigen_route"] == [0, 0]
+    assert info["psd_added"][0] == E.psd_shift(ar)[1] > 0
+    assert info["psd_added"][1] == E.psd_shift(ld1)[1]
+    _, ref = _run(seam)
+    assert_parity(got, ref.__dict__, pip_tol=1e-9, ll_rtol=1e-9)
+
+
 def test_indefinite_sigma_takes_eigen_route(gpu):
     """det > 0 with two negative eigenvalues: the PSD loop stops at a = 0 and the
     reference's |W| differs from Sigma'; the engine must take the eigen route."""
