@@ -366,10 +366,21 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     for (auto& u : all) wsum += u.work;
     double lo = wsum * rank / world, hi = wsum * (rank + 1) / world, run = 0;
     mine.clear();
-    for (auto& u : all) {
-        double mid = run + 0.5 * u.work;
-        if (mid >= lo && mid < hi) mine.push_back(u);
-        run += u.work;
+    // Contiguous work bands in enumeration order (C, K, a).  PSX_K3_DEAL=1 deals
+    // the units cyclically instead (every shard the same mix of tiles and unit
+    // kinds).  Measured on two boxes (world-8 rehearsal, 3 alternating reps
+    // each): dealing 4 % faster on one, 5 % slower on the other — the per-rank
+    // pattern is box-dependent, so the bands stay.
+    static const bool deal = std::getenv("PSX_K3_DEAL") != nullptr;
+    if (deal) {
+        for (size_t i = 0; i < all.size(); i++)
+            if ((int)(i % (size_t)world) == rank) mine.push_back(all[i]);
+    } else {
+        for (auto& u : all) {
+            double mid = run + 0.5 * u.work;
+            if (mid >= lo && mid < hi) mine.push_back(u);
+            run += u.work;
+        }
     }
     double bytes_cls[4][4][4];
     for (int x = 1; x < 4; x++)

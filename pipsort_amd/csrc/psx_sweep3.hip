@@ -554,11 +554,11 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
         Acc5 ra = lacc_rec(accA, A.Ck, A.pit0);
         wave_fold_acc(ra);
         const int qa = sPos[2][ai];
-        if (t == 0 && qa >= 0) rec[qa] = ra;
+        if (t == 0 && qa >= 0) store_rec(rec + qa, ra);
         if (A.trace && ai == 0) t_ph[3] = wall_clock64();
     }
     __syncthreads();
-    if (sPos[0][t] >= 0) rec[sPos[0][t]] = lacc_rec(accC, A.Ck, A.pit0);
+    if (sPos[0][t] >= 0) store_rec(rec + sPos[0][t], lacc_rec(accC, A.Ck, A.pit0));
     {
         LAcc sl;
         sl.m = sM[t];
@@ -567,7 +567,7 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
         sl.sh = sSh[t];
         sl.sl = sSl[t];
         sl.ns = sNs[t];
-        if (sPos[1][t] >= 0) rec[sPos[1][t]] = lacc_rec(sl, A.Ck, A.pit0);
+        if (sPos[1][t] >= 0) store_rec(rec + sPos[1][t], lacc_rec(sl, A.Ck, A.pit0));
     }
     SetRec sr;
     sr.tot = totC * A.pit0;
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
     sr.score = 1e300;
     sr.npat = npat;
     wave_fold_set(sr);
-    if (t == 0) srec[unit] = sr;
+    if (t == 0) store_rec(srec + unit, sr);
     if (A.trace && t == 0) {
         unsigned hw, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));

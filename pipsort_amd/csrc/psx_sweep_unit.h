@@ -288,7 +288,7 @@ __device__ __forceinline__ void sweep_unit(const TileArgs& A, int unit, const in
     put_rec(rec, pos, (size_t)unit * rec_stride + t, slot[t]);
     put_rec(rec, pos, (size_t)unit * rec_stride + 64 + t, sacc[1][t]);
     wave_fold_set(accs);
-    if (t == 0) srec[unit] = accs;
+    if (t == 0) store_rec(srec + unit, accs);
 }
 
 }  // namespace psx
