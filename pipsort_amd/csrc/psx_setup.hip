@@ -297,30 +297,35 @@ int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, dou
         // 1. util.cpp:195-226: add 0.01 until det(LU) > 0
         double add = 0.0;
         int it = 0;
-        bool fused = false;  // the last LU ran swap-free with z's forward solve
+        bool fused = false;      // the last LU ran swap-free with z's forward solve
+        bool try_fused = true;   // until some shift of this LD needed a row swap
         std::vector<double> udiag(M);
         for (;; it++) {
             if (it >= 100000) { rc = -1; if (err) *err = "PSD shift did not terminate"; break; }
             hipLaunchKernelGGL(k_psd_copy, dim3(gb), dim3(cb), 0, st, dL, M, add, dA);
-            if ((rc = chk(hipMemcpyAsync(dz, z, M * sizeof(double), hipMemcpyHostToDevice, st), "z upload", err)))
-                break;
-            if (enqueue_lu_fused(dA, M, dcol, dflag, dz, st)) { rc = chk(hipGetLastError(), "LU launch", err); break; }
-            hipLaunchKernelGGL(k_get_diag, dim3((M + 255) / 256), dim3(256), 0, st, dA, M, ddiag);
-            int hflag = 0;
-            if ((rc = chk(hipMemcpyAsync(udiag.data(), ddiag, M * sizeof(double), hipMemcpyDeviceToHost, st), "copy",
-                          err)) ||
-                (rc = chk(hipMemcpyAsync(&hflag, dflag, sizeof(int), hipMemcpyDeviceToHost, st), "copy", err)) ||
-                (rc = chk(hipStreamSynchronize(st), "LU sync", err)))
-                break;
             double det = 0;
+            int hflag = 1;
+            if (try_fused) {
+                if ((rc = chk(hipMemcpyAsync(dz, z, M * sizeof(double), hipMemcpyHostToDevice, st), "z upload", err)))
+                    break;
+                if (enqueue_lu_fused(dA, M, dcol, dflag, dz, st)) { rc = chk(hipGetLastError(), "LU launch", err); break; }
+                hipLaunchKernelGGL(k_get_diag, dim3((M + 255) / 256), dim3(256), 0, st, dA, M, ddiag);
+                if ((rc = chk(hipMemcpyAsync(udiag.data(), ddiag, M * sizeof(double), hipMemcpyDeviceToHost, st),
+                              "copy", err)) ||
+                    (rc = chk(hipMemcpyAsync(&hflag, dflag, sizeof(int), hipMemcpyDeviceToHost, st), "copy", err)) ||
+                    (rc = chk(hipStreamSynchronize(st), "LU sync", err)))
+                    break;
+                if (hflag) {  // a row swap is needed: the pivoting elimination from a fresh copy
+                    try_fused = false;
+                    hipLaunchKernelGGL(k_psd_copy, dim3(gb), dim3(cb), 0, st, dL, M, add, dA);
+                }
+            }
             if (!hflag) {
                 // gsl_linalg_LU_det with signum +1: the U_ii multiplied in index order
                 det = 1.0;
                 for (int i = 0; i < M; i++) det *= udiag[i];
                 fused = true;
             } else {
-                // a row swap is needed: the pivoting elimination from a fresh copy
-                hipLaunchKernelGGL(k_psd_copy, dim3(gb), dim3(cb), 0, st, dL, M, add, dA);
                 if ((rc = lu_det_device(dA, M, dswp, ddiag, st, &det, err))) break;
                 fused = false;
             }
