@@ -83,6 +83,12 @@ const char *psx_last_error(void);
 /* Number of HIP devices visible (0 on a host without a GPU; never initialises a context). */
 int psx_device_count(int *count);
 
+/* Optional (no reference counterpart): bring up the HIP runtime and context of
+ * `device` and load the engine's device code, so the first psx_create* does not
+ * pay for it.  Thread-safe; the drop-in CLI calls it on a second thread while
+ * it parses the LD / z files (model.h:86-144), overlapping the two. */
+int psx_warmup(int device);
+
 /* PostCal::PostCal (postcal.h:118-195).  Copies the problem to device `device`,
  * forms Sigma~_s = B_s^T B_s, y_s = B_s^T S'_s and ||S'||^2 on the GPU. */
 int psx_create(const psx_problem *prob, int device, psx_engine **out);

@@ -250,20 +250,29 @@ int main(int argc, char* argv[]) {
         exit(1);
     }
     auto t_setup0 = std::chrono::steady_clock::now();
+    int device = 0;
+    if (const char* d = getenv("PSX_DEVICE")) device = atoi(d);
+    // the HIP runtime / context comes up on a second thread while the inputs
+    // are parsed (errors, if any, surface again at psx_create*)
+    std::thread warm([device] { psx_warmup(device); });
+    auto quit = [&warm](int code) {  // input errors below exit as the reference does, after the warm-up
+        warm.join();
+        exit(code);
+    };
     // ---- Model (model.h:86-264) ----
     vector<vector<double>> sig(S), zs(S);
     vector<vector<string>> names(S);
     vector<int> m(S);
     for (int i = 0; i < S; i++) {
         vector<double> L;
-        if (!import_data(ldDir[i], L)) exit(1);
+        if (!import_data(ldDir[i], L)) quit(1);
         import_z(zDir[i], names[i], zs[i]);
         int M = (int)std::sqrt((double)L.size());  // model.h:98
         m[i] = M;
         if (M != (int)names[i].size()) {
             printf("ERROR: LD matrix is size %d x %d but zscores has %lu snps\n. Check LD file for nans.\n", M, M,
                    (unsigned long)names[i].size());
-            exit(1);
+            quit(1);
         }
         printf("pushing back num snps %d for study %d\n", i, M);
         L.resize((size_t)M * M);
@@ -271,20 +280,19 @@ int main(int argc, char* argv[]) {
     }
     vector<string> all_snp_pos;
     vector<vector<int>> u2l(S);
-    if (!import_snp_map(snpMapFile, S + 1, all_snp_pos, u2l)) exit(1);
+    if (!import_snp_map(snpMapFile, S + 1, all_snp_pos, u2l)) quit(1);
     const int U = (int)all_snp_pos.size();
     for (int i = 0; i < S; i++) {  // model.h:134-144
         int cnt = 0;
-        if ((int)u2l[i].size() != U) { printf("Invariant does not hold\n"); exit(1); }
+        if ((int)u2l[i].size() != U) { printf("Invariant does not hold\n"); quit(1); }
         for (int u = 0; u < U; u++) cnt += u2l[i][u] >= 0;
-        if (cnt != m[i]) { printf("Invariant does not hold\n"); exit(1); }
+        if (cnt != m[i]) { printf("Invariant does not hold\n"); quit(1); }
     }
     const int N = m[0] + m[1];
     vector<int32_t> u2l_flat(2 * U);
     for (int s = 0; s < 2; s++)
         for (int u = 0; u < U; u++) u2l_flat[s * U + u] = u2l[s][u];
-    int device = 0;
-    if (const char* d = getenv("PSX_DEVICE")) device = atoi(d);
+    warm.join();
     psx_engine* eng = nullptr;
     int rc;
     const char* hs = getenv("PSX_HOST_SETUP");

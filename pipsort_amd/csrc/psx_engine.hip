@@ -1338,6 +1338,22 @@ int gpu_ready(int device) {
 }
 }  // namespace
 
+int psx_warmup(int device) {
+    int rc;
+    if ((rc = gpu_ready(device))) return rc;
+    HIPCHK(hipFree(nullptr));  // context
+    // one launch loads the device code
+    double* d = nullptr;
+    HIPCHK(hipMalloc(&d, 64 * sizeof(double)));
+    hipLaunchKernelGGL(k_diag, dim3(1), dim3(64), 0, nullptr, d, 8, d + 8);
+    hipError_t le = hipGetLastError();
+    hipError_t se = hipDeviceSynchronize();
+    hipFree(d);
+    if (le != hipSuccess || se != hipSuccess)
+        return fail(PSX_EHIP, std::string("warm-up: ") + hipGetErrorString(le != hipSuccess ? le : se));
+    return 0;
+}
+
 int psx_lu_det_gpu(const double* a, int32_t m, int device, double* det) {
     if (!a || m <= 0 || !det) return fail(PSX_EINVAL, "bad argument");
     int rc;

@@ -29,7 +29,7 @@ PSX_EEXCHANGE = -7
 
 # Every symbol declared in include/pipsort_engine.h and include/pipsort_model.h
 EXPORTED = [
-    "psx_abi_version", "psx_last_error", "psx_device_count", "psx_create", "psx_destroy",
+    "psx_abi_version", "psx_last_error", "psx_device_count", "psx_warmup", "psx_create", "psx_destroy",
     "psx_set_shard", "psx_run_exhaustive", "psx_run_configs", "psx_run_sss",
     "psx_eval_union_batch", "psx_reset", "psx_get_accum", "psx_partials_bytes",
     "psx_export_partials", "psx_merge_partials", "psx_get_timing", "psx_count_configs",
@@ -144,6 +144,7 @@ def load_library(path: str = LIB_PATH):
         "psx_abi_version": (c_i32, []),
         "psx_last_error": (ctypes.c_char_p, []),
         "psx_device_count": (c_int, [P(c_int)]),
+        "psx_warmup": (c_int, [c_int]),
         "psx_create": (c_int, [P(_Problem), c_int, P(vp)]),
         "psx_destroy": (None, [vp]),
         "psx_set_shard": (c_int, [vp, c_int, c_int]),
