@@ -199,3 +199,16 @@ def test_example_pipeline_end_to_end(gpu, tmp_path):
     # LL columns: race-affected in the reference (postcal.cpp:1012-1017), 1 line may differ
     bad = sum(1 for x, y in zip(g[1:], e[1:]) if x[1:3] != y[1:3])
     assert bad <= 1
+
+
+def test_warmup_entry_point(gpu):
+    """psx_warmup (the CLI overlaps it with input parsing): brings the device up
+    and loads device code; a bad device index is an
+    error, not a crash; the engine works afterwards."""
+    lib = E.load_library()
+    assert lib.psx_warmup(0) == E.PSX_OK
+    assert lib.psx_warmup(E.device_count() + 3) == E.PSX_EINVAL
+    seam, _ = loci.seam_for(loci.SMALL, c=2)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    assert_parity(pc.accum(), O.postcal(seam))
