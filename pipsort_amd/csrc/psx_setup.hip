@@ -10,8 +10,9 @@
 // Q|W|Q^T, z and z^T Q|W|^-1 Q^T z, so whenever Sigma' is positive definite
 // they are exactly Sigma', z and z^T Sigma'^-1 z: no eigendecomposition.
 //
-//  * Step 1 runs here as an unblocked right-looking elimination, one pivot
-//    launch + one update launch per column, with the reference's operation
+//  * Step 1 runs here as a right-looking elimination (swap-free LDs: blocked,
+//    updates delayed by a kPanel-column panel; otherwise one pivot launch + one
+//    update launch per column), with the reference's operation
 //    order and IEEE rounding (division correctly rounded, multiply and
 //    subtract not fused), so the per-element update sequence — and hence
 //    every U_ii and the index-order determinant product — is bit-identical to
@@ -30,6 +31,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -125,72 +127,197 @@ __global__ __launch_bounds__(kElimCols) void k_elim(double* __restrict__ A, int 
     }
 }
 
-// Fused step j of the partial-pivot elimination for matrices that need no row
-// swap (LD matrices: the diagonal stays the column maximum).  Column j sits
-// contiguous in col[j & 1] (written by step j - 1's owners of column j), so
-// every block reduces it to GSL's pivot (first row of maximal |a_ij|, NaNs never
-// chosen; the same decision k_lu_pivot makes).  If that pivot is row j the
-// block eliminates exactly as k_elim (same operations, same rounding) and the
-// owners of column j + 1 publish its new entries to col[(j + 1) & 1]; else the
-// step raises *flag and this and every later step do nothing (the caller then
-// reruns the pivoting path from a fresh copy).  One launch per column instead
-// of a pivot launch plus an update launch.
-__global__ __launch_bounds__(kElimCols) void k_lu_step(double* __restrict__ A, int n, int j,
-                                                       double* __restrict__ col, int* __restrict__ flag,
-                                                       double* __restrict__ z) {
+// Swap-free elimination, blocked with delayed updates (LD matrices: the
+// diagonal stays the column maximum, so no row is ever swapped).  Element
+// (i, k) of the right-looking elimination receives, for every step q <
+// min(i, k), a_ik <- a_ik - l_iq * u_qk (multiply and subtract not fused), in
+// increasing q.  Delaying the updates of columns beyond a kPanel-wide panel
+// and applying them later, still in increasing q and with the same l_iq and
+// u_qk, gives every element — U_ii, z~ — bit for bit what the per-column
+// elimination gives, at one read-modify-write of the trailing matrix per
+// panel instead of per column.
+//   k_lu_panel  (one workgroup): steps j0 .. j0 + nb - 1 on the panel columns
+//               and z; l_iq kept in Lp[q - j0][i]; a row swap (GSL's pivot, the
+//               first row of maximal |a_iq| with NaNs never chosen, would not be
+//               row q) raises *flag and every later launch returns at once (the
+//               caller reruns the pivoting path from a fresh copy); a_qq == 0
+//               skips the step (GSL), marked in sk[q - j0].
+//               Then the panel's U rows on the trailing columns (row j0 + r
+//               takes steps j0 .. j0 + r - 1, one column per thread).
+//   k_lu_trail  the panel's nb updates on rows and columns >= j0 + nb,
+//               kTrRows rows per block (kTrRows / kTrGroups independent rows
+//               per thread), l from LDS.
+constexpr int kPanel = 16;
+constexpr int kPanelThreads = 1024;
+constexpr int kTrCols = 64;
+constexpr int kTrRows = 32;
+constexpr int kTrGroups = 4;  // row groups per trailing block (kTrRows / kTrGroups rows per thread)
+constexpr int kPanelLds = 152 * 1024;  // dynamic LDS budget of k_lu_panel_lds (160 KB per CU)
+
+__global__ __launch_bounds__(kPanelThreads) void k_lu_panel(double* __restrict__ A, int n, int j0, int nb,
+                                                            double* __restrict__ Lp, double* __restrict__ sk,
+                                                            int* __restrict__ flag, double* __restrict__ z) {
 #pragma clang fp contract(off)
-    __shared__ double sv[kElimCols];
-    __shared__ int si[kElimCols];
-    __shared__ double sl[kElimRows];
     if (*flag) return;
     const int t = threadIdx.x;
-    const double* cj = col + (size_t)(j & 1) * n;
-    double mx = -1.0;
-    int ip = n;
-    for (int i = j + t; i < n; i += kElimCols) {
-        const double v = fabs(cj[i]);
-        if (v > mx) { mx = v; ip = i; }
-    }
-    sv[t] = mx;
-    si[t] = ip;
-    __syncthreads();
-    for (int w = kElimCols / 2; w > 0; w >>= 1) {
-        if (t < w) {
-            const double v2 = sv[t + w];
-            const int i2 = si[t + w];
-            if (v2 > sv[t] || (v2 == sv[t] && i2 < si[t])) { sv[t] = v2; si[t] = i2; }
+    for (int q = j0; q < j0 + nb; q++) {
+        const double aqq = A[(size_t)q * n + q];
+        const double mq = fabs(aqq);
+        bool swap = false;
+        if (aqq == aqq)
+            for (int i = q + 1 + t; i < n; i += kPanelThreads) swap |= fabs(A[(size_t)i * n + q]) > mq;
+        if (__syncthreads_or(swap)) {
+            if (t == 0) *flag = 1;
+            return;
+        }
+        if (t == 0) sk[q - j0] = (aqq == 0.0) ? 1.0 : 0.0;
+        if (aqq == 0.0) continue;  // uniform
+        const double zq = z[q];
+        double* const lq = Lp + (size_t)(q - j0) * n;
+        for (int i = q + 1 + t; i < n; i += kPanelThreads) {  // one row per thread
+            const double l = A[(size_t)i * n + q] / aqq;
+            lq[i] = l;
+            const double prod = l * zq;
+            z[i] = z[i] - prod;
+            for (int k = q + 1; k < j0 + nb; k++) {  // panel columns right of q
+                const double pk = l * A[(size_t)q * n + k];
+                double* const p = A + (size_t)i * n + k;
+                *p = *p - pk;
+            }
         }
         __syncthreads();
     }
-    const double ajj = cj[j];
-    const int p = (ajj != ajj || si[0] >= n) ? j : si[0];
-    if (p != j) {
-        if (t == 0) *flag = 1;
-        return;
-    }
-    const int i0 = j + 1 + blockIdx.y * kElimRows;
-    const int nr = min(kElimRows, n - i0);
-    const int k = j + 1 + blockIdx.x * kElimCols + t;
-    double* cn = col + (size_t)((j + 1) & 1) * n;
-    if (ajj == 0.0) {  // GSL skips the column: column j + 1 is published unchanged
-        if (k == j + 1)
-            for (int r = 0; r < nr; r++) cn[i0 + r] = A[(size_t)(i0 + r) * n + k];
-        return;
-    }
-    if (t < nr) sl[t] = A[(size_t)(i0 + t) * n + j] / ajj;
     __syncthreads();
-    if (z && blockIdx.x == 0 && t < nr) {
-        const double zj = z[j];
-        z[i0 + t] = z[i0 + t] - sl[t] * zj;
+    // the panel's U rows on the trailing columns: row j0 + r takes steps j0 .. j0 + r - 1
+    for (int k = j0 + nb + t; k < n; k += kPanelThreads) {
+        double u[kPanel];
+#pragma unroll
+        for (int r = 0; r < kPanel; r++) {
+            if (r >= nb) break;
+            double v = A[(size_t)(j0 + r) * n + k];
+#pragma unroll
+            for (int q = 0; q < r; q++) {
+                if (sk[q] != 0.0) continue;
+                const double prod = Lp[(size_t)q * n + j0 + r] * u[q];
+                v = v - prod;
+            }
+            u[r] = v;
+            if (r > 0) A[(size_t)(j0 + r) * n + k] = v;
+        }
     }
+}
+
+// k_lu_panel with the panel rows j0 .. n - 1 and z[j0 .. n - 1] held in LDS
+// (dynamic, (n - j0) x (nb + 1) doubles): the same operations on the same
+// values, one global round trip in and out instead of several per step.
+__global__ __launch_bounds__(kPanelThreads) void k_lu_panel_lds(double* __restrict__ A, int n, int j0, int nb,
+                                                                double* __restrict__ Lp, double* __restrict__ sk,
+                                                                int* __restrict__ flag, double* __restrict__ z) {
+#pragma clang fp contract(off)
+    __shared__ double sT[kPanel][kPanel];  // l of the panel's own rows (the U-row solve)
+    __shared__ double sSk[kPanel];
+    extern __shared__ double sP[];
+    if (*flag) return;
+    const int t = threadIdx.x;
+    const int R = n - j0;
+    double* const sZ = sP + (size_t)R * nb;  // z[j0 .. n - 1]
+    for (int e = t; e < R * nb; e += kPanelThreads) sP[e] = A[(size_t)(j0 + e / nb) * n + j0 + e % nb];
+    for (int r = t; r < R; r += kPanelThreads) sZ[r] = z[j0 + r];
+    __syncthreads();
+    for (int qq = 0; qq < nb; qq++) {
+        const double aqq = sP[qq * nb + qq];
+        const double mq = fabs(aqq);
+        bool swap = false;
+        if (aqq == aqq)
+            for (int r = qq + 1 + t; r < R; r += kPanelThreads) swap |= fabs(sP[r * nb + qq]) > mq;
+        if (__syncthreads_or(swap)) {
+            if (t == 0) *flag = 1;
+            return;
+        }
+        if (t == 0) sk[qq] = sSk[qq] = (aqq == 0.0) ? 1.0 : 0.0;
+        if (aqq == 0.0) continue;  // uniform
+        const double zq = sZ[qq];
+        double* const lq = Lp + (size_t)qq * n + j0;
+        for (int r = qq + 1 + t; r < R; r += kPanelThreads) {  // one row per thread
+            const double l = sP[r * nb + qq] / aqq;
+            lq[r] = l;
+            if (r < nb) sT[qq][r] = l;
+            const double prod = l * zq;
+            sZ[r] = sZ[r] - prod;
+            for (int c = qq + 1; c < nb; c++) {
+                const double pc = l * sP[qq * nb + c];
+                sP[r * nb + c] = sP[r * nb + c] - pc;
+            }
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    for (int e = t; e < R * nb; e += kPanelThreads) A[(size_t)(j0 + e / nb) * n + j0 + e % nb] = sP[e];
+    for (int r = t; r < R; r += kPanelThreads) z[j0 + r] = sZ[r];
+    // the panel's U rows on the trailing columns (l and skip marks from LDS,
+    // the column's nb entries loaded before the triangular solve)
+    for (int k = j0 + nb + t; k < n; k += kPanelThreads) {
+        double u[kPanel];
+#pragma unroll
+        for (int r = 0; r < kPanel; r++) u[r] = r < nb ? A[(size_t)(j0 + r) * n + k] : 0.0;
+#pragma unroll
+        for (int r = 1; r < kPanel; r++) {
+            if (r >= nb) break;
+#pragma unroll
+            for (int q = 0; q < r; q++) {
+                if (sSk[q] != 0.0) continue;
+                const double prod = sT[q][r] * u[q];
+                u[r] = u[r] - prod;
+            }
+            A[(size_t)(j0 + r) * n + k] = u[r];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kTrCols * kTrGroups) void k_lu_trail(double* __restrict__ A, int n, int j0, int nb,
+                                                                  const double* __restrict__ Lp,
+                                                                  const double* __restrict__ sk,
+                                                                  const int* __restrict__ flag) {
+#pragma clang fp contract(off)
+    constexpr int kPer = kTrRows / kTrGroups;  // rows per thread, independent chains
+    __shared__ double sL[kPanel][kTrRows];
+    __shared__ double sS[kPanel];
+    if (*flag) return;
+    const int tx = threadIdx.x, ty = threadIdx.y, t = ty * kTrCols + tx;
+    const int c0 = j0 + nb;  // first trailing column / row
+    const int i0 = c0 + blockIdx.y * kTrRows;
+    const int nr = max(0, min(kTrRows, n - i0));
+    for (int e = t; e < kPanel * kTrRows; e += kTrCols * kTrGroups) {
+        const int q = e / kTrRows, r = e % kTrRows;
+        sL[q][r] = (q < nb && r < nr) ? Lp[(size_t)q * n + i0 + r] : 0.0;
+    }
+    if (t < kPanel) sS[t] = t < nb ? sk[t] : 1.0;
+    __syncthreads();
+    const int k = c0 + blockIdx.x * kTrCols + tx;
     if (k >= n) return;
-    const double ujk = A[(size_t)j * n + k];
-    for (int r = 0; r < nr; r++) {
-        double* q = A + (size_t)(i0 + r) * n + k;
-        const double prod = sl[r] * ujk;
-        const double v = *q - prod;
-        *q = v;
-        if (k == j + 1) cn[i0 + r] = v;
+    double u[kPanel];  // the panel's U rows, final (k_lu_panel)
+#pragma unroll
+    for (int q = 0; q < kPanel; q++) u[q] = q < nb ? A[(size_t)(j0 + q) * n + k] : 0.0;
+    double v[kPer];
+#pragma unroll
+    for (int m = 0; m < kPer; m++) {
+        const int r = ty + kTrGroups * m;
+        v[m] = r < nr ? A[(size_t)(i0 + r) * n + k] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < kPanel; q++) {
+        if (q >= nb) break;
+        if (sS[q] != 0.0) continue;
+#pragma unroll
+        for (int m = 0; m < kPer; m++) {
+            const double prod = sL[q][ty + kTrGroups * m] * u[q];
+            v[m] = v[m] - prod;
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < kPer; m++) {
+        const int r = ty + kTrGroups * m;
+        if (r < nr) A[(size_t)(i0 + r) * n + k] = v[m];
     }
 }
 
@@ -200,13 +327,6 @@ __global__ void k_sym_check(const double* __restrict__ L, int n, int* __restrict
     if (idx >= (size_t)n * n) return;
     const int i = (int)(idx / n), k = (int)(idx % n);
     if (k > i && !(L[idx] == L[(size_t)k * n + i])) *asym = 1;
-}
-
-// col[0][i] = A[i][0]: column 0 for the first fused step; flag re-armed
-__global__ void k_lu_begin(const double* __restrict__ A, int n, double* __restrict__ col, int* __restrict__ flag) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) col[i] = A[(size_t)i * n];
-    if (i == 0) *flag = 0;
 }
 
 __global__ void k_get_diag(const double* __restrict__ A, int n, double* __restrict__ d) {
@@ -231,14 +351,39 @@ int enqueue_lu(double* A, int n, int* dswp, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// enqueue the fused (swap-free) elimination; *flag != 0 afterwards when some
-// column needed a row swap (A is then partly eliminated: recopy and pivot)
-int enqueue_lu_fused(double* A, int n, double* col, int* flag, double* z, hipStream_t st) {
-    hipLaunchKernelGGL(k_lu_begin, dim3((n + 255) / 256), dim3(256), 0, st, A, n, col, flag);
-    for (int j = 0; j < n - 1; j++) {
-        const int r = n - j - 1;
-        hipLaunchKernelGGL(k_lu_step, dim3((r + kElimCols - 1) / kElimCols, (r + kElimRows - 1) / kElimRows),
-                           dim3(kElimCols), 0, st, A, n, j, col, flag, z);
+// enqueue the blocked swap-free elimination; *flag != 0 afterwards when some
+// column needed a row swap (A is then partly eliminated: recopy and pivot).
+// work: kPanel * n + kPanel doubles (panel multipliers, skipped-step marks)
+int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipStream_t st) {
+    if (hipMemsetAsync(flag, 0, sizeof(int), st) != hipSuccess) return -1;
+    double* const sk = work + (size_t)kPanel * n;
+    // panel width: the widest (<= kPanel) whose n rows fit in LDS; the global-
+    // memory panel kernel beyond that
+    static int lds_cap = -1;
+    if (lds_cap < 0) {
+        lds_cap = kPanelLds;
+        if (hipFuncSetAttribute((const void*)k_lu_panel_lds, hipFuncAttributeMaxDynamicSharedMemorySize, kPanelLds) !=
+            hipSuccess) {
+            (void)hipGetLastError();
+            lds_cap = 64 * 1024;
+        }
+    }
+    int pw = kPanel;
+    while (pw > 1 && (size_t)n * (pw + 1) * sizeof(double) > (size_t)lds_cap) pw /= 2;
+    // PSX_LU_GLOBAL: the global-memory panel kernel at any size (tests)
+    const bool lds = (size_t)n * (pw + 1) * sizeof(double) <= (size_t)lds_cap && !std::getenv("PSX_LU_GLOBAL");
+    if (!lds) pw = kPanel;
+    for (int j0 = 0; j0 < n - 1; j0 += pw) {
+        const int nb = std::min(pw, n - 1 - j0);
+        const int rest = n - j0 - nb;  // trailing columns (and rows), >= 1
+        if (lds)
+            hipLaunchKernelGGL(k_lu_panel_lds, dim3(1), dim3(kPanelThreads), (size_t)(n - j0) * (nb + 1) * sizeof(double), st,
+                               A, n, j0, nb, work, sk, flag, z);
+        else
+            hipLaunchKernelGGL(k_lu_panel, dim3(1), dim3(kPanelThreads), 0, st, A, n, j0, nb, work, sk, flag, z);
+        hipLaunchKernelGGL(k_lu_trail, dim3((rest + kTrCols - 1) / kTrCols, (rest + kTrRows - 1) / kTrRows),
+                           dim3(kTrCols, kTrGroups), 0, st, A, n, j0, nb, (const double*)work, (const double*)sk,
+                           (const int*)flag);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -274,7 +419,7 @@ int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, dou
     auto cleanup = [&]() { hipFree(dL); hipFree(dA); hipFree(dz); hipFree(ddiag); hipFree(dcol); hipFree(dswp); };
     if (hipMalloc(&dL, nn * sizeof(double)) != hipSuccess || hipMalloc(&dA, nn * sizeof(double)) != hipSuccess ||
         hipMalloc(&dz, M * sizeof(double)) != hipSuccess || hipMalloc(&ddiag, M * sizeof(double)) != hipSuccess ||
-        hipMalloc(&dcol, 2 * (size_t)M * sizeof(double)) != hipSuccess ||
+        hipMalloc(&dcol, ((size_t)kPanel * M + kPanel) * sizeof(double)) != hipSuccess ||
         hipMalloc(&dswp, (std::max(M, 1) + 2) * sizeof(int)) != hipSuccess) {
         cleanup();
         if (err) *err = "out of device memory (LD setup)";

@@ -212,3 +212,52 @@ def test_warmup_entry_point(gpu):
     pc = E.PostCal(seam)
     pc.run_exhaustive()
     assert_parity(pc.accum(), O.postcal(seam))
+
+
+def _elim_pivots(a):
+    """Host restatement of the swap-free right-looking elimination (GSL's
+    operation order: l = a_ij / a_jj, then a_ik - l * u_jk, not fused; a zero
+    pivot skips the column): the U diagonal."""
+    a = np.array(a, dtype=np.float64, copy=True)
+    n = a.shape[0]
+    for j in range(n - 1):
+        if a[j, j] == 0.0:
+            continue
+        l = a[j + 1:, j] / a[j, j]
+        a[j + 1:, j + 1:] -= np.outer(l, a[j, j + 1:])
+    return np.diag(a).copy()
+
+
+@pytest.mark.parametrize("M,glob", [(1, 0), (2, 0), (15, 0), (16, 0), (17, 0), (33, 0), (300, 0), (1000, 0),
+                                    (2000, 0), (17, 1), (300, 1)])
+def test_blocked_swap_free_elimination_bit_identical(gpu, M, glob, monkeypatch):
+    """The blocked (panel + delayed trailing update) swap-free elimination of
+    psx_setup.hip gives the per-column elimination's pivots bit for bit:
+    the setup's min pivot ratio equals the host restatement's exactly, on
+    sizes around the 16-column panel and on the SYN-v1 LDs (M = 2000: 8-column
+    panels in LDS); glob = 1 forces the global-memory panel kernel."""
+    if glob:
+        monkeypatch.setenv("PSX_LU_GLOBAL", "1")
+    if M >= 1000:
+        ld, z, _, _, u2l = synth.syn_v1(M)
+    else:
+        idx = np.arange(M)
+        a0 = 0.95 ** np.abs(idx[:, None] - idx[None, :])
+        a1 = 0.5 ** np.abs(idx[:, None] - idx[None, :])
+        rng = np.random.default_rng(M)
+        ld = [a0, a1]
+        z = [rng.standard_normal(M), rng.standard_normal(M)]
+        u2l = np.stack([idx, idx]).astype(np.int32)
+    mi = E.model_inputs(ld, z, u2l, (6000, 7000), max_causal=1, sharing_param=0.25)
+    pc = E.PostCal(mi)
+    info = pc.setup_info
+    for s in range(2):
+        add = E.psd_shift(ld[s])[1]
+        assert info["psd_added"][s] == add
+        if info["eigen_route"][s]:
+            continue
+        a = ld[s] + add * np.eye(ld[s].shape[0])
+        piv = _elim_pivots(a)
+        dmax = np.abs(np.diag(a)).max()
+        assert info["min_pivot_ratio"][s] == piv.min() / dmax, (s, info["min_pivot_ratio"][s], piv.min() / dmax)
+    pc.close()
