@@ -152,7 +152,7 @@ constexpr int kPanelThreads = 1024;
 constexpr int kTrCols = 64;
 constexpr int kTrRows = 32;
 constexpr int kTrGroups = 4;  // row groups per trailing block (kTrRows / kTrGroups rows per thread)
-constexpr int kPanelLds = 152 * 1024;  // dynamic LDS budget of k_lu_panel_lds (160 KB per CU)
+constexpr int kPanelLds = 152 * 1024;  // dynamic LDS budget of k_lu_panel_lds (160 KB per CU; 158 KB is refused)
 
 __global__ __launch_bounds__(kPanelThreads) void k_lu_panel(double* __restrict__ A, int n, int j0, int nb,
                                                             double* __restrict__ Lp, double* __restrict__ sk,
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kPanelThreads) void k_lu_panel(double* __restrict__
 }
 
 // k_lu_panel with the panel rows j0 .. n - 1 and z[j0 .. n - 1] held in LDS
-// (dynamic, (n - j0) x (nb + 1) doubles): the same operations on the same
+// (dynamic, (n - j0) x (nb + 2) doubles: rows padded to nb + 1, then z): the same operations on the same
 // values, one global round trip in and out instead of several per step.
 __global__ __launch_bounds__(kPanelThreads) void k_lu_panel_lds(double* __restrict__ A, int n, int j0, int nb,
                                                                 double* __restrict__ Lp, double* __restrict__ sk,
@@ -220,16 +220,17 @@ __global__ __launch_bounds__(kPanelThreads) void k_lu_panel_lds(double* __restri
     if (*flag) return;
     const int t = threadIdx.x;
     const int R = n - j0;
-    double* const sZ = sP + (size_t)R * nb;  // z[j0 .. n - 1]
-    for (int e = t; e < R * nb; e += kPanelThreads) sP[e] = A[(size_t)(j0 + e / nb) * n + j0 + e % nb];
+    const int ls = nb + 1;  // LDS row stride: odd in doubles, so a wave's rows spread over the banks
+    double* const sZ = sP + (size_t)R * ls;  // z[j0 .. n - 1]
+    for (int e = t; e < R * nb; e += kPanelThreads) sP[(e / nb) * ls + e % nb] = A[(size_t)(j0 + e / nb) * n + j0 + e % nb];
     for (int r = t; r < R; r += kPanelThreads) sZ[r] = z[j0 + r];
     __syncthreads();
     for (int qq = 0; qq < nb; qq++) {
-        const double aqq = sP[qq * nb + qq];
+        const double aqq = sP[qq * ls + qq];
         const double mq = fabs(aqq);
         bool swap = false;
         if (aqq == aqq)
-            for (int r = qq + 1 + t; r < R; r += kPanelThreads) swap |= fabs(sP[r * nb + qq]) > mq;
+            for (int r = qq + 1 + t; r < R; r += kPanelThreads) swap |= fabs(sP[r * ls + qq]) > mq;
         if (__syncthreads_or(swap)) {
             if (t == 0) *flag = 1;
             return;
@@ -239,20 +240,20 @@ __global__ __launch_bounds__(kPanelThreads) void k_lu_panel_lds(double* __restri
         const double zq = sZ[qq];
         double* const lq = Lp + (size_t)qq * n + j0;
         for (int r = qq + 1 + t; r < R; r += kPanelThreads) {  // one row per thread
-            const double l = sP[r * nb + qq] / aqq;
+            const double l = sP[r * ls + qq] / aqq;
             lq[r] = l;
             if (r < nb) sT[qq][r] = l;
             const double prod = l * zq;
             sZ[r] = sZ[r] - prod;
             for (int c = qq + 1; c < nb; c++) {
-                const double pc = l * sP[qq * nb + c];
-                sP[r * nb + c] = sP[r * nb + c] - pc;
+                const double pc = l * sP[qq * ls + c];
+                sP[r * ls + c] = sP[r * ls + c] - pc;
             }
         }
         __syncthreads();
     }
     __syncthreads();
-    for (int e = t; e < R * nb; e += kPanelThreads) A[(size_t)(j0 + e / nb) * n + j0 + e % nb] = sP[e];
+    for (int e = t; e < R * nb; e += kPanelThreads) A[(size_t)(j0 + e / nb) * n + j0 + e % nb] = sP[(e / nb) * ls + e % nb];
     for (int r = t; r < R; r += kPanelThreads) z[j0 + r] = sZ[r];
     // the panel's U rows on the trailing columns (l and skip marks from LDS,
     // the column's nb entries loaded before the triangular solve)
@@ -369,15 +370,15 @@ int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipSt
         }
     }
     int pw = kPanel;
-    while (pw > 1 && (size_t)n * (pw + 1) * sizeof(double) > (size_t)lds_cap) pw /= 2;
+    while (pw > 1 && (size_t)n * (pw + 2) * sizeof(double) > (size_t)lds_cap) pw--;
     // PSX_LU_GLOBAL: the global-memory panel kernel at any size (tests)
-    const bool lds = (size_t)n * (pw + 1) * sizeof(double) <= (size_t)lds_cap && !std::getenv("PSX_LU_GLOBAL");
+    const bool lds = (size_t)n * (pw + 2) * sizeof(double) <= (size_t)lds_cap && !std::getenv("PSX_LU_GLOBAL");
     if (!lds) pw = kPanel;
     for (int j0 = 0; j0 < n - 1; j0 += pw) {
         const int nb = std::min(pw, n - 1 - j0);
         const int rest = n - j0 - nb;  // trailing columns (and rows), >= 1
         if (lds)
-            hipLaunchKernelGGL(k_lu_panel_lds, dim3(1), dim3(kPanelThreads), (size_t)(n - j0) * (nb + 1) * sizeof(double), st,
+            hipLaunchKernelGGL(k_lu_panel_lds, dim3(1), dim3(kPanelThreads), (size_t)(n - j0) * (nb + 2) * sizeof(double), st,
                                A, n, j0, nb, work, sk, flag, z);
         else
             hipLaunchKernelGGL(k_lu_panel, dim3(1), dim3(kPanelThreads), 0, st, A, n, j0, nb, work, sk, flag, z);
