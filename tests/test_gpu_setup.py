@@ -111,7 +111,7 @@ def test_ld_route_syn1000(gpu):
 
 
 def test_ld_route_fused_lu_shift_loop_and_asymmetric(gpu):
-    """The swap-free fused elimination (one launch per column, z's forward
+    """The swap-free fused elimination (blocked panels, z's forward
     solve riding along, step 2 skipped for an exactly symmetric LD):
     * study 0: AR(1) rho = 0.95, M = 400, whose determinant underflows to 0,
       so util.cpp:195-226 adds 0.01 several times; the shift must equal the
