@@ -275,6 +275,117 @@ __global__ __launch_bounds__(kPanelThreads) void k_lu_panel_lds(double* __restri
     }
 }
 
+// The partial-pivot elimination (GSL 2.5 gsl_linalg_LU_decomp), blocked the
+// LAPACK getrf way: the panel (rows j0 .. n - 1, LDS, odd row stride) takes
+// each step's pivot (first row of maximal |a_iq|, NaNs never chosen, a NaN
+// a_qq keeps row q), swaps whole panel rows, stores l in place of a_iq and
+// updates the panel columns; then the trailing columns take the panel's swaps
+// in step order, the U-row solve, and k_lu_trail's delayed updates.  Swaps
+// only move data, and a row at position q is never moved after step q, so
+// every element of U sees the unblocked elimination's operations on the same
+// values: U_ii and the swap count are bit-identical.
+__global__ __launch_bounds__(kPanelThreads) void k_lu_panel_piv(double* __restrict__ A, int n, int j0, int nb,
+                                                                double* __restrict__ Lp, double* __restrict__ sk,
+                                                                int* __restrict__ swp) {
+#pragma clang fp contract(off)
+    __shared__ double sT[kPanel][kPanel];
+    __shared__ double sSk[kPanel];
+    __shared__ int sPiv[kPanel];
+    __shared__ double wv[kPanelThreads / 64];
+    __shared__ int wi[kPanelThreads / 64];
+    extern __shared__ double sP[];
+    const int t = threadIdx.x;
+    const int R = n - j0;
+    const int ls = nb + 1;
+    for (int e = t; e < R * nb; e += kPanelThreads) sP[(e / nb) * ls + e % nb] = A[(size_t)(j0 + e / nb) * n + j0 + e % nb];
+    __syncthreads();
+    for (int qq = 0; qq < nb; qq++) {
+        double mx = -1.0;
+        int ip = R;
+        for (int r = qq + t; r < R; r += kPanelThreads) {
+            const double v = fabs(sP[r * ls + qq]);
+            if (v > mx) { mx = v; ip = r; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double v2 = __shfl_xor(mx, o);
+            const int i2 = __shfl_xor(ip, o);
+            if (v2 > mx || (v2 == mx && i2 < ip)) { mx = v2; ip = i2; }
+        }
+        if ((t & 63) == 0) { wv[t >> 6] = mx; wi[t >> 6] = ip; }
+        __syncthreads();
+        mx = wv[0];
+        ip = wi[0];
+        for (int w = 1; w < kPanelThreads / 64; w++)
+            if (wv[w] > mx || (wv[w] == mx && wi[w] < ip)) { mx = wv[w]; ip = wi[w]; }
+        const double a0 = sP[qq * ls + qq];
+        const int p = (a0 != a0 || ip >= R) ? qq : ip;
+        if (t == 0) {
+            sPiv[qq] = p;
+            swp[j0 + qq] = (p != qq) ? 1 : 0;
+        }
+        __syncthreads();  // every thread has read wv / wi and row qq's old a_qq
+        if (p != qq) {
+            if (t < nb) {
+                const double x = sP[qq * ls + t];
+                sP[qq * ls + t] = sP[p * ls + t];
+                sP[p * ls + t] = x;
+            }
+            __syncthreads();
+        }
+        const double aqq = sP[qq * ls + qq];
+        if (t == 0) sk[qq] = sSk[qq] = (aqq == 0.0) ? 1.0 : 0.0;
+        if (aqq == 0.0) continue;  // uniform
+        for (int r = qq + 1 + t; r < R; r += kPanelThreads) {
+            const double l = sP[r * ls + qq] / aqq;
+            sP[r * ls + qq] = l;
+            for (int c = qq + 1; c < nb; c++) {
+                const double pc = l * sP[qq * ls + c];
+                sP[r * ls + c] = sP[r * ls + c] - pc;
+            }
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    for (int e = t; e < R * nb; e += kPanelThreads) {
+        const int r = e / nb, c = e % nb;
+        const double v = sP[r * ls + c];
+        if (r > c) Lp[(size_t)c * n + j0 + r] = v;  // l, at the row's final position
+        A[(size_t)(j0 + r) * n + j0 + c] = v;
+    }
+    for (int e = t; e < kPanel * kPanel; e += kPanelThreads) {
+        const int q = e / kPanel, r = e % kPanel;
+        sT[q][r] = (q < r && r < nb) ? sP[r * ls + q] : 0.0;
+    }
+    __syncthreads();
+    for (int k = j0 + nb + t; k < n; k += kPanelThreads) {
+        for (int q = 0; q < nb; q++) {  // the panel's swaps, in step order
+            const int p = sPiv[q];
+            if (p != q) {
+                double* const x = A + (size_t)(j0 + q) * n + k;
+                double* const y = A + (size_t)(j0 + p) * n + k;
+                const double tq = *x;
+                *x = *y;
+                *y = tq;
+            }
+        }
+        double u[kPanel];
+#pragma unroll
+        for (int r = 0; r < kPanel; r++) u[r] = r < nb ? A[(size_t)(j0 + r) * n + k] : 0.0;
+#pragma unroll
+        for (int r = 1; r < kPanel; r++) {
+            if (r >= nb) break;
+#pragma unroll
+            for (int q = 0; q < r; q++) {
+                if (sSk[q] != 0.0) continue;
+                const double prod = sT[q][r] * u[q];
+                u[r] = u[r] - prod;
+            }
+            A[(size_t)(j0 + r) * n + k] = u[r];
+        }
+    }
+}
+
 __global__ __launch_bounds__(kTrCols * kTrGroups) void k_lu_trail(double* __restrict__ A, int n, int j0, int nb,
                                                                   const double* __restrict__ Lp,
                                                                   const double* __restrict__ sk,
@@ -393,7 +504,42 @@ int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipSt
 
 int lu_det_device(double* dA, int n, int* dswp, double* ddiag, hipStream_t st, double* det, std::string* err) {
     if (n <= 0) return -1;
-    if (enqueue_lu(dA, n, dswp, st)) return chk(hipGetLastError(), "LU launch", err);
+    // blocked when the panel fits the LDS budget (PSX_LU_UNBLOCKED=1: per-column launches)
+    int pw = kPanel;
+    while (pw > 1 && (size_t)n * (pw + 1) * sizeof(double) > (size_t)(64 * 1024)) pw--;
+    static bool attr = false;
+    if (!attr && hipFuncSetAttribute((const void*)k_lu_panel_piv, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     kPanelLds) == hipSuccess)
+        attr = true;
+    (void)hipGetLastError();
+    if (attr) {
+        pw = kPanel;
+        while (pw > 1 && (size_t)n * (pw + 1) * sizeof(double) > (size_t)kPanelLds) pw--;
+    }
+    const size_t need = (size_t)n * (pw + 1) * sizeof(double);
+    if (need <= (size_t)(attr ? kPanelLds : 64 * 1024) && !std::getenv("PSX_LU_UNBLOCKED")) {
+        double* work = nullptr;
+        if (chk(hipMalloc(&work, ((size_t)kPanel * n + kPanel) * sizeof(double) + sizeof(int)), "LU work", err))
+            return -1;
+        double* const sk = work + (size_t)kPanel * n;
+        int* const zflag = (int*)(sk + kPanel);
+        int rc = chk(hipMemsetAsync(zflag, 0, sizeof(int), st), "memset", err);
+        for (int j0 = 0; !rc && j0 < n - 1; j0 += pw) {
+            const int nb = std::min(pw, n - 1 - j0);
+            const int rest = n - j0 - nb;
+            hipLaunchKernelGGL(k_lu_panel_piv, dim3(1), dim3(kPanelThreads), (size_t)(n - j0) * (nb + 1) * sizeof(double),
+                               st, dA, n, j0, nb, work, sk, dswp);
+            hipLaunchKernelGGL(k_lu_trail, dim3((rest + kTrCols - 1) / kTrCols, (rest + kTrRows - 1) / kTrRows),
+                               dim3(kTrCols, kTrGroups), 0, st, dA, n, j0, nb, (const double*)work, (const double*)sk,
+                               (const int*)zflag);
+        }
+        if (!rc) rc = chk(hipGetLastError(), "LU launch", err);
+        if (!rc) rc = chk(hipStreamSynchronize(st), "LU sync", err);
+        hipFree(work);
+        if (rc) return rc;
+    } else if (enqueue_lu(dA, n, dswp, st)) {
+        return chk(hipGetLastError(), "LU launch", err);
+    }
     hipLaunchKernelGGL(k_get_diag, dim3((n + 255) / 256), dim3(256), 0, st, dA, n, ddiag);
     std::vector<double> diag(n);
     std::vector<int> swp(std::max(n - 1, 1), 0);

@@ -261,3 +261,17 @@ def test_blocked_swap_free_elimination_bit_identical(gpu, M, glob, monkeypatch):
         dmax = np.abs(np.diag(a)).max()
         assert info["min_pivot_ratio"][s] == piv.min() / dmax, (s, info["min_pivot_ratio"][s], piv.min() / dmax)
     pc.close()
+
+
+@pytest.mark.parametrize("n", [2, 16, 17, 33, 300])
+def test_blocked_pivoting_lu_det_bit_identical(gpu, n, monkeypatch):
+    """The blocked partial-pivot elimination (LDS panel with row swaps, swaps
+    replayed on the trailing columns, delayed updates) gives the host
+    restatement's determinant bit for bit on random matrices that need row
+    swaps, and so does the per-column path (PSX_LU_UNBLOCKED=1)."""
+    a = np.random.default_rng(100 + n).standard_normal((n, n))
+    h = E.lu_det(a)
+    g = E.lu_det(a, gpu=True)
+    monkeypatch.setenv("PSX_LU_UNBLOCKED", "1")
+    u = E.lu_det(a, gpu=True)
+    assert _bits(h) == _bits(g) == _bits(u), (n, h, g, u)
