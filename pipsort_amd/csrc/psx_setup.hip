@@ -212,7 +212,8 @@ __global__ __launch_bounds__(kPanelThreads) void k_lu_panel(double* __restrict__
 // values, one global round trip in and out instead of several per step.
 __global__ __launch_bounds__(kPanelThreads) void k_lu_panel_lds(double* __restrict__ A, int n, int j0, int nb,
                                                                 double* __restrict__ Lp, double* __restrict__ sk,
-                                                                int* __restrict__ flag, double* __restrict__ z) {
+                                                                int* __restrict__ flag, double* __restrict__ z,
+                                                                int check) {
 #pragma clang fp contract(off)
     __shared__ double sT[kPanel][kPanel];  // l of the panel's own rows (the U-row solve)
     __shared__ double sSk[kPanel];
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(kPanelThreads) void k_lu_panel_lds(double* __restri
         const double aqq = sP[qq * ls + qq];
         const double mq = fabs(aqq);
         bool swap = false;
-        if (aqq == aqq)
+        if (check && aqq == aqq)
             for (int r = qq + 1 + t; r < R; r += kPanelThreads) swap |= fabs(sP[r * ls + qq]) > mq;
         if (__syncthreads_or(swap)) {
             if (t == 0) *flag = 1;
@@ -466,7 +467,7 @@ int enqueue_lu(double* A, int n, int* dswp, hipStream_t st) {
 // enqueue the blocked swap-free elimination; *flag != 0 afterwards when some
 // column needed a row swap (A is then partly eliminated: recopy and pivot).
 // work: kPanel * n + kPanel doubles (panel multipliers, skipped-step marks)
-int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipStream_t st) {
+int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipStream_t st, bool check = true) {
     if (hipMemsetAsync(flag, 0, sizeof(int), st) != hipSuccess) return -1;
     double* const sk = work + (size_t)kPanel * n;
     // panel width: the widest (<= kPanel) whose n rows fit in LDS; the global-
@@ -484,13 +485,14 @@ int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipSt
     while (pw > 1 && (size_t)n * (pw + 2) * sizeof(double) > (size_t)lds_cap) pw--;
     // PSX_LU_GLOBAL: the global-memory panel kernel at any size (tests)
     const bool lds = (size_t)n * (pw + 2) * sizeof(double) <= (size_t)lds_cap && !std::getenv("PSX_LU_GLOBAL");
+    if (!check && !lds) return 1;  // no unchecked global-memory panel: the caller eliminates per column
     if (!lds) pw = kPanel;
     for (int j0 = 0; j0 < n - 1; j0 += pw) {
         const int nb = std::min(pw, n - 1 - j0);
         const int rest = n - j0 - nb;  // trailing columns (and rows), >= 1
         if (lds)
             hipLaunchKernelGGL(k_lu_panel_lds, dim3(1), dim3(kPanelThreads), (size_t)(n - j0) * (nb + 2) * sizeof(double), st,
-                               A, n, j0, nb, work, sk, flag, z);
+                               A, n, j0, nb, work, sk, flag, z, check ? 1 : 0);
         else
             hipLaunchKernelGGL(k_lu_panel, dim3(1), dim3(kPanelThreads), 0, st, A, n, j0, nb, work, sk, flag, z);
         hipLaunchKernelGGL(k_lu_trail, dim3((rest + kTrCols - 1) / kTrCols, (rest + kTrRows - 1) / kTrRows),
@@ -642,11 +644,16 @@ int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, dou
                 break;
             if ((rc = chk(hipMemcpyAsync(dz, z, M * sizeof(double), hipMemcpyHostToDevice, st), "z upload", err)))
                 break;
-            for (int j = 0; j < M - 1; j++) {
-                const int r = M - j - 1;
-                hipLaunchKernelGGL(k_elim, dim3((r + kElimCols - 1) / kElimCols, (r + kElimRows - 1) / kElimRows),
-                                   dim3(kElimCols), 0, st, dA, M, j, dz);
-            }
+            // elimination without pivoting: the blocked panels with the pivot check off
+            // (per-column launches when the panel does not fit LDS)
+            const int lrc = enqueue_lu_fused(dA, M, dcol, dflag, dz, st, false);
+            if (lrc < 0) { rc = chk(hipGetLastError(), "elimination launch", err); if (!rc) rc = -1; break; }
+            if (lrc > 0)
+                for (int j = 0; j < M - 1; j++) {
+                    const int r = M - j - 1;
+                    hipLaunchKernelGGL(k_elim, dim3((r + kElimCols - 1) / kElimCols, (r + kElimRows - 1) / kElimRows),
+                                       dim3(kElimCols), 0, st, dA, M, j, dz);
+                }
             hipLaunchKernelGGL(k_get_diag, dim3((M + 255) / 256), dim3(256), 0, st, dA, M, ddiag);
             if ((rc = chk(hipGetLastError(), "elimination launch", err))) break;
             hipMemcpyAsync(piv.data(), ddiag, M * sizeof(double), hipMemcpyDeviceToHost, st);
