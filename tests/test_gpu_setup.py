@@ -275,3 +275,34 @@ def test_blocked_pivoting_lu_det_bit_identical(gpu, n, monkeypatch):
     monkeypatch.setenv("PSX_LU_UNBLOCKED", "1")
     u = E.lu_det(a, gpu=True)
     assert _bits(h) == _bits(g) == _bits(u), (n, h, g, u)
+
+
+def test_blocked_step2_elimination_bit_identical(gpu):
+    """Step 2 (no pivoting, on the lower triangle mirrored) through the blocked
+    panels with the pivot check off: the min pivot ratio equals the host
+    restatement's exactly, for an LD one ulp off symmetric (M = 300) and for
+    tests/example's LDs (they need row swaps, so step 1 took the pivoting
+    path)."""
+    M = 300
+    idx = np.arange(M)
+    ld1 = 0.5 ** np.abs(idx[:, None] - idx[None, :])
+    ld1[3, 17] = np.nextafter(ld1[3, 17], 1.0)
+    rng = np.random.default_rng(5)
+    cases = [([ld1, ld1.copy()], [rng.standard_normal(M), rng.standard_normal(M)],
+              np.stack([idx, idx]).astype(np.int32), (6000, 7000))]
+    L = loci.read_locus(loci.EXAMPLE["dirname"])
+    cases.append((L["ld"], L["z"], L["u2l"], loci.EXAMPLE["n"]))
+    for ld, z, u2l, n in cases:
+        mi = E.model_inputs(ld, z, u2l, n, max_causal=1, sharing_param=0.25)
+        pc = E.PostCal(mi)
+        info = pc.setup_info
+        for s in range(2):
+            if info["eigen_route"][s]:
+                continue
+            a = np.asarray(ld[s], dtype=np.float64)
+            add = info["psd_added"][s]
+            sym = np.tril(a) + np.tril(a, -1).T + add * np.eye(a.shape[0])
+            piv = _elim_pivots(sym)
+            dmax = np.abs(np.diag(sym)).max()
+            assert info["min_pivot_ratio"][s] == piv.min() / dmax, (s, info["min_pivot_ratio"][s], piv.min() / dmax)
+        pc.close()
