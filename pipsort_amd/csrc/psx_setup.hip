@@ -10,9 +10,11 @@
 // Q|W|Q^T, z and z^T Q|W|^-1 Q^T z, so whenever Sigma' is positive definite
 // they are exactly Sigma', z and z^T Sigma'^-1 z: no eigendecomposition.
 //
-//  * Step 1 runs here as a right-looking elimination (swap-free LDs: blocked,
-//    updates delayed by a kPanel-column panel; otherwise one pivot launch + one
-//    update launch per column), with the reference's operation
+//  * Step 1 runs here as a right-looking elimination, blocked (an LDS panel
+//    of <= kPanel columns, trailing updates delayed; swap-free LDs without
+//    pivot search, others with GSL's pivot and the swaps replayed on the
+//    trailing columns; per-column launches past the LDS budget), with the
+//    reference's operation
 //    order and IEEE rounding (division correctly rounded, multiply and
 //    subtract not fused), so the per-element update sequence — and hence
 //    every U_ii and the index-order determinant product — is bit-identical to
@@ -23,10 +25,10 @@
 //    comfortably positive (ratio to the largest diagonal < kPdRatio) the
 //    caller falls back to the reference's eigen route (host restatement).
 //
-// The elimination kernels are HBM/L2 streaming kernels (one read-modify-write
-// of the trailing matrix per column, 2/3 M^3 * 16 B over a setup); the matrix
-// (32 MB at M = 2000) stays L2/MALL resident.  Launch latency dominates below
-// a few hundred trailing rows.
+// The trailing update is an HBM/L2 streaming kernel (one read-modify-write of
+// the trailing matrix per panel); the matrix (32 MB at M = 2000) stays
+// L2/MALL resident.  The panel kernel is one workgroup on one CU (its LDS
+// throughput bounds it); launch latency dominates below a few hundred rows.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
