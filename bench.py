@@ -122,6 +122,102 @@ def cpu_baseline(seam, budget_s=15.0, threads=None):
                       f"{dt:.1f} s"}
 
 
+def example_patterns(seam):
+    """Every configuration of an exhaustive sweep except the null one
+    (postcal.cpp:716-1092: union subsets of size 1..c, then the per-study
+    assignments passing checkOR), as (sets, bits) per level for
+    oracle.eval_patterns."""
+    import itertools
+    u2l = seam.union_to_local
+    allowed = []
+    for u in range(seam.n_union):
+        a0, a1 = u2l[0, u] >= 0, u2l[1, u] >= 0
+        allowed.append([x for x in (1, 2, 3) if (x & 1 and a0 or not x & 1) and (x & 2 and a1 or not x & 2)])
+    out = []
+    for k in range(1, int(seam.max_causal) + 1):
+        sets, bits = [], []
+        for S in itertools.combinations(range(seam.n_union), k):
+            for xs in itertools.product(*(allowed[u] for u in S)):
+                sets.append(S)
+                bits.append([[x & 1 for x in xs], [(x >> 1) & 1 for x in xs]])
+        out.append((np.array(sets, dtype=np.int32), np.array(bits, dtype=np.int32)))
+    return out
+
+
+def cpu_baseline_example(threads=None):
+    """BASELINE configs[0] (tests/example, -c 2 -p 0.25) on this box's host
+    cores, in full: the oracle's literal N x N restatement of the reference
+    likelihood (lowrank_likelihood, postcal.cpp:214-304) for all 216,817
+    configurations, split over `threads` host threads.  The PIPs folded from its
+    L values are checked against the reference's expected_study*_post.txt."""
+    from oracle import oracle as O
+    import loci
+    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    seam = build_seam("example")
+    levels = example_patterns(seam)
+    O.load()
+    work = []
+    for sets, bits in levels:
+        for ch in np.array_split(np.arange(sets.shape[0]), threads * 4):
+            if ch.size:
+                work.append((sets[ch], bits[ch], ch))
+    res = [None] * len(work)
+    nxt = [0]
+    lock = threading.Lock()
+
+    def run():
+        while True:
+            with lock:
+                i = nxt[0]
+                nxt[0] += 1
+            if i >= len(work):
+                return
+            res[i] = O.eval_patterns(seam, work[i][0], work[i][1], literal=True)[0]
+
+    t0 = time.time()
+    th = [threading.Thread(target=run) for _ in range(threads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    dt = time.time() - t0
+    n = sum(s.shape[0] for s, _ in levels) + 1
+    # fold: total and per-SNP post (log-sum-exp), null configuration L0 (postcal.cpp:802-803)
+    L0 = -0.5 * float(np.dot(seam.s_prime, seam.s_prime)) - 1.0 + seam.n_union * np.log(1 - seam.gamma)
+    m0 = int(seam.m[0])
+    Ls, members = [np.array([L0])], []
+    wi = 0
+    for sets, bits in levels:
+        Lk = np.empty(sets.shape[0])
+        while wi < len(work) and work[wi][0].shape[1] == sets.shape[1]:
+            Lk[work[wi][2]] = res[wi]
+            wi += 1
+        Ls.append(Lk)
+        members.append((sets, bits, Lk))
+    allL = np.concatenate(Ls)
+    mx = allL.max()
+    total = mx + np.log(np.exp(allL - mx).sum())
+    acc = np.zeros(seam.N)
+    for sets, bits, Lk in members:
+        w = np.exp(Lk - total)
+        for s in range(2):
+            for j in range(sets.shape[1]):
+                sel = bits[:, s, j] == 1
+                loc = seam.union_to_local[s, sets[sel, j]] + s * m0
+                np.add.at(acc, loc, w[sel])
+    ok = True
+    for s in range(2):
+        exp = [float(l.split()[1]) for l in open(os.path.join(loci.GOLDEN, "example", f"expected_study{s}_post.txt"))
+               .read().splitlines()[1:]]
+        got = acc[s * m0: s * m0 + len(exp)]
+        ok = ok and bool(np.all(np.abs(got - np.array(exp)) <= 5e-6 * np.maximum(np.abs(exp), 1e-300) + 1e-12))
+    return {"value": n / dt, "unit": "configs/s", "cores": threads, "kind": "port", "wall_s": dt, "configs": n,
+            "pips_match_reference_expected": ok,
+            "sample": f"full tests/example c=2 sweep ({n} configurations), oracle literal N x N restatement of "
+                      f"lowrank_likelihood (postcal.cpp:214-304), {threads} host threads of "
+                      f"{os.cpu_count()} visible; PIPs checked against expected_study*_post.txt (6 digits)"}
+
+
 def sss_probe(reps=20):
     """BASELINE configs[4]: the SSS path (sss_postcal.cpp:102-380) on SYN-v1
     M = 2000, -c 5 — the walk itself, and the throughput of one SSS proposal
@@ -247,27 +343,59 @@ def example_wall():
     return wall if r.returncode == 0 else None, same
 
 
+KERNEL_SOURCES = ("psx_sweep3.hip", "psx_sweep_dev.h", "psx_sweep_unit.h", "psx_math.h", "psx_sweep.h")
+
+
+def kernel_src_sha():
+    """Hash of the sources k_sweep3 is compiled from: a PMC summary describes
+    this build only if it carries the same hash (tools/pmc_summary.py)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, "pipsort_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def load_pmc(workload):
+    """profiles/pmc_latest.json (rocprofv3 --pmc passes, tools/gpu_pmc.sh +
+    tools/pmc_summary.py) if it was collected on this workload AND this build
+    of the kernel; else None."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(p):
         return None
     try:
         d = json.load(open(p))
-        if d.get("workload") == workload:
+        if d.get("workload") == workload and d.get("kernel_src_sha") == kernel_src_sha():
             return d
     except Exception:
         pass
     return None
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): start N ranks,
+    one process per GPU, as a torch.distributed.run child — before this process
+    touches the GPU (device_count() does not create a context) — and exit with
+    its status.  Rank 0 prints the bench line on the inherited stdout.  The
+    whole-node analogue of the reference's 64 OpenMP threads
+    (postcal.cpp:747-769)."""
+    import socket
+    backend = os.environ.get("PSX_DIST_BACKEND", "nccl")
+    have = torch.cuda.device_count()
+    if backend == "nccl" and have < n:
+        print(f"bench: --gpus {n} but only {have} HIP device(s) visible", file=sys.stderr)
+        return 2
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
-    # the bench line must be the only thing on stdout: native libraries print
-    # banners there (RCCL prints its version block at communicator init), so
-    # fd 1 is pointed at stderr for the whole run and the line is written to a
-    # saved copy of the original stdout
-    sys.stdout.flush()
-    line_fd = os.dup(1)
-    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -276,6 +404,15 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    # the bench line must be the only thing on stdout: native libraries print
+    # banners there (RCCL prints its version block at communicator init), so
+    # fd 1 is pointed at stderr for the whole run and the line is written to a
+    # saved copy of the original stdout
+    sys.stdout.flush()
+    line_fd = os.dup(1)
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -283,8 +420,11 @@ def main():
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
     # PSX_DIST_BACKEND=gloo lets a multi-rank run share one GPU for validation
-    # (host-staged exchange); the real path is nccl = RCCL over xGMI.
+    # (host-staged exchange); the real path is nccl = RCCL over xGMI, one GPU per rank.
     backend = os.environ.get("PSX_DIST_BACKEND", "nccl")
+    if backend == "nccl" and world > 1 and torch.cuda.device_count() < world:
+        print(f"bench: {world} ranks but only {torch.cuda.device_count()} HIP device(s)", file=sys.stderr)
+        sys.exit(2)
     # PSX_FORCE_DIST=1 takes the multi-rank code path even at world 1 (under
     # torch.distributed.run): the RCCL calls of the exchange then run on a
     # one-GPU box, as a check of the N > 1 path (not a bench line)
@@ -383,22 +523,41 @@ def main():
         value = configs_per_step * args.steps / elapsed
         avg_kernel_s = (kms / max(launches, 1)) / 1e3
         alg_bytes = tm["alg_bytes"]  # per launch of the dominant kernel (this rank's shard)
-        achieved = alg_bytes / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
-        pmc = load_pmc(args.workload) if world == 1 else None
-        roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK_GBS,
-                    "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
-                    "kernel": "k_sweep<3>" if seam.max_causal >= 3 else "k_sweep<2>",
+        pmc = load_pmc(args.workload)
+        # The binding roof of k_sweep3 is FP64 VALU issue, not HBM:
+        # achieved = FP64 operations of one launch (PMC SQ_INSTS_VALU_FLOPS_FP64,
+        # FMA = 2, per wave instruction x 64 lanes, collected on this build) / the
+        # launch's average duration measured here (HIP events of its own dispatch).
+        if pmc and pmc.get("fp64_flops_per_launch"):
+            # counters of the world-1 launch; a shard of `world` equal-work slices does 1/world of it
+            flops = pmc["fp64_flops_per_launch"] * 64.0 / world
+            flops_src = ("PMC SQ_INSTS_VALU_FLOPS_FP64 x 64 (profiles/pmc_latest.json, same kernel build)"
+                         + (f" / {world} (this rank's shard)" if world > 1 else ""))
+        else:
+            flops = tm["flops"]
+            flops_src = "model: 281 FP64 operations per 3-SNP union set (PMC-calibrated, earlier build)"
+        achieved = flops / avg_kernel_s / 1e12 if avg_kernel_s > 0 else 0.0
+        roofline = {"bound": "valu_fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": achieved / FP64_PEAK_TFLOPS,
+                    "traffic": (pmc or {}).get("hbm_bytes_per_launch") if world == 1 else None,
+                    "kernel": "k_sweep3" if seam.max_causal >= 3 else "k_sweep<2>",
                     "kernel_ms": avg_kernel_s * 1e3,
-                    "alg_bytes_per_launch": alg_bytes}
-        fp64 = {"achieved": tm["flops"] / avg_kernel_s / 1e12 if avg_kernel_s > 0 else 0.0,
-                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "note": "FP64 flops per set calibrated from PMC instruction counts (FMA = 2); the kernel is "
-                        "VALU-issue bound, not FMA bound: see valu_busy"}
-        fp64["frac"] = fp64["achieved"] / FP64_PEAK_TFLOPS
-        if pmc and "valu_busy" in pmc:
-            fp64["valu_busy"] = pmc["valu_busy"]
-            fp64["valu_busy_source"] = "profiles/pmc_latest.json (rocprofv3 --pmc, same workload)"
+                    "flops_per_launch": flops, "flops_source": flops_src,
+                    "pmc_kernel_src_sha": (pmc or {}).get("kernel_src_sha"), "kernel_src_sha": kernel_src_sha()}
+        if pmc and world == 1:
+            roofline["valu_busy"] = pmc.get("valu_busy")
+            roofline["fp64_valu_share"] = pmc.get("fp64_valu_share")
+            if pmc.get("hbm_bytes_per_launch") and avg_kernel_s > 0:
+                gbs = pmc["hbm_bytes_per_launch"] / avg_kernel_s / 1e9
+                roofline["hbm"] = {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                                   "source": "PMC 2 x FETCH_SIZE + WRITE_SIZE per launch / kernel_ms"}
+        # SURVEY 8(d)'s per-configuration byte count, kept as a labelled
+        # diagnostic only: the kernel reuses each gathered operand from
+        # registers / LDS across 3^k assignments and 64 lanes, so these bytes
+        # never cross HBM and their "rate" is not bounded by any roof
+        alg_diag = {"bytes_per_launch": alg_bytes,
+                    "rate_GBs": alg_bytes / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0,
+                    "note": "SURVEY 8(d) 8*sum_s(|C_s|^2+|C_s|) per configuration; register/LDS-reused, not HBM traffic"}
         out = {
             "metric": "causal configurations evaluated/sec (whole node)",
             "value": value,
@@ -417,7 +576,8 @@ def main():
                        "parallelism": (f"config-shard x{world} + 1 {'RCCL' if backend == 'nccl' else backend} all-gather"
                             if use_dist else "single GPU")},
             "roofline": roofline,
-            "fp64": fp64,
+            "algorithmic_bytes_diagnostic": alg_diag,
+            "rccl_world": dist.get_world_size() if use_dist else 1,
             "setup_s": setup_s,
             "setup": {"synthetic_locus_s": t_synth, "gpu_model_setup_and_create_ms": pc.setup_info["setup_ms"],
                       "psd_added": pc.setup_info["psd_added"], "eigen_route": pc.setup_info["eigen_route"]},
@@ -433,6 +593,11 @@ def main():
             out["example_wall_s"] = w
             out["example_outputs_match_reference"] = same
             if not args.no_cpu_baseline:
+                # BASELINE configs[0] on the same box: the north star's >= 100x is
+                # cpu_baseline_example.wall_s / example_wall_s
+                out["cpu_baseline_example"] = cpu_baseline_example()
+                if w:
+                    out["cpu_baseline_example"]["speedup_vs_example_wall"] = out["cpu_baseline_example"]["wall_s"] / w
                 # the reference's N x N likelihood needs B and S': host eigen route
                 out["cpu_baseline"] = cpu_baseline(build_seam(args.workload), budget_s=args.cpu_budget)
         sys.stdout.flush()

@@ -120,6 +120,7 @@ typedef struct {
     int32_t eigen_route[2];    /* 1 if Sigma'_s was not positive definite (host eigen)   */
     double min_pivot_ratio[2]; /* smallest L D L^T pivot / largest |diagonal|            */
     double setup_ms;           /* wall time of the whole setup + create                  */
+    double spsq[2];            /* ||S'_s||^2 = z~^T D^-1 z~ (0 on the eigen route)       */
 } psx_setup_info;
 
 int psx_create_from_ld(const psx_ld_problem *prob, int device, psx_engine **out, psx_setup_info *info);

@@ -78,16 +78,54 @@ struct ParsedChunk {
     bool stopped = false;
 };
 
+// One `istream >> double` extraction (libstdc++ num_get::_M_extract_float +
+// __convert_to_v): an optional sign, digits with at most one '.', then - after
+// at least one digit - an 'e'/'E' with an optional sign and digits; the
+// collected characters must convert completely and finitely ("1e400", "-nan",
+// "inf", "1e+" fail; "0x10" yields 0 and stops at 'x').  Returns the end of
+// the characters consumed, or nullptr when the extraction fails.
+const char* extract_double(const char* s, const char* end, double& v) {
+    char buf[512];
+    size_t n = 0;
+    const char* p = s;
+    auto put = [&](char c) {
+        if (n + 1 < sizeof(buf)) buf[n++] = c;
+    };
+    if (p < end && (*p == '+' || *p == '-')) put(*p++);
+    bool mant = false, dec = false, sci = false;
+    while (p < end) {
+        const char c = *p;
+        if (isdigit((unsigned char)c)) {
+            put(c);
+            mant = true;
+        } else if (c == '.' && !dec && !sci) {
+            put('.');
+            dec = true;
+        } else if ((c == 'e' || c == 'E') && !sci && mant) {
+            put('e');
+            sci = true;
+            if (p + 1 < end && (p[1] == '+' || p[1] == '-')) put(*++p);
+        } else {
+            break;
+        }
+        p++;
+    }
+    if (n + 1 >= sizeof(buf)) return nullptr;  // a 500-character number: not an LD entry
+    buf[n] = 0;
+    char* e = nullptr;
+    v = strtod(buf, &e);
+    if (e == buf || *e != 0 || std::isinf(v)) return nullptr;
+    return p;
+}
+
 void parse_chunk(const char* s, const char* end, ParsedChunk& out) {
     out.v.reserve((size_t)(end - s) / 8 + 1);
     while (s < end) {
         while (s < end && isspace((unsigned char)*s)) s++;
         if (s >= end) break;
-        char c = *s;
-        if (!(isdigit((unsigned char)c) || c == '-' || c == '+' || c == '.')) { out.stopped = true; return; }
-        char* e = nullptr;
-        double v = strtod(s, &e);
-        if (e == s) { out.stopped = true; return; }
+        double v = 0;
+        const char* e = extract_double(s, end, v);
+        if (!e) { out.stopped = true; return; }
         out.v.push_back(v);
         s = e;
     }
@@ -414,7 +452,15 @@ int main(int argc, char* argv[]) {
         std::ofstream lf((outputFileName + "_log.txt").c_str(), std::ios::out | std::ios::app);  // util.cpp:183-187
         lf << std::exp(total) << std::endl;
     }
+    // postcal.cpp:1145-1148: addlogSpace (postcal.h:102-112) over postValues in index order
     double total_post = 0;
+    for (int i = 0; i < N; i++) {
+        const double a = total_post, b = post[i];
+        if (a == 0) { total_post = b; continue; }
+        if (b == 0) continue;
+        const double base = std::max(a, b);
+        total_post = (base - std::min(a, b) > 700) ? base : base + std::log(1 + std::exp(std::min(a, b) - base));
+    }
     printf("\nTotal Likelihood = %e SNP=%d \n", total_post, N);
     printf("total post as total likelihood log = %f\n", total);
     for (int i = 0; i < 2; i++) {

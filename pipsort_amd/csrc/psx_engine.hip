@@ -1224,6 +1224,7 @@ int create_impl(const psx_problem* p, const psx_ld_problem* ld, int device, psx_
                 info->eigen_route[s] = r.path;
                 info->min_pivot_ratio[s] = r.min_pivot_ratio;
             }
+            if (info) info->spsq[s] = r.path == 0 ? r.spsq : 0.0;
             if (r.path == 0) {
                 lowrank = false;
                 spsq += r.spsq;
@@ -1418,7 +1419,7 @@ int psx_run_exhaustive(psx_engine* e) {
     std::memset(&e->timing, 0, sizeof(e->timing));
     double gms = 0;
     int flag = 0;
-    if (fused_eligible(e) && !std::getenv("PSX_NO_FUSED_PASS")) {
+    if (fused_eligible(e)) {
         if ((rc = fused_pass(e, &flag))) return rc;
     } else {
         if ((rc = exhaustive_pass(e, false, &gms))) return rc;
@@ -1433,7 +1434,7 @@ int psx_run_exhaustive(psx_engine* e) {
 
 int psx_run_exhaustive_async(psx_engine* e) {
     HIPCHK(hipSetDevice(e->dev));
-    if (!fused_eligible(e) || std::getenv("PSX_NO_FUSED_PASS")) return psx_run_exhaustive(e);
+    if (!fused_eligible(e)) return psx_run_exhaustive(e);
     int flag = 0;
     return fused_pass(e, &flag, true);
 }

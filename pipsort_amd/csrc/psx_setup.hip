@@ -456,32 +456,34 @@ int chk(hipError_t e, const char* what, std::string* err) {
 }
 
 // enqueue the partial-pivot elimination of A (n x n, device) on st
-int enqueue_lu(double* A, int n, int* dswp, hipStream_t st) {
+// (returns -1 with *err set when a launch failed; the HIP error is read once, here)
+int enqueue_lu(double* A, int n, int* dswp, hipStream_t st, std::string* err) {
     for (int j = 0; j < n - 1; j++) {
         hipLaunchKernelGGL(k_lu_pivot, dim3(1), dim3(1024), 0, st, A, n, j, dswp);
         const int r = n - j - 1;
         hipLaunchKernelGGL(k_elim, dim3((r + kElimCols - 1) / kElimCols, (r + kElimRows - 1) / kElimRows),
                            dim3(kElimCols), 0, st, A, n, j, (double*)nullptr);
     }
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return chk(hipGetLastError(), "LU launch", err);
 }
 
 // enqueue the blocked swap-free elimination; *flag != 0 afterwards when some
 // column needed a row swap (A is then partly eliminated: recopy and pivot).
 // work: kPanel * n + kPanel doubles (panel multipliers, skipped-step marks)
-int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipStream_t st, bool check = true) {
-    if (hipMemsetAsync(flag, 0, sizeof(int), st) != hipSuccess) return -1;
+// Returns -1 with *err set when a launch failed (the HIP error is read once,
+// here), 1 when !check and the panel does not fit LDS (nothing enqueued).
+int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipStream_t st, std::string* err,
+                     bool check = true) {
+    if (chk(hipMemsetAsync(flag, 0, sizeof(int), st), "memset", err)) return -1;
     double* const sk = work + (size_t)kPanel * n;
     // panel width: the widest (<= kPanel) whose n rows fit in LDS; the global-
-    // memory panel kernel beyond that
-    static int lds_cap = -1;
-    if (lds_cap < 0) {
-        lds_cap = kPanelLds;
-        if (hipFuncSetAttribute((const void*)k_lu_panel_lds, hipFuncAttributeMaxDynamicSharedMemorySize, kPanelLds) !=
-            hipSuccess) {
-            (void)hipGetLastError();
-            lds_cap = 64 * 1024;
-        }
+    // memory panel kernel beyond that.  The attribute is set on every call: it is
+    // per device (a process may drive several) and cheap.
+    int lds_cap = kPanelLds;
+    if (hipFuncSetAttribute((const void*)k_lu_panel_lds, hipFuncAttributeMaxDynamicSharedMemorySize, kPanelLds) !=
+        hipSuccess) {
+        (void)hipGetLastError();
+        lds_cap = 64 * 1024;
     }
     int pw = kPanel;
     while (pw > 1 && (size_t)n * (pw + 2) * sizeof(double) > (size_t)lds_cap) pw--;
@@ -501,7 +503,7 @@ int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipSt
                            dim3(kTrCols, kTrGroups), 0, st, A, n, j0, nb, (const double*)work, (const double*)sk,
                            (const int*)flag);
     }
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return chk(hipGetLastError(), "LU launch", err);
 }
 
 }  // namespace
@@ -511,10 +513,9 @@ int lu_det_device(double* dA, int n, int* dswp, double* ddiag, hipStream_t st, d
     // blocked when the panel fits the LDS budget (PSX_LU_UNBLOCKED=1: per-column launches)
     int pw = kPanel;
     while (pw > 1 && (size_t)n * (pw + 1) * sizeof(double) > (size_t)(64 * 1024)) pw--;
-    static bool attr = false;
-    if (!attr && hipFuncSetAttribute((const void*)k_lu_panel_piv, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     kPanelLds) == hipSuccess)
-        attr = true;
+    // per call: the attribute is per device, and a process may drive several
+    const bool attr = hipFuncSetAttribute((const void*)k_lu_panel_piv, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          kPanelLds) == hipSuccess;
     (void)hipGetLastError();
     if (attr) {
         pw = kPanel;
@@ -541,8 +542,8 @@ int lu_det_device(double* dA, int n, int* dswp, double* ddiag, hipStream_t st, d
         if (!rc) rc = chk(hipStreamSynchronize(st), "LU sync", err);
         hipFree(work);
         if (rc) return rc;
-    } else if (enqueue_lu(dA, n, dswp, st)) {
-        return chk(hipGetLastError(), "LU launch", err);
+    } else if (enqueue_lu(dA, n, dswp, st, err)) {
+        return -1;
     }
     hipLaunchKernelGGL(k_get_diag, dim3((n + 255) / 256), dim3(256), 0, st, dA, n, ddiag);
     std::vector<double> diag(n);
@@ -604,7 +605,7 @@ int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, dou
             if (try_fused) {
                 if ((rc = chk(hipMemcpyAsync(dz, z, M * sizeof(double), hipMemcpyHostToDevice, st), "z upload", err)))
                     break;
-                if (enqueue_lu_fused(dA, M, dcol, dflag, dz, st)) { rc = chk(hipGetLastError(), "LU launch", err); break; }
+                if (enqueue_lu_fused(dA, M, dcol, dflag, dz, st, err)) { rc = -1; break; }
                 hipLaunchKernelGGL(k_get_diag, dim3((M + 255) / 256), dim3(256), 0, st, dA, M, ddiag);
                 if ((rc = chk(hipMemcpyAsync(udiag.data(), ddiag, M * sizeof(double), hipMemcpyDeviceToHost, st),
                               "copy", err)) ||
@@ -648,8 +649,8 @@ int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, dou
                 break;
             // elimination without pivoting: the blocked panels with the pivot check off
             // (per-column launches when the panel does not fit LDS)
-            const int lrc = enqueue_lu_fused(dA, M, dcol, dflag, dz, st, false);
-            if (lrc < 0) { rc = chk(hipGetLastError(), "elimination launch", err); if (!rc) rc = -1; break; }
+            const int lrc = enqueue_lu_fused(dA, M, dcol, dflag, dz, st, err, false);
+            if (lrc < 0) { rc = -1; break; }
             if (lrc > 0)
                 for (int j = 0; j < M - 1; j++) {
                     const int r = M - j - 1;

@@ -325,7 +325,6 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // syn1000c3, tools/ca_sweep.sh: ca = 4 at world 1, 2 at worlds 2 and 4, 1 at
     // world 8).
     static const double kTarget = [] {  // units per shard the a-chunk is sized for
-        if (const char* v = std::getenv("PSX_K3_UNITS")) return std::atof(v);
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) {
             hipDeviceProp_t pr;
@@ -336,7 +335,6 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     }();
     ca = (int)std::lround(total_a / (kTarget * world));
     ca = std::min(ca, 4);
-    if (const char* v = std::getenv("PSX_K3_CA")) ca = std::atoi(v);
     ca = std::max(1, std::min(64, ca));
     // Every union triple x < y < z belongs to exactly one unit family, by which
     // of its members share a 64-block:
@@ -366,21 +364,12 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     for (auto& u : all) wsum += u.work;
     double lo = wsum * rank / world, hi = wsum * (rank + 1) / world, run = 0;
     mine.clear();
-    // Contiguous work bands in enumeration order (C, K, a).  PSX_K3_DEAL=1 deals
-    // the units cyclically instead (every shard the same mix of tiles and unit
-    // kinds).  Measured on two boxes (world-8 rehearsal, 3 alternating reps
-    // each): dealing 4 % faster on one, 5 % slower on the other — the per-rank
-    // pattern is box-dependent, so the bands stay.
-    static const bool deal = std::getenv("PSX_K3_DEAL") != nullptr;
-    if (deal) {
-        for (size_t i = 0; i < all.size(); i++)
-            if ((int)(i % (size_t)world) == rank) mine.push_back(all[i]);
-    } else {
-        for (auto& u : all) {
-            double mid = run + 0.5 * u.work;
-            if (mid >= lo && mid < hi) mine.push_back(u);
-            run += u.work;
-        }
+    // Contiguous work bands in enumeration order (C, K, a).  (Dealing the units
+    // cyclically instead was measured box-dependent, -4 % .. +5 % at world 8.)
+    for (auto& u : all) {
+        double mid = run + 0.5 * u.work;
+        if (mid >= lo && mid < hi) mine.push_back(u);
+        run += u.work;
     }
     double bytes_cls[4][4][4];
     for (int x = 1; x < 4; x++)
@@ -433,45 +422,8 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // workgroup i running on XCD (i + launch offset) % 8, so each 4 MB L2 serves
     // ~1/8 of the tile rows — measured neutral (r01y, worlds 1-8) once the next
     // step's tile row is prefetched; not used.)
-    // Tail split (PSX_K3_TAIL="frac:q"): the units that make up the last `frac`
-    // of this shard's work are cut into q b-walk ranges (steps [64i/q, 64(i+1)/q);
-    // a folded diagonal unit halves them), so the launch's last dispatch rounds
-    // are made of short pieces and the 2048 wave slots drain together.  Each
-    // piece repeats the unit prologue and writes its own records (the merge
-    // folds them like any other unit's).  Totals above are unchanged.
-    double tail_frac = 0.0;
-    int tail_q = 1;
-    if (const char* v = std::getenv("PSX_K3_TAIL")) {
-        tail_frac = std::atof(v);
-        if (const char* c = std::strchr(v, ':')) tail_q = std::atoi(c + 1);
-    } else if (std::getenv("PSX_K3_SPLIT")) {  // former option: last round in halves
-        tail_frac = -1.0;
-        tail_q = 2;
-    }
-    tail_q = std::max(1, std::min(32, tail_q));
-    if (tail_q > 1 && tail_frac != 0.0 && !mine.empty()) {
-        size_t cut = mine.size();
-        if (tail_frac < 0) {
-            const size_t slots = (size_t)(kTarget / 3.5);
-            cut = mine.size() > 2 * slots ? mine.size() - slots : mine.size();
-        } else {
-            double tot = 0, run = 0;
-            for (auto& u : mine) tot += u.work;
-            while (cut > 0 && run + mine[cut - 1].work <= tail_frac * tot) run += mine[--cut].work;
-        }
-        std::vector<PlanUnit> out(mine.begin(), mine.begin() + cut);
-        for (size_t i = cut; i < mine.size(); i++)
-            for (int p = 0; p < tail_q; p++) {
-                PlanUnit h = mine[i];
-                h.work /= tail_q;
-                h.j0 = 64 * p / tail_q;
-                h.j1 = 64 * (p + 1) / tail_q;
-                out.push_back(h);
-            }
-        std::stable_sort(out.begin() + cut, out.end(),
-                         [](const PlanUnit& x, const PlanUnit& y) { return x.work > y.work; });
-        mine.swap(out);
-    }
+    // (Splitting the last dispatch rounds into shorter b-walk pieces was
+    // measured +1-6 % slower: a unit's fixed cost is ~11 us)
     return 0;
 }
 

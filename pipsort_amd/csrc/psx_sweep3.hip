@@ -405,11 +405,7 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
         for (int j = j0; j < j1; j++) {
             const double gcur0 = gnx.x, gcur1 = gnx.y, mcur0 = mnx.x, mcur1 = mnx.y;
             const int2 ncur = nnx;
-#ifndef PSX_K3_NOLOAD_EXPERIMENT
             if (j + 1 < j1) {
-#else
-            if (false) {  // timing experiment only: results invalid
-#endif
                 gnx = g01[(j + 1) * 64];
                 mnx = m01[(j + 1) * 64];
                 nnx = bnn[(j + 1) * 64];

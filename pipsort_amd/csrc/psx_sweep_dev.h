@@ -137,20 +137,11 @@ __device__ __forceinline__ void split2(double h, double rP, int& n, double& mu) 
     mu = exp2_frac(h - fl) * rP;
 }
 
-// Record stores.  PSX_NT_REC: non-temporal (streaming) stores, so the records
-// (read once, by the merge, after the launch) do not sit dirty in L2 until the
-// end-of-kernel release writes them back.
+// Record stores (plain stores: non-temporal ones were measured neutral at
+// world 1 and slower at world 8).
 template <typename T>
 __device__ __forceinline__ void store_rec(T* dst, const T& v) {
-#ifdef PSX_NT_REC
-    static_assert(sizeof(T) % 8 == 0, "record of 8-byte words");
-    const unsigned long long* s = reinterpret_cast<const unsigned long long*>(&v);
-    unsigned long long* d = reinterpret_cast<unsigned long long*>(dst);
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(T) / 8); i++) __builtin_nontemporal_store(s[i], d + i);
-#else
     *dst = v;
-#endif
 }
 
 // record slot i goes to its CSR position pos[i] (merges then read contiguous runs)

@@ -90,6 +90,7 @@ class SetupInfo(ctypes.Structure):
         ("eigen_route", ctypes.c_int32 * 2),
         ("min_pivot_ratio", ctypes.c_double * 2),
         ("setup_ms", ctypes.c_double),
+        ("spsq", ctypes.c_double * 2),
     ]
 
     def as_dict(self):

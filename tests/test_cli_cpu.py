@@ -89,3 +89,25 @@ def test_ld_parser_stops_at_first_rejected_token(tmp_path, stop_at):
         m = int(np.sqrt(stop_at))
         assert r.returncode == 1
         assert f"LD matrix is size {m} x {m} but zscores has {M} snps" in r.stdout
+
+
+@pytest.mark.parametrize("tok,parsed", [("-nan", 399), ("-inf", 399), ("nan", 399), ("inf", 399), ("1e400", 399),
+                                        ("-1e400", 399), ("1e+", 399), ("+-1", 399), ("-", 399), ("0x10", 400),
+                                        ("1e5e3", 400), ("x1", 399)])
+def test_ld_parser_matches_istream_extraction(tmp_path, tok, parsed):
+    """util.cpp:94 `while (file >> data)`: libstdc++'s num_get collects a sign,
+    digits with one '.', and an exponent, and fails on a partial conversion or an
+    overflow to inf (checked with a g++ probe: "0x10" yields 0 then stops at 'x';
+    "1e5e3" yields 1e5 then stops; nan / inf / 1e400 / "1e+" stop at once)."""
+    from pipsort_amd import synth
+    M = 30
+    ld, z, names, rows, _ = synth.syn_v1(M)
+    d = synth.write_locus(str(tmp_path / "loc"), ld, z, names, rows)
+    p = os.path.join(d, "syn0.ld")
+    toks = open(p).read().split()
+    toks[399] = tok
+    open(p, "w").write(" ".join(toks) + "\n")
+    r = run(["-c", "2", "-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "snp_map", "-n", "10000,8000", "-o", "out"], d)
+    m = int(parsed ** 0.5)
+    assert r.returncode == 1
+    assert f"LD matrix is size {m} x {m} but zscores has {M} snps" in r.stdout

@@ -59,3 +59,39 @@ def test_bench_rccl_path_world1(gpu):
     assert "RCCL" in out["config"]["parallelism"]
     assert out["configs_checked"] == out["config"]["configs_per_step"] == 179_701
     assert out["sss"]["walk_iterations"] == 2 and out["sss"]["walk_configs"] == 23_993
+
+
+def test_bench_gpus2_launches_its_own_ranks(gpu):
+    """`python bench.py --gpus 2` with no launcher (WORLD_SIZE unset) starts two
+    ranks itself (a torch.distributed.run child, before any GPU call) and the
+    line reports both: n_gpus 2, a 2-rank process group, every configuration of
+    the locus counted once after the exchange.  gloo lets the two ranks share
+    this box's one GPU; on a node each rank gets its own GPU over RCCL."""
+    env = dict(os.environ, PSX_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--workload", "syn200c2", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["rccl_world"] == 2
+    assert out["configs_checked"] == out["config"]["configs_per_step"] == 179_701
+
+
+def test_bench_gpus_more_than_visible_fails(gpu):
+    """With the RCCL backend, asking for more GPUs than are visible fails
+    non-zero instead of silently measuring fewer."""
+    import torch
+    env = dict(os.environ)
+    env.pop("PSX_DIST_BACKEND", None)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    n = torch.cuda.device_count() + 1
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "1", "--warmup", "0",
+           "--workload", "syn200c2", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and r.stdout == ""
+    assert f"--gpus {n} but only" in r.stderr

@@ -228,6 +228,24 @@ def _elim_pivots(a):
     return np.diag(a).copy()
 
 
+def _elim_spsq(a, z):
+    """||S'||^2 of the setup's step 2: the same unpivoted elimination with z's
+    forward solve riding along (z_i - l_ij z_j, unfused), then sum z~_i^2 / D_i
+    in index order."""
+    a = np.array(a, dtype=np.float64)
+    z = np.array(z, dtype=np.float64)
+    n = a.shape[0]
+    for j in range(n - 1):
+        l = a[j + 1:, j] / a[j, j]
+        a[j + 1:, j + 1:] -= np.outer(l, a[j, j + 1:])
+        z[j + 1:] -= l * z[j]
+    piv = np.diag(a)
+    q = 0.0
+    for i in range(n):
+        q += float(z[i]) * float(z[i]) / float(piv[i])
+    return q
+
+
 @pytest.mark.parametrize("M,glob", [(1, 0), (2, 0), (15, 0), (16, 0), (17, 0), (33, 0), (300, 0), (1000, 0),
                                     (2000, 0), (17, 1), (300, 1)])
 def test_blocked_swap_free_elimination_bit_identical(gpu, M, glob, monkeypatch):
@@ -260,6 +278,8 @@ def test_blocked_swap_free_elimination_bit_identical(gpu, M, glob, monkeypatch):
         piv = _elim_pivots(a)
         dmax = np.abs(np.diag(a)).max()
         assert info["min_pivot_ratio"][s] == piv.min() / dmax, (s, info["min_pivot_ratio"][s], piv.min() / dmax)
+        if M <= 300:  # z's forward solve (it feeds K = -||S'||^2 / 2): bit-identical too
+            assert _bits(info["spsq"][s]) == _bits(_elim_spsq(a, z[s])), (s, info["spsq"][s], _elim_spsq(a, z[s]))
     pc.close()
 
 
@@ -305,4 +325,6 @@ def test_blocked_step2_elimination_bit_identical(gpu):
             piv = _elim_pivots(sym)
             dmax = np.abs(np.diag(sym)).max()
             assert info["min_pivot_ratio"][s] == piv.min() / dmax, (s, info["min_pivot_ratio"][s], piv.min() / dmax)
+            zs = np.asarray(z[s], dtype=np.float64)
+            assert _bits(info["spsq"][s]) == _bits(_elim_spsq(sym, zs)), (s, info["spsq"][s], _elim_spsq(sym, zs))
         pc.close()

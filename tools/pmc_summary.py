@@ -31,7 +31,10 @@ per = collections.defaultdict(list)
 for (p, c, disp), v in agg.items():
     per[c].append(v)
 c = {k: sum(v) / len(v) for k, v in per.items()}
-out = {"workload": workload, "kernel": name, "counters_per_dispatch": c}
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import bench  # noqa: E402  (kernel_src_sha: which build these counters describe)
+
+out = {"workload": workload, "kernel": name, "kernel_src_sha": bench.kernel_src_sha(), "counters_per_dispatch": c}
 if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
     out["hbm_bytes_per_launch"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
     out["hbm_bytes_note"] = "2 x FETCH_SIZE + WRITE_SIZE (KB -> B), gfx950 FETCH_SIZE half-count correction"
