@@ -528,9 +528,9 @@ def main():
         # achieved = FP64 operations of one launch (PMC SQ_INSTS_VALU_FLOPS_FP64,
         # FMA = 2, per wave instruction x 64 lanes, collected on this build) / the
         # launch's average duration measured here (HIP events of its own dispatch).
-        if pmc and pmc.get("fp64_flops_per_launch"):
+        if pmc and pmc.get("fp64_flop_insts_per_launch"):
             # counters of the world-1 launch; a shard of `world` equal-work slices does 1/world of it
-            flops = pmc["fp64_flops_per_launch"] * 64.0 / world
+            flops = pmc["fp64_flop_insts_per_launch"] * 64.0 / world
             flops_src = ("PMC SQ_INSTS_VALU_FLOPS_FP64 x 64 (profiles/pmc_latest.json, same kernel build)"
                          + (f" / {world} (this rank's shard)" if world > 1 else ""))
         else:

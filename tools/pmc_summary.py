@@ -39,7 +39,7 @@ if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
     out["hbm_bytes_per_launch"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
     out["hbm_bytes_note"] = "2 x FETCH_SIZE + WRITE_SIZE (KB -> B), gfx950 FETCH_SIZE half-count correction"
 if "SQ_INSTS_VALU_FLOPS_FP64" in c:
-    out["fp64_flops_per_launch"] = c["SQ_INSTS_VALU_FLOPS_FP64"]
+    out["fp64_flop_insts_per_launch"] = c["SQ_INSTS_VALU_FLOPS_FP64"]  # per wave instruction (FMA = 2); x 64 lanes = FP64 operations
 if "SQ_INSTS_VALU" in c and "GRBM_GUI_ACTIVE" in c:
     # every wave64 VALU instruction occupies its SIMD for 4 cycles; 1024 SIMDs.
     # GRBM_GUI_ACTIVE is summed over the 8 XCDs (8 x 2.4 GHz x kernel time), so
