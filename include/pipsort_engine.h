@@ -75,6 +75,7 @@ typedef struct {
     double alg_bytes;       /* algorithmic bytes of the dominant kernel      */
     double flops;           /* FP64 operation estimate of the dominant kernel              */
     int32_t exact_rerun;    /* 1 if the sweep was redone with the exact notSharedLL variant */
+    int32_t robust_units;   /* k = 3 units redone by the robust variant (cumulative since create) */
 } psx_timing;
 
 int32_t psx_abi_version(void);

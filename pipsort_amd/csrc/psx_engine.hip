@@ -1468,6 +1468,7 @@ int psx_sync(psx_engine* e, int32_t* exact_needed) {
     e->timing.alg_bytes = top->alg_bytes + top->fused_bytes;
     e->timing.flops = top->flops + top->fused_flops;
     e->timing.exact_rerun = sticky;
+    if (psx::sweep_redo_count(e->plans, &e->timing.robust_units)) return fail(PSX_EHIP, psx::sweep_error());
     SetRec st;
     std::memcpy(&st, e->hstat, sizeof(SetRec));
     e->timing.configs = (uint64_t)(st.npat + 0.5);
@@ -1503,6 +1504,7 @@ int fill_timing(psx_engine* e, double gms, int flag) {
     }
     e->timing.merge_ms = st.merge_ms;
     e->timing.exact_rerun = flag;
+    if (psx::sweep_redo_count(e->plans, &e->timing.robust_units)) return fail(PSX_EHIP, psx::sweep_error());
     SetRec s;
     std::memcpy(&s, e->hstat, sizeof(SetRec));
     e->timing.configs = (uint64_t)(s.npat + 0.5);

@@ -83,6 +83,7 @@ struct Sweep3Args {
     double rho, pit0;          // pit[nsh] = pit0 * rho^nsh (prior per member is multiplicative)
     int U, ldg, pad, Ck;
     unsigned long long* trace = nullptr;  // diagnostics (PSX_UNIT_TRACE): per unit {start, end, hw id, unit}
+    int* redo_count = nullptr;            // units redone by the robust variant (cumulative)
 };
 struct Level2Blocks;  // psx_sweep_dev.h
 int launch_sweep3(bool allpres, const Sweep3Args& A, int n_units, const int4* units, Acc5* rec, SetRec* srec,
@@ -110,6 +111,7 @@ struct SweepPlanCache {
     bool allpres = false;                    // every union SNP is in both studies
     int skew_ldg = 0;
     const double* skew_src[2] = {nullptr, nullptr};
+    int* d_redo = nullptr;  // k = 3 units redone by the robust variant since creation
     int* d_flag = nullptr;  // raised when a set needs the EXACT notSharedLL variant
     bool own_flag = true;   // false: d_flag lives in the engine's status block
 };
@@ -141,6 +143,7 @@ int sweep_kernel(SweepPlanCache& cache, SweepPlan& plan, hipStream_t stream, con
 // the record buffer of a parity (allocating the second one on first use)
 Acc5* plan_records(SweepPlan& plan, int parity);
 int sweep_flag(SweepPlanCache& cache, int* flag);                          // after sync
+int sweep_redo_count(SweepPlanCache& cache, int* count);                   // after sync
 int sweep_stats(SweepPlanCache& cache, int k, int U, int rank, int world, SweepStats* st);  // after sync
 void sweep_free(SweepPlanCache& cache);
 int launch_merge_members(const Acc5* rec, const int* ptr, const int* idx, const int* rows, int n_rows, Acc5* acc,

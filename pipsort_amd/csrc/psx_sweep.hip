@@ -535,6 +535,7 @@ static Sweep3Args sweep3_args(const SweepPlanCache& C, const SweepArgs& a, int U
     S3.pit0 = A.pit[0];
     S3.rho = A.pit[0] > 0 ? A.pit[1] / A.pit[0] : 0.0;
     S3.U = U; S3.ldg = ldg; S3.Ck = A.Ck;
+    S3.redo_count = C.d_redo;
     return S3;
 }
 
@@ -581,6 +582,10 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
         hipLaunchKernelGGL(k_build_skew, dim3(ntile, 64), dim3(64), 0, st, s ? a.G1 : a.G0, ldg, nblk, C.d_skew[s]);
         SWCHK(hipGetLastError());
     }
+    if (!C.d_redo) {
+        SWCHK(hipMalloc(&C.d_redo, sizeof(int)));
+        SWCHK(hipMemsetAsync(C.d_redo, 0, sizeof(int), st));
+    }
     {  // the a-independent {b, c} weights of every k = 3 step
         Sweep3Args S3 = sweep3_args(C, a, U, ldg);
         SWCHK(hipMalloc(&C.d_mu01, sizeof(double2) * (size_t)ntile * 4096));
@@ -598,6 +603,12 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
 int sweep_begin(SweepPlanCache& C, hipStream_t st) {
     if (!C.d_flag) SWCHK(hipMalloc(&C.d_flag, sizeof(int)));
     SWCHK(hipMemsetAsync(C.d_flag, 0, sizeof(int), st));
+    return 0;
+}
+
+int sweep_redo_count(SweepPlanCache& C, int* count) {
+    *count = 0;
+    if (C.d_redo) SWCHK(hipMemcpy(count, C.d_redo, sizeof(int), hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -793,6 +804,7 @@ void sweep_free(SweepPlanCache& C) {
     hipFree(C.d_bcn); C.d_bcn = nullptr;
     hipFree(C.d_g01); C.d_g01 = nullptr;
     hipFree(C.d_mu01); C.d_mu01 = nullptr;
+    hipFree(C.d_redo); C.d_redo = nullptr;
     if (C.own_flag) hipFree(C.d_flag);
     C.d_flag = nullptr;
 }

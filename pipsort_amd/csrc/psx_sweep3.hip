@@ -125,6 +125,25 @@ __device__ __forceinline__ Acc5 lacc_rec(const LAcc& a, int Ck, double pit0) {
     return r;
 }
 
+// fast-variant accumulator (shift m; W0, W1, W2 = prior-weighted sums over
+// the member's assignments study 0 only / study 1 only / both, W2 without the
+// member's own rho) -> merge record (Acc5 convention, as lacc_rec)
+__device__ __forceinline__ Acc5 wrec(int m, double W0, double W1, double W2, double sl, double ns, double rho, int Ck,
+                                     double pit0) {
+    Acc5 r;
+    const double sh = rho * W2;
+    r.post0 = (W0 + sh) * pit0;
+    r.post1 = (W1 + sh) * pit0;
+    r.shared = sh * pit0;
+    r.sll = sl;
+    r.nsll = ns;
+    r.mP = (r.post0 + r.post1 != 0.0) ? m + Ck : EMPTY;
+    r.mS = (sl != 0.0) ? m : EMPTY;
+    r.mN = (ns != 0.0) ? m : EMPTY;
+    r.pad = 0;
+    return r;
+}
+
 // b-block terms of SNP v (v space) in study s: 1/A_bb, y_b / 2, the {b}
 // quadratic form and its pivot factor (x the c step's rsd / 2)
 struct BTerms {
@@ -214,18 +233,14 @@ union SweepSmem {  // a block runs either a k = 3 unit or a level-2 unit
     SweepUnitSmem u2;
 };
 
+// One k = 3 unit, ROBUST variant: every step's subset weights are taken
+// relative to the set's own top exponent (n_abc per study) and the lane / slot
+// accumulators shift lazily, so any dynamic range is handled.  Run for the
+// units the fast variant (below) flags.
 template <bool ALLPRES>
-__global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const int4* __restrict__ units,
-                                                  Acc5* __restrict__ rec, SetRec* __restrict__ srec, int rec_stride,
-                                                  int* __restrict__ flag, const int* __restrict__ pos, int nk3,
-                                                  TileArgs A2, const int4* __restrict__ units2,
-                                                  Acc5* __restrict__ rec2, SetRec* __restrict__ srec2,
-                                                  const int* __restrict__ pos2) {
-    __shared__ SweepSmem sm;
-    if ((int)blockIdx.x >= nk3) {  // level-2 units ride in the same launch, after the k = 3 units
-        sweep_unit<2, false>(A2, blockIdx.x - nk3, units2, rec2, srec2, 128, flag, pos2, sm.u2);
-        return;
-    }
+__device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit, const int4* __restrict__ units,
+                                                Acc5* __restrict__ rec, SetRec* __restrict__ srec, int rec_stride,
+                                                int* __restrict__ flag, const int* __restrict__ pos, SweepSmem& sm) {
     double (&tab)[256] = sm.s3.tab;
     double (&bH)[2][64] = sm.s3.bH;
     double (&bR)[2][64] = sm.s3.bR;
@@ -249,9 +264,7 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
     double (&g1ac)[2][64] = sm.s3.g1ac;
     int (&sPos)[3][64] = sm.s3.sPos;
 
-    const int unit = blockIdx.x;  // grid position = unit index: XCD = unit % 8 (plan_units3c)
     const int t = threadIdx.x;
-    const unsigned long long t_start = A.trace ? wall_clock64() : 0ull;
     const int4 un = units[unit];
     const int a0 = un.x, a1 = un.y, K = un.z & 0xffff, C = un.w & 0xffff;
     // b-walk steps of this (half) unit.  A diagonal tile (K == C) is walked
@@ -326,8 +339,6 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
         }
     }
 
-    unsigned long long t_ph[4] = {0ull, 0ull, 0ull, 0ull};  // diagnostics: phases of the first a
-    if (A.trace) t_ph[0] = wall_clock64();
     for (int ai = 0; ai < a1 - a0; ai++) {
         const int va = a0 + ai, ua = va - pad;  // a0 >= pad: a is always a real SNP
         const unsigned pa = A.pres[ua];
@@ -398,7 +409,6 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
         LAcc accA;
         lacc_zero(accA);
         __syncthreads();  // (a, b) terms visible
-        if (A.trace && ai == 0) t_ph[1] = wall_clock64();
 
         // the next step's skewed Sigma~ entries and {b, c} weights are loaded one
         // step ahead (L2 / MALL latency is longer than the VALU work between)
@@ -546,12 +556,10 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
             // compiler must keep program order (no lgkmcnt drain per step)
             __builtin_amdgcn_wave_barrier();
         }
-        if (A.trace && ai == 0) t_ph[2] = wall_clock64();
         Acc5 ra = lacc_rec(accA, A.Ck, A.pit0);
         wave_fold_acc(ra);
         const int qa = sPos[2][ai];
         if (t == 0 && qa >= 0) store_rec(rec + qa, ra);
-        if (A.trace && ai == 0) t_ph[3] = wall_clock64();
     }
     __syncthreads();
     if (sPos[0][t] >= 0) store_rec(rec + sPos[0][t], lacc_rec(accC, A.Ck, A.pit0));
@@ -577,6 +585,400 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
     sr.npat = npat;
     wave_fold_set(sr);
     if (t == 0) store_rec(srec + unit, sr);
+}
+
+constexpr int kMaxRefGap = 960;  // fast variant: largest n_abc - n_ac (bits, both studies) it accepts
+
+// One k = 3 unit, FAST variant.  All of a lane's subset weights for one a are
+// taken relative to R_s = n_{ac} (the {a, c} exponent of study s, fixed for the
+// whole b-walk), so per step only the four weights that involve b are rescaled
+// and the accumulators need no per-step shift: the a accumulator sits at G =
+// R_0 + R_1, the c accumulator and noCausal move their shift once per a, and
+// every b slot is moved once per a to the wave's largest G.  Weights relative
+// to 2^R stay below 2^(n_abc - n_ac + 2); a unit in which some set exceeds
+// kMaxRefGap bits over both studies (a very strong b given {a, c}) is redone by
+// the ROBUST variant in the same block.
+//
+// The 27 assignments are folded in factored form (E_s[m]: weight of subset m
+// of {a, b, c}, bit 0 a, bit 1 b, bit 2 c; P_s = E_s without c, Q_s = with c):
+//  * members a, b: for the 9 (x_a, x_b), with c marginalised,
+//      Pl = Q0[al] (P1 + Q1)[be] + P0[al] Q1[be],  Pw = Q0[al] (P1 + rho Q1)[be] + P0[al] Q1[be]
+//  * member c: bilinear forms Q0' M P1 etc. with M = m (x) m over (a, b),
+//      m = [[0, 1], [1, rho]] (prior-weighted) or [[0, 1], [1, 1]] (LL sums)
+// (101 VALU operations instead of 27 products and ~90 partial sums).  Each
+// member's own rho (x = 2) is applied when its record is written.
+template <bool ALLPRES>
+__device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, const int4* __restrict__ units,
+                                                 Acc5* __restrict__ rec, SetRec* __restrict__ srec, int rec_stride,
+                                                 int* __restrict__ flag, const int* __restrict__ pos, SweepSmem& sm,
+                                                 bool& redo) {
+    double (&tab)[256] = sm.s3.tab;
+    double (&bH)[2][64] = sm.s3.bH;
+    double (&bR)[2][64] = sm.s3.bR;
+    double (&abG)[2][64] = sm.s3.abG;
+    double (&abD)[2][64] = sm.s3.abD;
+    double (&abI)[2][64] = sm.s3.abI;
+    double (&abW)[2][64] = sm.s3.abW;
+    double (&abH)[2][64] = sm.s3.abH;
+    double (&abR)[2][64] = sm.s3.abR;
+    double (&abMu)[2][64] = sm.s3.abMu;
+    double (&abMuB)[2][64] = sm.s3.abMuB;
+    int (&abN)[2][64] = sm.s3.abN;
+    double (&bW)[64] = sm.s3.bW;
+    double (&sW0)[64] = sm.s3.sP0;  // b slots: W0, W1, W2 (own rho deferred), sharedLL, notSharedLL
+    double (&sW1)[64] = sm.s3.sP1;
+    double (&sW2)[64] = sm.s3.sSh;
+    double (&sSl)[64] = sm.s3.sSl;
+    double (&sNs)[64] = sm.s3.sNs;
+    int (&sM)[64] = sm.s3.sM;
+    double (&g1ab)[2][64] = sm.s3.g1ab;
+    double (&g1ac)[2][64] = sm.s3.g1ac;
+    int (&sPos)[3][64] = sm.s3.sPos;
+
+    const int t = threadIdx.x;
+    const unsigned long long t_start = A.trace ? wall_clock64() : 0ull;
+    const int4 un = units[unit];
+    const int a0 = un.x, a1 = un.y, K = un.z & 0xffff, C = un.w & 0xffff;
+    const bool diag = K == C;
+    const int j0 = diag ? 1 + (un.z >> 17) : un.z >> 16;
+    const int j1 = diag ? 1 + (un.w >> 17) : un.w >> 16;
+    const int pad = A.pad, ldg = A.ldg;
+    const int tile = C * (C + 1) / 2 + K;
+    const double rho = A.rho;
+
+    // ---- unit prologue (as the robust variant) -------------------------------------
+    for (int i = t; i < 256; i += 64) tab[i] = A.tab[i];
+    const int vbl = 64 * K + t, ubl = vbl - pad;
+    const bool okb = vbl >= pad;
+    const unsigned pbl = okb ? A.pres[ubl] : 0u;
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        const BTerms b = b_terms<ALLPRES>(A, s, vbl);
+        bH[s][t] = b.H;
+        bR[s][t] = b.R;
+    }
+    bW[t] = memb_weight(pbl);
+    sM[t] = EMPTY;
+    sW0[t] = sW1[t] = sW2[t] = sSl[t] = sNs[t] = 0.0;
+
+    const int vc = 64 * C + t, uc = vc - pad;
+    const bool okc = vc >= pad;
+    const unsigned pcm = okc ? A.pres[uc] : 0u;
+    double Acc[2], yc[2], chic[2], muC[2];
+    int nC[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        chic[s] = (okc && (ALLPRES || ((pcm >> s) & 1u))) ? 1.0 : 0.0;
+        Acc[s] = okc ? A.Ad[s][uc] : 1.0;
+        yc[s] = okc ? A.ys[s][uc] : 0.0;
+        muC[s] = okc ? A.muS[s][uc] * chic[s] : 0.0;
+        nC[s] = okc ? A.nS[s][uc] : 0;
+    }
+    const double wc = memb_weight(pcm);
+
+    // c accumulator (shift mC), noCausal (shifts m0, m1), redo gap
+    int mC = EMPTY, m0 = EMPTY, m1 = EMPTY, dmax = 0;
+    double cW0 = 0.0, cW1 = 0.0, cW2 = 0.0, cSl = 0.0, cNs = 0.0;
+    double nc0 = 0.0, nc1 = 0.0, npat = 0.0;
+    const double2* g01 = A.g01 + (size_t)tile * 4096 + t;
+    const double2* m01 = A.mu01 + (size_t)tile * 4096 + t;
+    const int2* bnn = A.bcn + (size_t)tile * 4096 + t;
+    {
+        const size_t rbase = (size_t)unit * rec_stride;
+        sPos[0][t] = pos[rbase + t];
+        sPos[1][t] = pos[rbase + 64 + t];
+        sPos[2][t] = (t < a1 - a0) ? pos[rbase + 128 + t] : -1;
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            g1ab[s][t] = okb ? A.G[s][(size_t)(a0 - pad) * ldg + ubl] : 0.0;
+            g1ac[s][t] = okc ? A.G[s][(size_t)(a0 - pad) * ldg + uc] : 0.0;
+        }
+    }
+
+    unsigned long long t_ph[4] = {0ull, 0ull, 0ull, 0ull};  // diagnostics: phases of the first a
+    if (A.trace) t_ph[0] = wall_clock64();
+    for (int ai = 0; ai < a1 - a0; ai++) {
+        const int va = a0 + ai, ua = va - pad;
+        const unsigned pa = A.pres[ua];
+        double l1[2], D1[2], w1h[2], Ep[2][4];  // Ep: {}, {a}, {c}, {a,c} relative to 2^R
+        int R[2];
+        double2 gnx = g01[j0 * 64], mnx = m01[j0 * 64];
+        int2 nnx = bnn[j0 * 64];
+        __syncthreads();  // previous a's (a, b) terms and slots fully consumed
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const double chia = (ALLPRES || ((pa >> s) & 1u)) ? 1.0 : 0.0;
+            const double ya = A.ys[s][ua];
+            const double ra = rsqrt_nr(A.Ad[s][ua]);
+            const double iAaa = ra * ra;
+            const double ha = ya * ya * iAaa;
+            const double rPa = ra * A.rsd[s] * chia;
+            int nA;
+            double muA;
+            split3(ha, rPa, tab, nA, muA);
+            {
+                const double Gab = ai ? (okb ? A.G[s][(size_t)ua * ldg + ubl] : 0.0) : g1ab[s][t];
+                const double Abb = okb ? A.Ad[s][ubl] : 1.0;
+                const double yb = okb ? A.ys[s][ubl] : 0.0;
+                const double l = Gab * iAaa;
+                const double Dab = fma(-l, Gab, Abb);
+                const double rab = rsqrt_nr(Dab);
+                const double wab = fma(-l, ya, yb);
+                const double hab = fma(wab * wab, rab * rab, ha);
+                const bool chib = okb && (ALLPRES || ((pbl >> s) & 1u));
+                const double rPab = chib ? rPa * rab * A.rsd[s] : 0.0;
+                int nAB, nB;
+                double muAB, muB;
+                split3(hab, rPab, tab, nAB, muAB);
+                split3(bH[s][t], bR[s][t] * (2.0 / A.rsd[s]), tab, nB, muB);
+                abG[s][t] = Gab;
+                abD[s][t] = Dab;
+                abI[s][t] = rab * rab;
+                abW[s][t] = 0.5 * wab;
+                abH[s][t] = hab;
+                abR[s][t] = rPab * (0.5 * A.rsd[s]);
+                abMu[s][t] = muAB;
+                abMuB[s][t] = ldexp(muB, nB - nAB);
+                abN[s][t] = nAB;
+            }
+            const double Gac = ai ? (okc ? A.G[s][(size_t)ua * ldg + uc] : 0.0) : g1ac[s][t];
+            l1[s] = Gac * iAaa;
+            D1[s] = fma(-l1[s], Gac, Acc[s]);
+            const double w1 = fma(-l1[s], ya, yc[s]);
+            w1h[s] = 0.5 * w1;
+            const double r1 = rsqrt_nr(D1[s]);
+            const double h1 = fma(w1 * w1, r1 * r1, ha);
+            const double rP1 = rPa * r1 * A.rsd[s] * chic[s];
+            int n1;
+            double mu1;
+            split3(h1, rP1, tab, n1, mu1);
+            R[s] = n1;
+            Ep[s][0] = ldexp(1.0, -n1);
+            Ep[s][1] = ldexp(muA, nA - n1);
+            Ep[s][2] = ldexp(muC[s], nC[s] - n1);
+            Ep[s][3] = mu1;
+        }
+        const double wac = wc * memb_weight(pa);
+        // this a's reference G: the a accumulator sits at it; c / noCausal / the b
+        // slots move their shift up to it (values scale down exactly) once per a
+        const int G = R[0] + R[1];
+        double aW0 = 0.0, aW1 = 0.0, aW2 = 0.0, aSl = 0.0, aNs = 0.0;
+        {
+            const int M = max(mC, G), d = mC - M;
+            cW0 = ldexp(cW0, d); cW1 = ldexp(cW1, d); cW2 = ldexp(cW2, d); cSl = ldexp(cSl, d); cNs = ldexp(cNs, d);
+            mC = M;
+            const int M0 = max(m0, R[1]), M1 = max(m1, R[0]);
+            nc0 = ldexp(nc0, m0 - M0);
+            nc1 = ldexp(nc1, m1 - M1);
+            m0 = M0;
+            m1 = M1;
+        }
+        const double fC = ldexp(1.0, G - mC), f0 = ldexp(1.0, R[1] - m0), f1 = ldexp(1.0, R[0] - m1);
+        {
+            int Gm = G;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) Gm = max(Gm, __shfl_xor(Gm, o));
+            const int Ms = max(sM[t], Gm), d = sM[t] - Ms;
+            sW0[t] = ldexp(sW0[t], d);
+            sW1[t] = ldexp(sW1[t], d);
+            sW2[t] = ldexp(sW2[t], d);
+            sSl[t] = ldexp(sSl[t], d);
+            sNs[t] = ldexp(sNs[t], d);
+            sM[t] = Ms;
+        }
+        __syncthreads();  // (a, b) terms and slot shifts visible
+        if (A.trace && ai == 0) t_ph[1] = wall_clock64();
+
+        // LDS operands are software-pipelined: the (a, b) terms that start a
+        // step's dependent chain are read one step ahead, the rest and the b
+        // slot at the top of their step (the slot after the previous step's
+        // writes: LDS executes a wave's instructions in issue order)
+        double nG[2], nI[2], nD[2], nW[2];
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const int b0 = (t + j0) & 63;
+            nG[s] = abG[s][b0];
+            nI[s] = abI[s][b0];
+            nD[s] = abD[s][b0];
+            nW[s] = abW[s][b0];
+        }
+        for (int j = j0; j < j1; j++) {
+            const double gcur0 = gnx.x, gcur1 = gnx.y, mcur0 = mnx.x, mcur1 = mnx.y;
+            const int2 ncur = nnx;
+            if (j + 1 < j1) {
+                gnx = g01[(j + 1) * 64];
+                mnx = m01[(j + 1) * 64];
+                nnx = bnn[(j + 1) * 64];
+            }
+            const int bs = (t + j) & 63;
+            double cG[2], cI[2], cD[2], cW[2], cH[2], cR[2], cMu[2], cMuB[2];
+            int cN[2];
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                cG[s] = nG[s];
+                cI[s] = nI[s];
+                cD[s] = nD[s];
+                cW[s] = nW[s];
+                cH[s] = abH[s][bs];
+                cR[s] = abR[s][bs];
+                cMu[s] = abMu[s][bs];
+                cMuB[s] = abMuB[s][bs];
+                cN[s] = abN[s][bs];
+            }
+            const int sm_ = sM[bs];
+            const double o0 = sW0[bs], o1 = sW1[bs], o2 = sW2[bs], oS = sSl[bs], oN = sNs[bs];
+            {
+                const int b1 = (t + j + 1) & 63;
+#pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    nG[s] = abG[s][b1];
+                    nI[s] = abI[s][b1];
+                    nD[s] = abD[s][b1];
+                    nW[s] = abW[s][b1];
+                }
+            }
+            const int vb = 64 * K + bs;
+            const bool act = diag ? (((vb > va && vc > va) || (va >= 64 * K + 64 && vb >= pad && vc >= pad)) &&
+                                     (j < 32 || t < 32))
+                                  : (okc && vb > va && vb < vc);
+            if (act) {
+                // P[s][m] = E_s[m], Q[s][m] = E_s[m | c], m over {a, b}; relative to 2^{R_s}
+                double P[2][4], Q[2][4];
+                int d3s = 0;
+#pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    const double Gbc = s ? gcur1 : gcur0;
+                    const int n2 = s ? ncur.y : ncur.x;
+                    const double mu2 = s ? mcur1 : mcur0;
+                    const double lcb = fma(-l1[s], cG[s], Gbc) * cI[s];
+                    const double u3 = lcb * cD[s];
+                    const double D3 = fma(-u3, lcb, D1[s]);
+                    const double w3 = fma(-lcb, cW[s], w1h[s]);
+                    const double r3 = rsq2x(D3);
+                    const double t3 = w3 * r3;
+                    const double h3 = fma(t3, t3, cH[s]);
+                    double rP3 = cR[s] * r3;
+                    if (!ALLPRES && !((pcm >> s) & 1u)) rP3 = 0.0;
+                    int n3;
+                    double mu3;
+                    split3(h3, rP3, tab, n3, mu3);
+                    const int d3 = n3 - R[s], dab = cN[s] - R[s];
+                    d3s += d3;
+                    P[s][0] = Ep[s][0];
+                    P[s][1] = Ep[s][1];
+                    P[s][2] = ldexp(cMuB[s], dab);
+                    P[s][3] = ldexp(cMu[s], dab);
+                    Q[s][0] = Ep[s][2];
+                    Q[s][1] = Ep[s][3];
+                    Q[s][2] = ldexp(mu2, n2 - R[s]);
+                    Q[s][3] = ldexp(mu3, d3);
+                }
+                dmax = max(dmax, d3s);
+                // ---- member c: bilinear forms over the (a, b) assignments ----
+                double MrP[4], MrQ[4], M1P[4], M1Q[4];
+                MrP[0] = P[1][3];
+                MrP[1] = fma(rho, P[1][3], P[1][2]);
+                MrP[2] = fma(rho, P[1][3], P[1][1]);
+                MrP[3] = fma(rho, MrP[1], fma(rho, P[1][1], P[1][0]));
+                MrQ[0] = Q[1][3];
+                MrQ[1] = fma(rho, Q[1][3], Q[1][2]);
+                MrQ[2] = fma(rho, Q[1][3], Q[1][1]);
+                MrQ[3] = fma(rho, MrQ[1], fma(rho, Q[1][1], Q[1][0]));
+                M1P[0] = P[1][3];
+                M1P[1] = P[1][2] + P[1][3];
+                M1P[2] = P[1][1] + P[1][3];
+                M1P[3] = (P[1][0] + P[1][1]) + M1P[1];
+                M1Q[0] = Q[1][3];
+                M1Q[1] = Q[1][2] + Q[1][3];
+                M1Q[2] = Q[1][1] + Q[1][3];
+                M1Q[3] = (Q[1][0] + Q[1][1]) + M1Q[1];
+                auto dot4 = [](const double (&u)[4], const double (&x)[4], double acc0) {
+                    return fma(u[3], x[3], fma(u[2], x[2], fma(u[1], x[1], fma(u[0], x[0], acc0))));
+                };
+                const double WC0 = dot4(Q[0], MrP, 0.0);
+                const double WC1 = dot4(P[0], MrQ, 0.0);
+                const double WC2 = dot4(Q[0], MrQ, 0.0);
+                const double LC2 = dot4(Q[0], M1Q, 0.0);
+                const double NC = dot4(P[0], M1Q, dot4(Q[0], M1P, 0.0));
+                // ---- members a, b: the 9 (x_a, x_b) with c marginalised ----
+                double S1[4], T1[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    S1[q] = P[1][q] + Q[1][q];
+                    T1[q] = fma(rho, Q[1][q], P[1][q]);
+                }
+                double Pl[3][3], Pw[3][3];
+#pragma unroll
+                for (int xa = 0; xa < 3; xa++)
+#pragma unroll
+                    for (int xb = 0; xb < 3; xb++) {
+                        const int al = (xa != 1) | ((xb != 1) << 1), be = (xa != 0) | ((xb != 0) << 1);
+                        const double X = P[0][al] * Q[1][be];
+                        Pl[xa][xb] = fma(Q[0][al], S1[be], X);
+                        Pw[xa][xb] = fma(Q[0][al], T1[be], X);
+                    }
+                double WA[3], WB[3];
+#pragma unroll
+                for (int x = 0; x < 3; x++) {
+                    WA[x] = fma(rho, Pw[x][2], Pw[x][0] + Pw[x][1]);
+                    WB[x] = fma(rho, Pw[2][x], Pw[0][x] + Pw[1][x]);
+                }
+                const double LA2 = (Pl[2][0] + Pl[2][1]) + Pl[2][2];
+                const double NA = ((Pl[0][0] + Pl[0][1]) + Pl[0][2]) + ((Pl[1][0] + Pl[1][1]) + Pl[1][2]);
+                const double LB2 = (Pl[0][2] + Pl[1][2]) + Pl[2][2];
+                const double NB = ((Pl[0][0] + Pl[1][0]) + Pl[2][0]) + ((Pl[0][1] + Pl[1][1]) + Pl[2][1]);
+                if (__builtin_amdgcn_ballot_w64((NA < kTinyNs) | (NB < kTinyNs) | (NC < kTinyNs)))
+                    if (NA < kTinyNs || NB < kTinyNs || NC < kTinyNs) atomicOr(flag, 1);
+                // ---- folds: a (registers, at G), c (registers, x fC), b (LDS slot, x fS), noCausal ----
+                const double fS = ldexp(1.0, G - sm_);
+                sW0[bs] = fma(WB[0], fS, o0);
+                sW1[bs] = fma(WB[1], fS, o1);
+                sW2[bs] = fma(WB[2], fS, o2);
+                sSl[bs] = fma(LB2, fS, oS);
+                sNs[bs] = fma(NB, fS, oN);
+                aW0 += WA[0];
+                aW1 += WA[1];
+                aW2 += WA[2];
+                aSl += LA2;
+                aNs += NA;
+                cW0 = fma(WC0, fC, cW0);
+                cW1 = fma(WC1, fC, cW1);
+                cW2 = fma(WC2, fC, cW2);
+                cSl = fma(LC2, fC, cSl);
+                cNs = fma(NC, fC, cNs);
+                // noCausal[s]: every member in the other study only
+                nc0 = fma(Q[1][3], f0, nc0);
+                nc1 = fma(Q[0][3], f1, nc1);
+                npat += ALLPRES ? 27.0 : wac * bW[bs];
+            }
+            // b-slot ownership rotates across lanes every step: the workgroup is one
+            // wave and LDS executes a wave's instructions in issue order
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (A.trace && ai == 0) t_ph[2] = wall_clock64();
+        Acc5 ra = wrec(G, aW0, aW1, aW2, aSl, aNs, rho, A.Ck, A.pit0);
+        wave_fold_acc(ra);
+        const int qa = sPos[2][ai];
+        if (t == 0 && qa >= 0) store_rec(rec + qa, ra);
+        if (A.trace && ai == 0) t_ph[3] = wall_clock64();
+    }
+    __syncthreads();
+    if (sPos[0][t] >= 0) store_rec(rec + sPos[0][t], wrec(mC, cW0, cW1, cW2, cSl, cNs, rho, A.Ck, A.pit0));
+    if (sPos[1][t] >= 0)
+        store_rec(rec + sPos[1][t], wrec(sM[t], sW0[t], sW1[t], sW2[t], sSl[t], sNs[t], rho, A.Ck, A.pit0));
+    SetRec sr;
+    sr.tot = ((cW0 + cW1) + rho * cW2) * A.pit0;  // every assignment of the lane's sets
+    sr.m = (sr.tot != 0.0) ? mC + A.Ck : EMPTY;
+    sr.nc0 = nc0 * A.pit0;
+    sr.m0 = (sr.nc0 != 0.0) ? m0 + A.Ck : EMPTY;
+    sr.nc1 = nc1 * A.pit0;
+    sr.m1 = (sr.nc1 != 0.0) ? m1 + A.Ck : EMPTY;
+    sr.pad = 0;
+    sr.score = 1e300;
+    sr.npat = npat;
+    wave_fold_set(sr);
+    if (t == 0) store_rec(srec + unit, sr);
+    redo = __builtin_amdgcn_ballot_w64(dmax > kMaxRefGap) != 0;
     if (A.trace && t == 0) {
         unsigned hw, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -585,8 +987,32 @@ __global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const
         tr[0] = t_start;
         tr[1] = wall_clock64();
         tr[2] = hw | ((unsigned long long)xcc << 32);
-        tr[3] = (unsigned long long)unit | ((unsigned long long)diag << 32) | ((unsigned long long)(a1 - a0) << 33);
+        tr[3] = (unsigned long long)unit | ((unsigned long long)diag << 32) | ((unsigned long long)(a1 - a0) << 33) |
+                ((unsigned long long)redo << 40);
         for (int i = 0; i < 4; i++) tr[4 + i] = t_ph[i];
+    }
+}
+
+// The k = 3 sweep: one block per unit (fast variant, redone robustly in the same
+// block when flagged); level-2 units ride in the same launch, after them.
+template <bool ALLPRES>
+__global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const int4* __restrict__ units,
+                                                  Acc5* __restrict__ rec, SetRec* __restrict__ srec, int rec_stride,
+                                                  int* __restrict__ flag, const int* __restrict__ pos, int nk3,
+                                                  TileArgs A2, const int4* __restrict__ units2,
+                                                  Acc5* __restrict__ rec2, SetRec* __restrict__ srec2,
+                                                  const int* __restrict__ pos2) {
+    __shared__ SweepSmem sm;
+    if ((int)blockIdx.x >= nk3) {
+        sweep_unit<2, false>(A2, blockIdx.x - nk3, units2, rec2, srec2, 128, flag, pos2, sm.u2);
+        return;
+    }
+    bool redo = false;
+    sweep3_unit_fast<ALLPRES>(A, blockIdx.x, units, rec, srec, rec_stride, flag, pos, sm, redo);
+    if (redo) {
+        if (threadIdx.x == 0 && A.redo_count) atomicAdd(A.redo_count, 1);
+        __syncthreads();
+        sweep3_unit_robust<ALLPRES>(A, blockIdx.x, units, rec, srec, rec_stride, flag, pos, sm);
     }
 }
 

@@ -120,6 +120,7 @@ class Timing(ctypes.Structure):
         ("alg_bytes", ctypes.c_double),
         ("flops", ctypes.c_double),
         ("exact_rerun", ctypes.c_int32),
+        ("robust_units", ctypes.c_int32),
     ]
 
     def as_dict(self):

@@ -365,6 +365,33 @@ def test_extreme_signal_exact_rerun(gpu):
     assert_parity(pc.accum(), O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-10)
 
 
+def test_strong_signal_robust_units(gpu):
+    """A shared SNP with z ~ 30 in both studies: adding it to a set {a, c}
+    raises the set's weight by ~2^570 per study, beyond the fast k = 3
+    variant's 960-bit window over both studies, so the units holding it as b
+    are redone by the robust variant (in the same block); its notSharedLL groups
+    stay within range, so no exact rerun.  Parity with the oracle at 1e-9."""
+    M = 80
+    idx = np.arange(M)
+    ld, z = [], []
+    for s, rho in enumerate((0.5, 0.3)):
+        sig = rho ** np.abs(idx[:, None] - idx[None, :])
+        lam = np.zeros(M)
+        lam[50] = 30.0
+        lam[10] = 5.0 if s == 0 else 0.0
+        eps = np.random.default_rng(19 + s).standard_normal(M)
+        z.append(sig @ lam + np.linalg.cholesky(sig) @ eps)
+        ld.append(sig)
+    u2l = np.stack([idx, idx]).astype(np.int32)
+    seam = E.seam_from_arrays(ld, z, u2l, (12000, 9000), max_causal=3, sharing_param=0.3)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    t = pc.timing()
+    assert t["exact_rerun"] == 0 and t["robust_units"] > 0, t
+    assert_parity(pc.accum(), O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-10)
+    pc.close()
+
+
 def _cli_pair(tmp_path, src, args):
     d1, d2 = tmp_path / "engine", tmp_path / "oracle"
     shutil.copytree(os.path.join(loci.GOLDEN, src), d1)
