@@ -90,6 +90,34 @@ __device__ __forceinline__ void split3(double h, double rP, const double* tab, i
     mu = tab[N & 255] * p * rP;
 }
 
+// the table-free first half of split3: N = round(256 h), q = 2^{f/256} * rP
+// (the caller completes mu = tab[N & 255] * q, n = N >> 8)
+__device__ __forceinline__ void split3a(double h, double rP, int& N, double& q) {
+    const double xr = fma(h, 256.0, kMagic);
+    N = __double2loint(xr);
+    const double kf = xr - kMagic;
+    const double f = fma(h, 256.0, -kf);
+    double p = fma(kQ4, f, kQ3);
+    p = fma(p, f, kQ2);
+    p = fma(p, f, kQ1);
+    p = fma(p, f, 1.0);
+    q = p * rP;
+}
+
+// split3a with the rounding offset by an integer R (cmag = kMagic - 256 R):
+// N = round(256 (h - R)), so the caller's exponent is N >> 8 = n - R directly
+__device__ __forceinline__ void split3r(double h, double rP, double cmag, int& N, double& q) {
+    const double xr = fma(h, 256.0, cmag);
+    N = __double2loint(xr);
+    const double kf = xr - cmag;
+    const double f = fma(h, 256.0, -kf);
+    double p = fma(kQ4, f, kQ3);
+    p = fma(p, f, kQ2);
+    p = fma(p, f, kQ1);
+    p = fma(p, f, 1.0);
+    q = p * rP;
+}
+
 // lazy accumulator: move the shift up to G (values scale down exactly)
 __device__ __forceinline__ void lacc_shift(LAcc& a, int G) {
     const int d = a.m - G;
@@ -616,7 +644,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     double (&bH)[2][64] = sm.s3.bH;
     double (&bR)[2][64] = sm.s3.bR;
     double (&abG)[2][64] = sm.s3.abG;
-    double (&abD)[2][64] = sm.s3.abD;
+    double (&abIW)[2][64] = sm.s3.abD;  // fast variant: I_ab * w_ab / 2 (the pivot itself is not needed)
     double (&abI)[2][64] = sm.s3.abI;
     double (&abW)[2][64] = sm.s3.abW;
     double (&abH)[2][64] = sm.s3.abH;
@@ -732,9 +760,9 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 split3(hab, rPab, tab, nAB, muAB);
                 split3(bH[s][t], bR[s][t] * (2.0 / A.rsd[s]), tab, nB, muB);
                 abG[s][t] = Gab;
-                abD[s][t] = Dab;
                 abI[s][t] = rab * rab;
                 abW[s][t] = 0.5 * wab;
+                abIW[s][t] = rab * rab * (0.5 * wab);
                 abH[s][t] = hab;
                 abR[s][t] = rPab * (0.5 * A.rsd[s]);
                 abMu[s][t] = muAB;
@@ -774,6 +802,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             m1 = M1;
         }
         const double fC = ldexp(1.0, G - mC), f0 = ldexp(1.0, R[1] - m0), f1 = ldexp(1.0, R[0] - m1);
+        // round-to-nearest magic offset by R: N = round(256 (h3 - R)), so n3 - R = N >> 8
+        const double cmag[2] = {kMagic - 256.0 * R[0], kMagic - 256.0 * R[1]};
         {
             int Gm = G;
 #pragma unroll
@@ -789,172 +819,184 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         __syncthreads();  // (a, b) terms and slot shifts visible
         if (A.trace && ai == 0) t_ph[1] = wall_clock64();
 
-        // LDS operands are software-pipelined: the (a, b) terms that start a
-        // step's dependent chain are read one step ahead, the rest and the b
-        // slot at the top of their step (the slot after the previous step's
-        // writes: LDS executes a wave's instructions in issue order)
-        double nG[2], nI[2], nD[2], nW[2];
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const int b0 = (t + j0) & 63;
-            nG[s] = abG[s][b0];
-            nI[s] = abI[s][b0];
-            nD[s] = abD[s][b0];
-            nW[s] = abW[s][b0];
-        }
-        for (int j = j0; j < j1; j++) {
-            const double gcur0 = gnx.x, gcur1 = gnx.y, mcur0 = mnx.x, mcur1 = mnx.y;
-            const int2 ncur = nnx;
-            if (j + 1 < j1) {
-                gnx = g01[(j + 1) * 64];
-                mnx = m01[(j + 1) * 64];
-                nnx = bnn[(j + 1) * 64];
-            }
+        // The b-walk.  chain(j) is step j's dependent {a, b, c} extension up to
+        // the split of 2^h3 (N = round(256 h3), q = 2^(f/256) P^(-1/2)); finish(j)
+        // takes the table entry, rescales the four b weights, folds the 27
+        // assignments and accumulates.  Off-diagonal tiles (every lane active every
+        // step) run chain(j + 1) beside finish(j), so the serial chain of one step
+        // overlaps the wide fold of the previous one; the Sigma~ tile row is
+        // fetched two steps ahead, the {b, c} weights one.
+        bool tiny = false;
+        auto chain = [&](int j, double2 g, int (&N)[2], double (&q)[2]) {
             const int bs = (t + j) & 63;
-            double cG[2], cI[2], cD[2], cW[2], cH[2], cR[2], cMu[2], cMuB[2];
-            int cN[2];
 #pragma unroll
             for (int s = 0; s < 2; s++) {
-                cG[s] = nG[s];
-                cI[s] = nI[s];
-                cD[s] = nD[s];
-                cW[s] = nW[s];
-                cH[s] = abH[s][bs];
-                cR[s] = abR[s][bs];
-                cMu[s] = abMu[s][bs];
-                cMuB[s] = abMuB[s][bs];
-                cN[s] = abN[s][bs];
+                // x = the unnormalised L entry of c against b; D_ab I_ab = 1 folds the pivot away
+                const double Gbc = s ? g.y : g.x;
+                const double x = fma(-l1[s], abG[s][bs], Gbc);
+                const double lcb = x * abI[s][bs];
+                const double D3 = fma(-x, lcb, D1[s]);
+                const double w3 = fma(-x, abIW[s][bs], w1h[s]);
+                const double r3 = rsq2x(D3);
+                const double t3 = w3 * r3;
+                const double h3 = fma(t3, t3, abH[s][bs]);
+                double rP3 = abR[s][bs] * r3;
+                if (!ALLPRES && !((pcm >> s) & 1u)) rP3 = 0.0;  // c absent from study s
+                split3r(h3, rP3, cmag[s], N[s], q[s]);
             }
+        };
+        auto finish = [&](int j, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
+            const int bs = (t + j) & 63;
             const int sm_ = sM[bs];
             const double o0 = sW0[bs], o1 = sW1[bs], o2 = sW2[bs], oS = sSl[bs], oN = sNs[bs];
-            {
-                const int b1 = (t + j + 1) & 63;
+            // P[s][m] = E_s[m], Q[s][m] = E_s[m | c], m over {a, b}; relative to 2^{R_s}
+            double P[2][4], Q[2][4];
+            int d3s = 0;
 #pragma unroll
-                for (int s = 0; s < 2; s++) {
-                    nG[s] = abG[s][b1];
-                    nI[s] = abI[s][b1];
-                    nD[s] = abD[s][b1];
-                    nW[s] = abW[s][b1];
-                }
+            for (int s = 0; s < 2; s++) {
+                const int d3 = N[s] >> 8;  // n3 - R (N is R-relative)
+                const double mu3 = tab[N[s] & 255] * q[s];
+                const int n2 = s ? ncur.y : ncur.x;
+                const double mu2 = s ? mcur.y : mcur.x;
+                const int dab = abN[s][bs] - R[s];
+                d3s += d3;
+                P[s][0] = Ep[s][0];
+                P[s][1] = Ep[s][1];
+                P[s][2] = ldexp(abMuB[s][bs], dab);
+                P[s][3] = ldexp(abMu[s][bs], dab);
+                Q[s][0] = Ep[s][2];
+                Q[s][1] = Ep[s][3];
+                Q[s][2] = ldexp(mu2, n2 - R[s]);
+                Q[s][3] = ldexp(mu3, d3);
             }
-            const int vb = 64 * K + bs;
-            const bool act = diag ? (((vb > va && vc > va) || (va >= 64 * K + 64 && vb >= pad && vc >= pad)) &&
-                                     (j < 32 || t < 32))
-                                  : (okc && vb > va && vb < vc);
-            if (act) {
-                // P[s][m] = E_s[m], Q[s][m] = E_s[m | c], m over {a, b}; relative to 2^{R_s}
-                double P[2][4], Q[2][4];
-                int d3s = 0;
+            dmax = max(dmax, d3s);
+            // ---- member c: bilinear forms over the (a, b) assignments ----
+            double MrP[4], MrQ[4], M1P[4], M1Q[4];
+            MrP[0] = P[1][3];
+            MrP[1] = fma(rho, P[1][3], P[1][2]);
+            MrP[2] = fma(rho, P[1][3], P[1][1]);
+            MrP[3] = fma(rho, MrP[1], fma(rho, P[1][1], P[1][0]));
+            MrQ[0] = Q[1][3];
+            MrQ[1] = fma(rho, Q[1][3], Q[1][2]);
+            MrQ[2] = fma(rho, Q[1][3], Q[1][1]);
+            MrQ[3] = fma(rho, MrQ[1], fma(rho, Q[1][1], Q[1][0]));
+            M1P[0] = P[1][3];
+            M1P[1] = P[1][2] + P[1][3];
+            M1P[2] = P[1][1] + P[1][3];
+            M1P[3] = (P[1][0] + P[1][1]) + M1P[1];
+            M1Q[0] = Q[1][3];
+            M1Q[1] = Q[1][2] + Q[1][3];
+            M1Q[2] = Q[1][1] + Q[1][3];
+            M1Q[3] = (Q[1][0] + Q[1][1]) + M1Q[1];
+            auto dot4 = [](const double (&u)[4], const double (&x)[4], double acc0) {
+                return fma(u[3], x[3], fma(u[2], x[2], fma(u[1], x[1], fma(u[0], x[0], acc0))));
+            };
+            const double WC0 = dot4(Q[0], MrP, 0.0);
+            const double WC1 = dot4(P[0], MrQ, 0.0);
+            const double WC2 = dot4(Q[0], MrQ, 0.0);
+            const double LC2 = dot4(Q[0], M1Q, 0.0);
+            const double NC = dot4(P[0], M1Q, dot4(Q[0], M1P, 0.0));
+            // ---- members a, b: the 9 (x_a, x_b) with c marginalised ----
+            double S1[4], T1[4];
 #pragma unroll
-                for (int s = 0; s < 2; s++) {
-                    const double Gbc = s ? gcur1 : gcur0;
-                    const int n2 = s ? ncur.y : ncur.x;
-                    const double mu2 = s ? mcur1 : mcur0;
-                    const double lcb = fma(-l1[s], cG[s], Gbc) * cI[s];
-                    const double u3 = lcb * cD[s];
-                    const double D3 = fma(-u3, lcb, D1[s]);
-                    const double w3 = fma(-lcb, cW[s], w1h[s]);
-                    const double r3 = rsq2x(D3);
-                    const double t3 = w3 * r3;
-                    const double h3 = fma(t3, t3, cH[s]);
-                    double rP3 = cR[s] * r3;
-                    if (!ALLPRES && !((pcm >> s) & 1u)) rP3 = 0.0;
-                    int n3;
-                    double mu3;
-                    split3(h3, rP3, tab, n3, mu3);
-                    const int d3 = n3 - R[s], dab = cN[s] - R[s];
-                    d3s += d3;
-                    P[s][0] = Ep[s][0];
-                    P[s][1] = Ep[s][1];
-                    P[s][2] = ldexp(cMuB[s], dab);
-                    P[s][3] = ldexp(cMu[s], dab);
-                    Q[s][0] = Ep[s][2];
-                    Q[s][1] = Ep[s][3];
-                    Q[s][2] = ldexp(mu2, n2 - R[s]);
-                    Q[s][3] = ldexp(mu3, d3);
-                }
-                dmax = max(dmax, d3s);
-                // ---- member c: bilinear forms over the (a, b) assignments ----
-                double MrP[4], MrQ[4], M1P[4], M1Q[4];
-                MrP[0] = P[1][3];
-                MrP[1] = fma(rho, P[1][3], P[1][2]);
-                MrP[2] = fma(rho, P[1][3], P[1][1]);
-                MrP[3] = fma(rho, MrP[1], fma(rho, P[1][1], P[1][0]));
-                MrQ[0] = Q[1][3];
-                MrQ[1] = fma(rho, Q[1][3], Q[1][2]);
-                MrQ[2] = fma(rho, Q[1][3], Q[1][1]);
-                MrQ[3] = fma(rho, MrQ[1], fma(rho, Q[1][1], Q[1][0]));
-                M1P[0] = P[1][3];
-                M1P[1] = P[1][2] + P[1][3];
-                M1P[2] = P[1][1] + P[1][3];
-                M1P[3] = (P[1][0] + P[1][1]) + M1P[1];
-                M1Q[0] = Q[1][3];
-                M1Q[1] = Q[1][2] + Q[1][3];
-                M1Q[2] = Q[1][1] + Q[1][3];
-                M1Q[3] = (Q[1][0] + Q[1][1]) + M1Q[1];
-                auto dot4 = [](const double (&u)[4], const double (&x)[4], double acc0) {
-                    return fma(u[3], x[3], fma(u[2], x[2], fma(u[1], x[1], fma(u[0], x[0], acc0))));
-                };
-                const double WC0 = dot4(Q[0], MrP, 0.0);
-                const double WC1 = dot4(P[0], MrQ, 0.0);
-                const double WC2 = dot4(Q[0], MrQ, 0.0);
-                const double LC2 = dot4(Q[0], M1Q, 0.0);
-                const double NC = dot4(P[0], M1Q, dot4(Q[0], M1P, 0.0));
-                // ---- members a, b: the 9 (x_a, x_b) with c marginalised ----
-                double S1[4], T1[4];
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    S1[q] = P[1][q] + Q[1][q];
-                    T1[q] = fma(rho, Q[1][q], P[1][q]);
-                }
-                double Pl[3][3], Pw[3][3];
-#pragma unroll
-                for (int xa = 0; xa < 3; xa++)
-#pragma unroll
-                    for (int xb = 0; xb < 3; xb++) {
-                        const int al = (xa != 1) | ((xb != 1) << 1), be = (xa != 0) | ((xb != 0) << 1);
-                        const double X = P[0][al] * Q[1][be];
-                        Pl[xa][xb] = fma(Q[0][al], S1[be], X);
-                        Pw[xa][xb] = fma(Q[0][al], T1[be], X);
-                    }
-                double WA[3], WB[3];
-#pragma unroll
-                for (int x = 0; x < 3; x++) {
-                    WA[x] = fma(rho, Pw[x][2], Pw[x][0] + Pw[x][1]);
-                    WB[x] = fma(rho, Pw[2][x], Pw[0][x] + Pw[1][x]);
-                }
-                const double LA2 = (Pl[2][0] + Pl[2][1]) + Pl[2][2];
-                const double NA = ((Pl[0][0] + Pl[0][1]) + Pl[0][2]) + ((Pl[1][0] + Pl[1][1]) + Pl[1][2]);
-                const double LB2 = (Pl[0][2] + Pl[1][2]) + Pl[2][2];
-                const double NB = ((Pl[0][0] + Pl[1][0]) + Pl[2][0]) + ((Pl[0][1] + Pl[1][1]) + Pl[2][1]);
-                if (__builtin_amdgcn_ballot_w64((NA < kTinyNs) | (NB < kTinyNs) | (NC < kTinyNs)))
-                    if (NA < kTinyNs || NB < kTinyNs || NC < kTinyNs) atomicOr(flag, 1);
-                // ---- folds: a (registers, at G), c (registers, x fC), b (LDS slot, x fS), noCausal ----
-                const double fS = ldexp(1.0, G - sm_);
-                sW0[bs] = fma(WB[0], fS, o0);
-                sW1[bs] = fma(WB[1], fS, o1);
-                sW2[bs] = fma(WB[2], fS, o2);
-                sSl[bs] = fma(LB2, fS, oS);
-                sNs[bs] = fma(NB, fS, oN);
-                aW0 += WA[0];
-                aW1 += WA[1];
-                aW2 += WA[2];
-                aSl += LA2;
-                aNs += NA;
-                cW0 = fma(WC0, fC, cW0);
-                cW1 = fma(WC1, fC, cW1);
-                cW2 = fma(WC2, fC, cW2);
-                cSl = fma(LC2, fC, cSl);
-                cNs = fma(NC, fC, cNs);
-                // noCausal[s]: every member in the other study only
-                nc0 = fma(Q[1][3], f0, nc0);
-                nc1 = fma(Q[0][3], f1, nc1);
-                npat += ALLPRES ? 27.0 : wac * bW[bs];
+            for (int q = 0; q < 4; q++) {
+                S1[q] = P[1][q] + Q[1][q];
+                T1[q] = fma(rho, Q[1][q], P[1][q]);
             }
-            // b-slot ownership rotates across lanes every step: the workgroup is one
-            // wave and LDS executes a wave's instructions in issue order
-            __builtin_amdgcn_wave_barrier();
+            double Pl[3][3], Pw[3][3];
+#pragma unroll
+            for (int xa = 0; xa < 3; xa++)
+#pragma unroll
+                for (int xb = 0; xb < 3; xb++) {
+                    const int al = (xa != 1) | ((xb != 1) << 1), be = (xa != 0) | ((xb != 0) << 1);
+                    const double X = P[0][al] * Q[1][be];
+                    Pl[xa][xb] = fma(Q[0][al], S1[be], X);
+                    Pw[xa][xb] = fma(Q[0][al], T1[be], X);
+                }
+            double WA[3], WB[3];
+#pragma unroll
+            for (int x = 0; x < 3; x++) {
+                WA[x] = fma(rho, Pw[x][2], Pw[x][0] + Pw[x][1]);
+                WB[x] = fma(rho, Pw[2][x], Pw[0][x] + Pw[1][x]);
+            }
+            const double LA2 = (Pl[2][0] + Pl[2][1]) + Pl[2][2];
+            const double NA = ((Pl[0][0] + Pl[0][1]) + Pl[0][2]) + ((Pl[1][0] + Pl[1][1]) + Pl[1][2]);
+            const double LB2 = (Pl[0][2] + Pl[1][2]) + Pl[2][2];
+            const double NB = ((Pl[0][0] + Pl[1][0]) + Pl[2][0]) + ((Pl[0][1] + Pl[1][1]) + Pl[2][1]);
+            tiny |= (NA < kTinyNs) | (NB < kTinyNs) | (NC < kTinyNs);
+            // ---- folds: a (registers, at G), c (registers, x fC), b (LDS slot, x fS), noCausal ----
+            const double fS = ldexp(1.0, G - sm_);
+            sW0[bs] = fma(WB[0], fS, o0);
+            sW1[bs] = fma(WB[1], fS, o1);
+            sW2[bs] = fma(WB[2], fS, o2);
+            sSl[bs] = fma(LB2, fS, oS);
+            sNs[bs] = fma(NB, fS, oN);
+            aW0 += WA[0];
+            aW1 += WA[1];
+            aW2 += WA[2];
+            aSl += LA2;
+            aNs += NA;
+            cW0 = fma(WC0, fC, cW0);
+            cW1 = fma(WC1, fC, cW1);
+            cW2 = fma(WC2, fC, cW2);
+            cSl = fma(LC2, fC, cSl);
+            cNs = fma(NC, fC, cNs);
+            // noCausal[s]: every member in the other study only
+            nc0 = fma(Q[1][3], f0, nc0);
+            nc1 = fma(Q[0][3], f1, nc1);
+            npat += ALLPRES ? 27.0 : wac * bW[bs];
+        };
+        if (!diag && ((j1 - j0) & 1) == 0) {
+            // unrolled by two: the chained state alternates between (NA, qA) and (NB, qB)
+            double2 g_next = g01[min(j0 + 1, j1 - 1) * 64];
+            double2 m_cur = mnx;
+            int2 n_cur = nnx;
+            int NA[2], NB[2];
+            double qA[2], qB[2];
+            chain(j0, gnx, NA, qA);
+            for (int j = j0; j < j1; j += 2) {
+                const int r1 = min(j + 1, j1 - 1), r2 = min(j + 2, j1 - 1), r3 = min(j + 3, j1 - 1);
+                const double2 m_nxt = m01[r1 * 64];
+                const int2 n_nxt = bnn[r1 * 64];
+                const double2 g_after = g01[r2 * 64];
+                chain(r1, g_next, NB, qB);
+                finish(j, NA, qA, m_cur, n_cur);
+                // b-slot ownership rotates across lanes every step: the workgroup is
+                // one wave and LDS executes a wave's instructions in issue order
+                __builtin_amdgcn_wave_barrier();
+                m_cur = m01[r2 * 64];
+                n_cur = bnn[r2 * 64];
+                g_next = g01[r3 * 64];
+                chain(r2, g_after, NA, qA);  // (the last pair's repeat is unused)
+                finish(j + 1, NB, qB, m_nxt, n_nxt);
+                __builtin_amdgcn_wave_barrier();
+            }
+        } else {
+            for (int j = j0; j < j1; j++) {
+                const double2 gcur = gnx, mcur = mnx;
+                const int2 ncur = nnx;
+                if (j + 1 < j1) {
+                    gnx = g01[(j + 1) * 64];
+                    mnx = m01[(j + 1) * 64];
+                    nnx = bnn[(j + 1) * 64];
+                }
+                const int bs = (t + j) & 63;
+                const int vb = 64 * K + bs;
+                // the pair {slot, t} of the block with a below both, or any real pair
+                // when a lies after the block (steps 1..31, + 32 on lanes < 32)
+                const bool act = ((vb > va && vc > va) || (va >= 64 * K + 64 && vb >= pad && vc >= pad)) &&
+                                 (j < 32 || t < 32);
+                if (act) {
+                    int N[2];
+                    double q[2];
+                    chain(j, gcur, N, q);
+                    finish(j, N, q, mcur, ncur);
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
         }
+        if (__builtin_amdgcn_ballot_w64(tiny))
+            if (tiny) atomicOr(flag, 1);
         if (A.trace && ai == 0) t_ph[2] = wall_clock64();
         Acc5 ra = wrec(G, aW0, aW1, aW2, aSl, aNs, rho, A.Ck, A.pit0);
         wave_fold_acc(ra);
