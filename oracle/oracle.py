@@ -36,6 +36,9 @@ def load():
         _lib.oracle_eval_patterns.restype = i32
         _lib.oracle_eval_patterns.argtypes = [i32, P(i32), P(d), P(d), i32, P(i32), P(i32), d, d, d, d, i32, i32,
                                               P(i32), P(i32), i32, P(d), P(d)]
+        _lib.oracle_member_sums.restype = i32
+        _lib.oracle_member_sums.argtypes = [i32, P(i32), P(d), P(d), i32, P(i32), P(i32), d, d, d, d, i32, i32, i32,
+                                            P(d), P(i64)]
         _lib.oracle_setup_dims.restype = i32
         _lib.oracle_setup_dims.argtypes = [ctypes.c_char_p] * 5 + [P(i32), P(i32)]
         _lib.oracle_setup.restype = i32
@@ -101,6 +104,50 @@ def eval_patterns(seam, sets, bits, literal=False):
     if rc != 0:
         raise RuntimeError("oracle_eval_patterns failed")
     return L, ll
+
+
+def member_sums(seam, u, threads=None):
+    """One union SNP's accumulators over the exhaustive sweep (oracle_member_sums):
+    dict post0, post1, shared, shared_ll, notshared_ll (log, 0 = empty) and
+    n_patterns.  Exact log-sum-exp over every union set containing u."""
+    lib = load()
+    m = np.ascontiguousarray(seam.m, dtype=np.int32)
+    B = np.ascontiguousarray(seam.B, dtype=np.float64)
+    sp = np.ascontiguousarray(seam.s_prime, dtype=np.float64)
+    u2l = np.ascontiguousarray(seam.union_to_local, dtype=np.int32)
+    n = np.ascontiguousarray(seam.sample_sizes, dtype=np.int32)
+    out = np.zeros(5)
+    npat = ctypes.c_long(0)
+    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    D = ctypes.c_double
+    rc = lib.oracle_member_sums(2, _p(m, ctypes.c_int), _p(B, D), _p(sp, D), u2l.shape[1], _p(u2l, ctypes.c_int),
+                                _p(n, ctypes.c_int), float(seam.sharing_param), float(seam.gamma),
+                                float(seam.t_squared), float(seam.s_squared), int(seam.max_causal), int(u),
+                                int(threads), _p(out, D), ctypes.byref(npat))
+    if rc != 0:
+        raise RuntimeError("oracle_member_sums failed")
+    return dict(post0=out[0], post1=out[1], shared=out[2], shared_ll=out[3], notshared_ll=out[4],
+                n_patterns=npat.value)
+
+
+def cholesky_seam(ld, z, union_to_local, sample_sizes, **params):
+    """A PostCal seam for a positive-definite LD without the eigen route: B_s =
+    L_s^T (Sigma_s = L_s L_s^T), S'_s = L_s^-1 z_s.  The path consumes only
+    B^T B = Sigma, B^T S' = z and ||S'||^2 = z^T Sigma^-1 z, which equal the
+    reference's eigen-route values (model.h:213-259) in exact arithmetic, so
+    this is a fast oracle input for large synthetic loci (no PSD shift: SYN-v1
+    needs none up to M = 2000)."""
+    import scipy.linalg
+    from pipsort_amd.engine import Seam
+    Bs, sps = [], []
+    for s in range(2):
+        L = np.linalg.cholesky(np.asarray(ld[s], dtype=np.float64))
+        Bs.append(np.asarray(L.T, order="F").ravel(order="F"))  # column-major B_s = L^T
+        sps.append(scipy.linalg.solve_triangular(L, np.asarray(z[s], dtype=np.float64), lower=True))
+    m = np.array([ld[0].shape[0], ld[1].shape[0]], dtype=np.int32)
+    return Seam(m=m, B=np.concatenate(Bs), s_prime=np.concatenate(sps),
+                union_to_local=np.asarray(union_to_local, dtype=np.int32),
+                sample_sizes=np.asarray(sample_sizes, dtype=np.int32), **params)
 
 
 def setup_from_files(ld0, ld1, z0, z1, snp_map):

@@ -21,6 +21,8 @@
 // reduction on small loci.
 // =============================================================================
 #include <algorithm>
+#include <array>
+#include <thread>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -559,6 +561,23 @@ class PostCal {
         L = ll + log_prior(k, b0, b1);
     }
 
+    // eval_pattern without its O(N) configuration scan: the same causal set C in
+    // the same ascending global order (postcal.cpp:245-253), built directly.
+    void eval_pattern_fast(const int* locs, const int* b0, const int* b1, int k, double& L, double& ll) const {
+        vector<int> C;
+        vector<double> dC;
+        C.reserve(2 * k);
+        for (int s = 0; s < 2; s++)
+            for (int j = 0; j < k; j++)
+                if ((s ? b1[j] : b0[j])) C.push_back(off[s] + P.u2l[s][locs[j]]);
+        std::sort(C.begin(), C.end());
+        const double d0 = dval(0), d1 = dval(1);
+        for (int i : C) dC.push_back(study_of(i) == 0 ? d0 : d1);
+        ll = lowrank_ll(C, dC);
+        vector<int> v0(b0, b0 + k), v1(b1, b1 + k);
+        L = ll + log_prior(k, v0, v1);
+    }
+
     // Expand a union set into all per-study assignments (postcal.cpp:856-955 and
     // sss_postcal.cpp:518-597): bits assigned in (union SNP j, study s) order, masks
     // 1..2^b-1, patterns failing checkOR skipped.  Returns the sss score
@@ -917,6 +936,117 @@ int oracle_eval_patterns(int n_studies, const int* m, const double* B, const dou
         vector<int> b1(bits + (size_t)i * 2 * k + k, bits + (size_t)(i + 1) * 2 * k);
         pc.eval_pattern(locs, b0, b1, cfg, L_out[i], ll_out[i]);
     }
+    return 0;
+}
+
+// Per-member accumulators of ONE union SNP u over an exhaustive sweep of level
+// <= c (postcal.cpp:716-1092): every union set containing u, every assignment
+// passing checkOR (postcal.cpp:907-955), accumulated for u exactly as
+// postcal.cpp:981-1030 routes it — post (u causal in study s), sharedPips (u
+// causal in both), sharedLL / notSharedLL (ll, u in both / not in both).  A
+// checker for loci too large for a whole-sweep oracle (the M = 1000 headline
+// locus): the sums are exact log-sum-exp (running max, long double), not the
+// reference's serial addlogSpace, and split over `threads` host threads.
+// out: [post0, post1, shared, sharedLL, notSharedLL] (log; 0 = empty);
+// *n_patterns: assignments visited.
+int oracle_member_sums(int n_studies, const int* m, const double* B, const double* s_prime, int n_union,
+                       const int* union_to_local, const int* sample_sizes, double p, double gamma, double t2,
+                       double s2, int c, int u, int threads, double* out, long* n_patterns) {
+    if (n_studies != 2 || c < 1 || c > 3 || u < 0 || u >= n_union) return -1;
+    orc::Problem P;
+    P.m.assign(m, m + 2);
+    P.N = m[0] + m[1];
+    size_t bo = 0;
+    P.B.resize(2);
+    for (int s = 0; s < 2; s++) { P.B[s].assign(B + bo, B + bo + (size_t)m[s] * m[s]); bo += (size_t)m[s] * m[s]; }
+    P.sp.assign(s_prime, s_prime + P.N);
+    P.U = n_union;
+    P.u2l.assign(2, vector<int>(n_union));
+    for (int s = 0; s < 2; s++) for (int v = 0; v < n_union; v++) P.u2l[s][v] = union_to_local[s * n_union + v];
+    P.n.assign(sample_sizes, sample_sizes + 2);
+    P.p = p; P.gamma = gamma; P.t2 = t2; P.s2 = s2;
+    const orc::PostCal pc(P, false);
+    const int U = n_union;
+    // the other members: {} , {v}, {v, w} with v < w, v, w != u
+    vector<int> others;
+    for (int v = 0; v < U; v++) if (v != u) others.push_back(v);
+    const int no = (int)others.size();
+    struct LSE {  // running log-sum-exp
+        long double m = 0, s = 0;
+        bool any = false;
+        void add(double x) {
+            if (!any) { m = x; s = 1; any = true; return; }
+            if (x > m) { s = s * std::exp((long double)(m - x)) + 1; m = x; }
+            else s += std::exp((long double)(x - m));
+        }
+        void merge(const LSE& o) {
+            if (!o.any) return;
+            if (!any) { *this = o; return; }
+            if (o.m > m) { s = s * std::exp(m - o.m) + o.s; m = o.m; }
+            else s += o.s * std::exp(o.m - m);
+        }
+        double value() const { return any ? (double)(m + std::log(s)) : 0.0; }
+    };
+    threads = std::max(1, std::min(threads, 64));
+    vector<std::array<LSE, 5>> acc(threads);
+    vector<long> cnt(threads, 0);
+    auto run = [&](int tid) {
+        auto visit = [&](const vector<int>& set) {  // set: ascending union indices, contains u
+            const int k = (int)set.size();
+            int ju = 0;
+            while (set[ju] != u) ju++;
+            int np = 1;
+            for (int j = 0; j < k; j++) np *= 3;
+            int b0[3], b1[3];
+            for (int q = 0; q < np; q++) {
+                int r = q;
+                bool ok = true;
+                for (int j = 0; j < k; j++) {
+                    const int x = r % 3 + 1;
+                    r /= 3;
+                    b0[j] = x & 1;
+                    b1[j] = (x >> 1) & 1;
+                    if ((b0[j] && P.u2l[0][set[j]] < 0) || (b1[j] && P.u2l[1][set[j]] < 0)) ok = false;
+                }
+                if (!ok) continue;  // checkOR over present studies (postcal.cpp:953)
+                double L, ll;
+                pc.eval_pattern_fast(set.data(), b0, b1, k, L, ll);
+                cnt[tid]++;
+                auto& a = acc[tid];
+                if (b0[ju]) a[0].add(L);
+                if (b1[ju]) a[1].add(L);
+                if (b0[ju] && b1[ju]) { a[2].add(L); a[3].add(ll); }
+                else a[4].add(ll);
+            }
+        };
+        if (tid == 0) visit({u});
+        for (int i = tid; i < no; i += threads) {
+            const int v = others[i];
+            if (c >= 2) {
+                vector<int> st = {std::min(u, v), std::max(u, v)};
+                visit(st);
+            }
+            if (c >= 3)
+                for (int i2 = i + 1; i2 < no; i2++) {
+                    int w = others[i2];
+                    vector<int> st = {u, v, w};
+                    std::sort(st.begin(), st.end());
+                    visit(st);
+                }
+        }
+    };
+    vector<std::thread> th;
+    for (int i = 1; i < threads; i++) th.emplace_back(run, i);
+    run(0);
+    for (auto& x : th) x.join();
+    std::array<LSE, 5> tot;
+    long n = 0;
+    for (int i = 0; i < threads; i++) {
+        for (int q = 0; q < 5; q++) tot[q].merge(acc[i][q]);
+        n += cnt[i];
+    }
+    for (int q = 0; q < 5; q++) out[q] = tot[q].value();
+    *n_patterns = n;
     return 0;
 }
 

@@ -946,16 +946,25 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             nc1 = fma(Q[0][3], f1, nc1);
             npat += ALLPRES ? 27.0 : wac * bW[bs];
         };
-        if (!diag && ((j1 - j0) & 1) == 0) {
+        // Steps on which every lane is active run pipelined: the whole walk of an
+        // off-diagonal tile, and steps 1..30 of a diagonal tile whose a lies
+        // outside its block (pairs {slot, t} of the block, no padding lane).  The
+        // rest (a inside the block, step 31 / 32, padding) take the masked loop.
+        int je = j0;
+        if (!diag)
+            je = j0 + ((j1 - j0) & ~1);
+        else if ((va < 64 * K || va >= 64 * K + 64) && 64 * K >= pad)
+            je = j0 + ((min(j1, 32) - j0) & ~1);
+        if (je > j0) {
             // unrolled by two: the chained state alternates between (NA, qA) and (NB, qB)
-            double2 g_next = g01[min(j0 + 1, j1 - 1) * 64];
+            double2 g_next = g01[min(j0 + 1, je - 1) * 64];
             double2 m_cur = mnx;
             int2 n_cur = nnx;
             int NA[2], NB[2];
             double qA[2], qB[2];
             chain(j0, gnx, NA, qA);
-            for (int j = j0; j < j1; j += 2) {
-                const int r1 = min(j + 1, j1 - 1), r2 = min(j + 2, j1 - 1), r3 = min(j + 3, j1 - 1);
+            for (int j = j0; j < je; j += 2) {
+                const int r1 = min(j + 1, je - 1), r2 = min(j + 2, je - 1), r3 = min(j + 3, je - 1);
                 const double2 m_nxt = m01[r1 * 64];
                 const int2 n_nxt = bnn[r1 * 64];
                 const double2 g_after = g01[r2 * 64];
@@ -971,29 +980,35 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 finish(j + 1, NB, qB, m_nxt, n_nxt);
                 __builtin_amdgcn_wave_barrier();
             }
-        } else {
-            for (int j = j0; j < j1; j++) {
-                const double2 gcur = gnx, mcur = mnx;
-                const int2 ncur = nnx;
-                if (j + 1 < j1) {
-                    gnx = g01[(j + 1) * 64];
-                    mnx = m01[(j + 1) * 64];
-                    nnx = bnn[(j + 1) * 64];
-                }
-                const int bs = (t + j) & 63;
-                const int vb = 64 * K + bs;
-                // the pair {slot, t} of the block with a below both, or any real pair
-                // when a lies after the block (steps 1..31, + 32 on lanes < 32)
-                const bool act = ((vb > va && vc > va) || (va >= 64 * K + 64 && vb >= pad && vc >= pad)) &&
-                                 (j < 32 || t < 32);
-                if (act) {
-                    int N[2];
-                    double q[2];
-                    chain(j, gcur, N, q);
-                    finish(j, N, q, mcur, ncur);
-                }
-                __builtin_amdgcn_wave_barrier();
+            if (je < j1) {
+                gnx = g01[je * 64];
+                mnx = m01[je * 64];
+                nnx = bnn[je * 64];
             }
+        }
+        for (int j = je; j < j1; j++) {
+            const double2 gcur = gnx, mcur = mnx;
+            const int2 ncur = nnx;
+            if (j + 1 < j1) {
+                gnx = g01[(j + 1) * 64];
+                mnx = m01[(j + 1) * 64];
+                nnx = bnn[(j + 1) * 64];
+            }
+            const int bs = (t + j) & 63;
+            const int vb = 64 * K + bs;
+            // off-diagonal: a < block K < block C.  Diagonal: the pair {slot, t} of
+            // the block with a below both, or any real pair when a lies after the
+            // block (steps 1..31, + 32 on lanes < 32)
+            const bool act = diag ? (((vb > va && vc > va) || (va >= 64 * K + 64 && vb >= pad && vc >= pad)) &&
+                                     (j < 32 || t < 32))
+                                  : (okc && vb > va && vb < vc);
+            if (act) {
+                int N[2];
+                double q[2];
+                chain(j, gcur, N, q);
+                finish(j, N, q, mcur, ncur);
+            }
+            __builtin_amdgcn_wave_barrier();
         }
         if (__builtin_amdgcn_ballot_w64(tiny))
             if (tiny) atomicOr(flag, 1);

@@ -463,3 +463,85 @@ def test_max_size_m2000_c3_properties(gpu):
     assert g.n_configs == a.n_configs
     d = np.abs(_sexp(g.post, g.total) - _sexp(a.post, a.total)).max()
     assert d <= 1e-12
+
+
+def _member_pins(pc_accum, seam, snps, rtol=1e-10):
+    """Engine accumulators of the given union SNPs against the oracle's
+    per-SNP sums over every union set containing the SNP (oracle.member_sums):
+    value pins at loci too large for the whole-sweep oracle."""
+    m0 = int(seam.m[0])
+    for u in snps:
+        r = O.member_sums(seam, u)
+        l0, l1 = seam.union_to_local[:, u]
+        got = [pc_accum.post[l0] if l0 >= 0 else 0.0, pc_accum.post[m0 + l1] if l1 >= 0 else 0.0,
+               pc_accum.shared[u], pc_accum.shared_ll[u], pc_accum.notshared_ll[u]]
+        want = [r["post0"], r["post1"], r["shared"], r["shared_ll"], r["notshared_ll"]]
+        np.testing.assert_allclose(got, want, rtol=rtol, atol=0, err_msg=f"SNP {u}")
+
+
+def test_headline_locus_value_pins(gpu):
+    """BASELINE configs[3], the bench locus (SYN-v1 M = 1000, c = 3, 4.49e9
+    configurations) through the GPU Model setup: post (both studies), shared,
+    sharedLL and notSharedLL of five SNPs — the planted shared causal (250),
+    the study-0 causal (750), both ends and the middle — each against an exact
+    sum over its 13.5M assignments by the oracle (about 2 s per SNP on 16
+    host threads)."""
+    M = 1000
+    ld, z, _, _, u2l = synth.syn_v1(M)
+    mi = E.model_inputs(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    pc = E.PostCal(mi)
+    pc.run_exhaustive()
+    a = pc.accum()
+    assert a.n_configs == 4_491_007_501
+    seam = O.cholesky_seam(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    _member_pins(a, seam, [250, 750, 0, 499, 999])
+    pc.close()
+
+
+def test_syn500c3_full_size(gpu):
+    """BASELINE configs[2] at full size (SYN-v1 M = 500, c = 3, 560,253,751
+    configurations): exact count, four SNPs pinned against the oracle's
+    per-SNP sums, and a world-2 shard fold equal to the single pass."""
+    import torch
+    M = 500
+    ld, z, _, _, u2l = synth.syn_v1(M)
+    mi = E.model_inputs(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    pc = E.PostCal(mi)
+    pc.run_exhaustive()
+    a = pc.accum()
+    assert a.n_configs == 560_253_751 == mi.count_configs()
+    seam = O.cholesky_seam(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    _member_pins(a, seam, [125, 375, 0, 499])
+    nb = pc.partials_bytes()
+    buf = torch.empty(2 * nb, dtype=torch.uint8, device="cuda")
+    for r in range(2):
+        x = E.PostCal(mi)
+        x.set_shard(r, 2)
+        x.run_exhaustive()
+        x.export_partials(buf.data_ptr() + r * nb)
+        x.close()
+    torch.cuda.synchronize()
+    m = E.PostCal(mi)
+    m.merge_partials(buf.data_ptr(), 2)
+    g = m.accum()
+    assert g.n_configs == a.n_configs
+    assert np.abs(_sexp(g.post, g.total) - _sexp(a.post, a.total)).max() <= 1e-12
+    m.close()
+    pc.close()
+
+
+def test_sss_m2000_c5_full_size(gpu):
+    """BASELINE configs[4] at full size (SYN-v1 M = 2000, -c 5 -q 1) through the
+    GPU Model setup, against the whole oracle SSS walk (sss_postcal.cpp:102-380,
+    same mt19937(12345) draws) on a Cholesky seam: the same walk (2 iterations,
+    23,993 configurations) and every accumulator at parity."""
+    M = 2000
+    ld, z, _, _, u2l = synth.syn_v1(M)
+    mi = E.model_inputs(ld, z, u2l, (10000, 8000), max_causal=5, sharing_param=0.25)
+    pc = E.PostCal(mi)
+    it = pc.run_sss()
+    a = pc.accum()
+    assert it == 2 and a.n_configs == 23_993
+    seam = O.cholesky_seam(ld, z, u2l, (10000, 8000), max_causal=5, sharing_param=0.25)
+    assert_parity(a, O.postcal(seam, "sss"), pip_tol=1e-9, ll_rtol=1e-9)
+    pc.close()

@@ -6,9 +6,11 @@ import shutil
 import subprocess
 
 import numpy as np
+import pytest
 
 import loci
 from oracle import oracle as O
+from pipsort_amd import engine as E
 
 FILES = ("study0_post", "study1_post", "study0_set", "study1_set", "nocausal", "shared_pips")
 
@@ -69,3 +71,42 @@ def test_configs_file_and_sss_paths():
     # the walk hits "no new configurations" after 2 iterations and the null
     # configuration is accumulated twice (sss_postcal.cpp:202 then as a minus-neighbour)
     assert s["n_configs"] == 25
+
+
+@pytest.mark.parametrize("spec_c", [("small", 3), ("mixed", 3), ("syn", 2)])
+def test_member_sums_checker_matches_whole_oracle(spec_c):
+    """oracle.member_sums (the per-SNP checker used at loci too large for the
+    whole-sweep oracle) reproduces the whole-sweep oracle's post / shared /
+    sharedLL / notSharedLL entries of every union SNP."""
+    from pipsort_amd import synth
+    name, c = spec_c
+    if name == "small":
+        seam, _ = loci.seam_for(loci.SMALL, c=c)
+    elif name == "mixed":
+        ld, z, _, _, u2l = synth.mixed_locus(30, 25, 12, seed=7)
+        seam = E.seam_from_arrays(ld, z, u2l, (5000, 9000), max_causal=c, sharing_param=0.5)
+    else:
+        ld, z, _, _, u2l = synth.syn_v1(40)
+        seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=c, sharing_param=0.25)
+    ref = O.postcal(seam)
+    m0 = int(seam.m[0])
+    for u in range(seam.n_union):
+        g = O.member_sums(seam, u, threads=4)
+        l0, l1 = seam.union_to_local[:, u]
+        want = [ref["post"][l0] if l0 >= 0 else 0.0, ref["post"][m0 + l1] if l1 >= 0 else 0.0,
+                ref["shared"][u], ref["shared_ll"][u], ref["notshared_ll"][u]]
+        got = [g["post0"], g["post1"], g["shared"], g["shared_ll"], g["notshared_ll"]]
+        np.testing.assert_allclose(got, want, rtol=1e-12, atol=0, err_msg=f"u={u}")
+
+
+def test_cholesky_seam_equals_eigen_seam():
+    """A Cholesky seam (B = L^T, S' = L^-1 z) gives the eigen-route seam's
+    accumulators (the path consumes only B^T B, B^T S', ||S'||^2)."""
+    from pipsort_amd import synth
+    ld, z, _, _, u2l = synth.syn_v1(50)
+    a = O.postcal(E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25))
+    b = O.postcal(O.cholesky_seam(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25))
+    assert a["n_configs"] == b["n_configs"]
+    for k in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+        np.testing.assert_allclose(a[k], b[k], rtol=1e-11, atol=0, err_msg=k)
+    assert abs(a["total"] - b["total"]) <= 1e-11 * abs(a["total"])
