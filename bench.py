@@ -254,8 +254,40 @@ def sss_probe(reps=20):
             "gpu_model_setup_and_create_ms": setup_ms, "walk_iterations": iters, "walk_configs": walk_configs,
             "walk_ms": walk_ms, "batch_sets": len(sets), "batch_configs": npat, "batch_ms": batch_ms,
             "batch_configs_per_s": npat / (batch_ms / 1e3),
-            "multi_gpu": "replicas only: the walk is serial (host mt19937 sampling between batches) and one "
-                         "batch is sub-millisecond on one GPU"}
+            "multi_gpu": "sharded under --gpus N (psx_run_sss_sharded: every iteration's batch split over the "
+                         "ranks, one all-gather of scores per iteration); this N = 1 line times one GPU"}
+
+
+def configs_probe(reps=3):
+    """The -b configs-file enumerator (postcal.cpp:400-714) at scale: a file
+    made by the restated generator (synth.construct_configs =
+    utils/construct_configs_all_studies.py:50-158) for SYN-v1 M = 1000 with
+    three 12-SNP groups per study around the planted signals: 13^6 = 4,826,809
+    rows of 6 int16 global indices.  Timed: psx_run_configs from the host rows
+    (parallel host row preprocessing, one upload, the GPU evaluation and
+    merges), inputs already set up on the GPU; best of `reps`."""
+    M = 1000
+    ld, z, _, _, u2l = synth.syn_v1(M)
+    mi = E.model_inputs(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    grp = [list(range(c - 6, c + 6)) for c in (M // 4, M // 2, 3 * M // 4)]
+    rows = synth.construct_configs([grp, grp], [M, M])
+    pc = E.PostCal(mi)
+    pc.run_configs(rows)  # warm-up (buffers)
+    best = None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pc.run_configs(rows)
+        dt = time.perf_counter() - t0
+        if best is None or dt < best[0]:
+            best = (dt, pc.timing())
+    n = pc.accum().n_configs
+    pc.close()
+    dt, tm = best
+    return {"workload": "SYN-v1 M=1000 -c 3, -b file of 3 x 12-SNP groups per study (construct_configs_all_studies)",
+            "rows": int(rows.shape[0]), "n_groups": int(rows.shape[1]), "configs_checked": int(n),
+            "wall_ms": dt * 1e3, "configs_per_s": rows.shape[0] / dt, "kernel_ms": tm["kernel_ms"],
+            "note": "host rows -> parallel preprocessing -> one upload -> k_eval_sets + merges; best of %d" % reps}
 
 
 def torch_allgather(backend):
@@ -589,6 +621,10 @@ def main():
         else:
             out["pcie_inclusive"] = pcie_inclusive(seam, configs_per_step, local)
             out["sss"] = sss_probe()
+            try:
+                out["configs_file"] = configs_probe()
+            except Exception as ex:  # noqa: BLE001  (a side measurement must not lose the line)
+                out["configs_file"] = {"error": f"{type(ex).__name__}: {ex}"}
             w, same = example_wall()
             out["example_wall_s"] = w
             out["example_outputs_match_reference"] = same

@@ -18,6 +18,7 @@
 #include <tuple>
 #include <unordered_map>
 #include <vector>
+#include <thread>
 
 #include "../../include/pipsort_engine.h"
 #include "../../include/pipsort_model.h"
@@ -666,38 +667,24 @@ void build_csr(const std::vector<int>& sets, int stride, size_t nsets, int U, st
 
 // Evaluate a batch of union sets with the generic kernel; optionally fold all
 // patterns into the accumulators and/or return SSS scores.
-int eval_generic(psx_engine* e, const std::vector<int>& sets, int stride, size_t nsets, const int* forced,
-                 bool accumulate, double* scores, double* kernel_ms) {
-    if (nsets == 0) return 0;
-    if (stride > PSX_KMAX) return fail(PSX_ERANGE, "union set larger than PSX_KMAX");
+// k_eval_sets over n sets staged in e->hstage as [sets (n * stride) | forced
+// (n * 2, optional) | CSR ptr | idx | rows (accumulate)]: one upload, the
+// kernel, the deterministic record merges.
+int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool has_forced, size_t n_ptr, size_t n_idx,
+                        size_t n_rows, bool accumulate, double* scores, double* kernel_ms) {
     int rc;
-    std::vector<int> ptr, idx, rows;
-    if (accumulate) build_csr(sets, stride, nsets, e->U, ptr, idx, rows);
-    const size_t n_sets = nsets * stride, n_forced = forced ? nsets * 2 : 0;
-    const size_t n_csr = ptr.size() + idx.size() + rows.size();
-    const size_t total = n_sets + n_forced + n_csr;
+    const size_t n_sets = nsets * stride, n_forced = has_forced ? nsets * 2 : 0;
+    const size_t total = n_sets + n_forced + n_ptr + n_idx + n_rows;
     if ((rc = ensure(e->dgen, e->cap_gen, total))) return rc;
     if ((rc = ensure(e->dsrec, e->cap_srec, nsets))) return rc;
     if ((rc = ensure(e->dmrec, e->cap_mrec, nsets * stride))) return rc;
     if (scores && (rc = ensure(e->dscore, e->cap_score, nsets))) return rc;
-    // one upload: the staging buffer is reused once its previous upload is done
-    if (e->stage_rec) HIPCHK(hipEventSynchronize(e->stage_ev));
-    if ((rc = ensure_host(e->hstage, e->cap_stage, total))) return rc;
-    int* h = e->hstage;
-    std::memcpy(h, sets.data(), n_sets * sizeof(int));
-    if (forced) std::memcpy(h + n_sets, forced, n_forced * sizeof(int));
-    int* hc = h + n_sets + n_forced;
-    if (accumulate) {
-        std::memcpy(hc, ptr.data(), ptr.size() * sizeof(int));
-        std::memcpy(hc + ptr.size(), idx.data(), idx.size() * sizeof(int));
-        std::memcpy(hc + ptr.size() + idx.size(), rows.data(), rows.size() * sizeof(int));
-    }
-    HIPCHK(hipMemcpyAsync(e->dgen, h, total * sizeof(int), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(e->dgen, e->hstage, total * sizeof(int), hipMemcpyHostToDevice, e->stream));
     if (!e->stage_ev) HIPCHK(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
     HIPCHK(hipEventRecord(e->stage_ev, e->stream));
     e->stage_rec = true;
     const int* dsets = e->dgen;
-    const int* dforced = forced ? e->dgen + n_sets : nullptr;
+    const int* dforced = has_forced ? e->dgen + n_sets : nullptr;
     const int* dcsr = e->dgen + n_sets + n_forced;
     if (kernel_ms) HIPCHK(hipEventRecord(e->ev[2], e->stream));
     hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)nsets), dim3(64), 0, e->stream, e->dp, dsets, stride, dforced,
@@ -705,8 +692,8 @@ int eval_generic(psx_engine* e, const std::vector<int>& sets, int stride, size_t
     HIPCHK(hipGetLastError());
     if (kernel_ms) HIPCHK(hipEventRecord(e->ev[3], e->stream));
     if (accumulate) {
-        if (psx::launch_merge_members(e->dmrec, dcsr, dcsr + ptr.size(), dcsr + ptr.size() + idx.size(),
-                                      (int)rows.size(), e->dacc, e->stream))
+        if (psx::launch_merge_members(e->dmrec, dcsr, dcsr + n_ptr, dcsr + n_ptr + n_idx, (int)n_rows, e->dacc,
+                                      e->stream))
             return fail(PSX_EHIP, psx::sweep_error());
         SetRec none = psx::set_zero();
         if (psx::launch_merge_sets(e->dsrec, (long)nsets, none, e->dsacc, e->stream))
@@ -725,6 +712,31 @@ int eval_generic(psx_engine* e, const std::vector<int>& sets, int stride, size_t
         *kernel_ms += ms;
     }
     return 0;
+}
+
+int eval_generic(psx_engine* e, const std::vector<int>& sets, int stride, size_t nsets, const int* forced,
+                 bool accumulate, double* scores, double* kernel_ms) {
+    if (nsets == 0) return 0;
+    if (stride > PSX_KMAX) return fail(PSX_ERANGE, "union set larger than PSX_KMAX");
+    int rc;
+    std::vector<int> ptr, idx, rows;
+    if (accumulate) build_csr(sets, stride, nsets, e->U, ptr, idx, rows);
+    const size_t n_sets = nsets * stride, n_forced = forced ? nsets * 2 : 0;
+    const size_t total = n_sets + n_forced + ptr.size() + idx.size() + rows.size();
+    // the staging buffer is reused once its previous upload is done
+    if (e->stage_rec) HIPCHK(hipEventSynchronize(e->stage_ev));
+    if ((rc = ensure_host(e->hstage, e->cap_stage, total))) return rc;
+    int* h = e->hstage;
+    std::memcpy(h, sets.data(), n_sets * sizeof(int));
+    if (forced) std::memcpy(h + n_sets, forced, n_forced * sizeof(int));
+    int* hc = h + n_sets + n_forced;
+    if (accumulate) {
+        std::memcpy(hc, ptr.data(), ptr.size() * sizeof(int));
+        std::memcpy(hc + ptr.size(), idx.data(), idx.size() * sizeof(int));
+        std::memcpy(hc + ptr.size() + idx.size(), rows.data(), rows.size() * sizeof(int));
+    }
+    return eval_generic_staged(e, stride, nsets, forced != nullptr, ptr.size(), idx.size(), rows.size(), accumulate,
+                               scores, kernel_ms);
 }
 
 // `count` null configurations (postcal.cpp:793-822) as a set record
@@ -1555,46 +1567,54 @@ int psx_run_configs(psx_engine* e, const int16_t* rows, int64_t n_rows, int32_t 
     int rc;
     if ((rc = reset_acc(e))) return rc;
     std::memset(&e->timing, 0, sizeof(e->timing));
+    if (n_rows < 0 || n_groups < 0 || (n_rows > 0 && (!rows || n_groups == 0)))
+        return fail(PSX_EINVAL, "bad configs rows");
+    // this rank's contiguous slice of the rows (psx_set_shard)
+    const int64_t r0 = n_rows * e->rank / e->world, r1 = n_rows * (e->rank + 1) / e->world;
     const int stride = PSX_KMAX;
-    std::vector<int> sets;
-    std::vector<int> forced;
-    double nulls = 0;
-    int off1 = e->m[0];
+    if ((r1 - r0) * stride >= (int64_t)INT32_MAX) return fail(PSX_ERANGE, "configs file too large for one pass");
     // idx_to_union_pos_map (model.h:134-139)
     std::vector<int> l2u[2];
     for (int s = 0; s < 2; s++)
         for (int u = 0; u < e->U; u++)
             if (e->u2l[s * e->U + u] >= 0) l2u[s].push_back(u);
-    HIPCHK(hipEventRecord(e->ev[0], e->stream));
-    for (int64_t r = 0; r < n_rows; r++) {
-        const int16_t* in = rows + r * n_groups;
-        std::vector<int> locs;
-        int numc = 0;
+    const int off1 = e->m[0];
+    // One row of computeTotalLikelihoodGivenConfigs (postcal.cpp:441-590):
+    // global indices -> union positions (sorted, unique), then the walk that
+    // assigns each entry to (study, member) and rejects rows out of order.
+    // Returns k (0: null row), -1 index out of range, -2 > PSX_KMAX members,
+    // -3 the walk failed (postcal.cpp:587-590).
+    auto parse = [&](const int16_t* in, int* locs, int* b) -> int {
+        int n = 0;
+        bool over = false;
         for (int i = 0; i < n_groups; i++) {
-            int g = in[i];
+            const int g = in[i];
             if (g < 0) continue;
-            if (g >= e->N) return fail(PSX_EINVAL, "configs row index outside the SNP range");
-            numc++;
-            int st = g >= off1 ? 1 : 0;  // postcal.cpp:500-504
-            locs.push_back(l2u[st][g - (st ? off1 : 0)]);
+            if (g >= e->N) return -1;
+            const int st = g >= off1 ? 1 : 0;  // postcal.cpp:500-504
+            const int u = l2u[st][g - (st ? off1 : 0)];
+            int j = n;  // insertion into the sorted unique list
+            bool dup = false;
+            for (int q = 0; q < n; q++) dup |= locs[q] == u;
+            if (dup) continue;
+            if (n == stride) { over = true; continue; }
+            while (j > 0 && locs[j - 1] > u) { locs[j] = locs[j - 1]; j--; }
+            locs[j] = u;
+            n++;
         }
-        if (numc == 0) { nulls += 1; continue; }  // postcal.cpp:459-488
-        std::sort(locs.begin(), locs.end());
-        locs.erase(std::unique(locs.begin(), locs.end()), locs.end());
-        int k = (int)locs.size();
-        if (k > PSX_KMAX) return fail(PSX_ERANGE, "configs row has more than 6 union SNPs");
-        // postcal.cpp:546-590: walk the row in (study, union position) order
-        int b[2] = {0, 0};
+        if (over) return -2;
+        if (n == 0) return 0;  // postcal.cpp:459-488
+        b[0] = b[1] = 0;
         int aux = 0;
         while (aux < n_groups && in[aux] < 0) aux++;
         int cum = 0;
         for (int i = 0; i < 2; i++) {
             cum += e->m[i];
-            int offi = i ? off1 : 0;
-            for (int j = 0; j < k; j++) {
-                int loc = e->u2l[i * e->U + locs[j]];
+            const int offi = i ? off1 : 0;
+            for (int j = 0; j < n; j++) {
+                const int loc = e->u2l[i * e->U + locs[j]];
                 if (loc >= 0) {
-                    int gidx = offi + loc;
+                    const int gidx = offi + loc;
                     if (gidx >= cum) break;
                     if (aux < n_groups && in[aux] == gidx) {
                         aux++;
@@ -1605,15 +1625,119 @@ int psx_run_configs(psx_engine* e, const int16_t* rows, int64_t n_rows, int32_t 
             }
             if (aux == n_groups) break;
         }
-        if (aux != n_groups) return fail(PSX_EORDER, "This did not work as expected (postcal.cpp:587-590)");
-        for (int j = 0; j < stride; j++) sets.push_back(j < k ? locs[j] : -1);
-        forced.push_back(b[0]);
-        forced.push_back(b[1]);
+        return aux == n_groups ? n : -3;
+    };
+    HIPCHK(hipEventRecord(e->ev[0], e->stream));
+    // Host preprocessing, parallel over contiguous row chunks and allocation-free
+    // per row.  Pass 1 validates and counts (non-null rows, records per union
+    // SNP); pass 2 writes the sets, forced masks and the record CSR straight into
+    // the pinned staging buffer at offsets fixed by the chunk order, so the
+    // result is identical to a serial pass (deterministic merges).
+    const int64_t nr = r1 - r0;
+    const int T = (int)std::max<int64_t>(1, std::min<int64_t>(
+        std::min(16u, std::max(1u, std::thread::hardware_concurrency())), (nr + 4095) / 4096));
+    std::vector<int64_t> c_sets(T, 0), c_nulls(T, 0), c_err(T, INT64_MAX);
+    std::vector<int> c_code(T, 0);
+    std::vector<std::vector<int>> c_hist(T);
+    auto chunk = [&](int t, int64_t& a, int64_t& b) {
+        a = r0 + nr * t / T;
+        b = r0 + nr * (t + 1) / T;
+    };
+    auto pass1 = [&](int t) {
+        int64_t a, b;
+        chunk(t, a, b);
+        std::vector<int>& h = c_hist[t];
+        h.assign(e->U, 0);
+        int locs[PSX_KMAX], bb[2];
+        for (int64_t r = a; r < b; r++) {
+            const int k = parse(rows + r * n_groups, locs, bb);
+            if (k < 0) { c_err[t] = r; c_code[t] = k; return; }
+            if (k == 0) { c_nulls[t]++; continue; }
+            c_sets[t]++;
+            for (int j = 0; j < k; j++) h[locs[j]]++;
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; t++) th.emplace_back(pass1, t);
+        pass1(0);
+        for (auto& x : th) x.join();
     }
-    size_t ns = forced.size() / 2;
+    for (int t = 0; t < T; t++)  // the first failing row in row order
+        if (c_err[t] != INT64_MAX) {
+            if (c_code[t] == -1) return fail(PSX_EINVAL, "configs row index outside the SNP range");
+            if (c_code[t] == -2) return fail(PSX_ERANGE, "configs row has more than 6 union SNPs");
+            return fail(PSX_EORDER, "This did not work as expected (postcal.cpp:587-590)");
+        }
+    int64_t nsets = 0, nulls = 0;
+    std::vector<int64_t> set_off(T, 0);
+    for (int t = 0; t < T; t++) {
+        set_off[t] = nsets;
+        nsets += c_sets[t];
+        nulls += c_nulls[t];
+    }
+    // CSR of records (set * stride + member) by union SNP, in record order
+    std::vector<int> cnt(e->U, 0);
+    for (int t = 0; t < T; t++)
+        for (int u = 0; u < e->U; u++) cnt[u] += c_hist[t][u];
+    std::vector<int> ptr(1, 0), rowsnp;
+    std::vector<int64_t> start(e->U, 0);
+    int64_t acc = 0;
+    for (int u = 0; u < e->U; u++)
+        if (cnt[u]) {
+            start[u] = acc;
+            rowsnp.push_back(u);
+            acc += cnt[u];
+            ptr.push_back((int)acc);
+        }
+    // per-chunk fill offsets: chunk t's records of SNP u follow chunks < t
+    std::vector<std::vector<int64_t>> c_start(T, std::vector<int64_t>(e->U, 0));
+    for (int u = 0; u < e->U; u++) {
+        int64_t run = start[u];
+        for (int t = 0; t < T; t++) {
+            c_start[t][u] = run;
+            run += c_hist[t][u];
+        }
+    }
+    const size_t n_sets = (size_t)nsets * stride, n_forced = (size_t)nsets * 2;
+    const size_t total = n_sets + n_forced + ptr.size() + (size_t)acc + rowsnp.size();
+    if (e->stage_rec) HIPCHK(hipEventSynchronize(e->stage_ev));
+    if (nsets > 0 && (rc = ensure_host(e->hstage, e->cap_stage, total))) return rc;
+    int* const hsets = e->hstage;
+    int* const hforced = hsets + n_sets;
+    int* const hptr = hforced + n_forced;
+    int* const hidx = hptr + ptr.size();
+    int* const hrows = hidx + acc;
+    auto pass2 = [&](int t) {
+        int64_t a, b;
+        chunk(t, a, b);
+        std::vector<int64_t>& fill = c_start[t];
+        int64_t si = set_off[t];
+        int locs[PSX_KMAX], bb[2];
+        for (int64_t r = a; r < b; r++) {
+            const int k = parse(rows + r * n_groups, locs, bb);
+            if (k <= 0) continue;
+            int* S = hsets + si * stride;
+            for (int j = 0; j < stride; j++) S[j] = j < k ? locs[j] : -1;
+            hforced[2 * si] = bb[0];
+            hforced[2 * si + 1] = bb[1];
+            for (int j = 0; j < k; j++) hidx[fill[locs[j]]++] = (int)(si * stride + j);
+            si++;
+        }
+    };
+    if (nsets > 0) {
+        std::memcpy(hptr, ptr.data(), ptr.size() * sizeof(int));
+        std::memcpy(hrows, rowsnp.data(), rowsnp.size() * sizeof(int));
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; t++) th.emplace_back(pass2, t);
+        pass2(0);
+        for (auto& x : th) x.join();
+    }
     double kms = 0;
-    if ((rc = eval_generic(e, sets, stride, ns, forced.data(), true, nullptr, &kms))) return rc;
-    if ((rc = fold_null(e, nulls))) return rc;
+    if (nsets > 0 && (rc = eval_generic_staged(e, stride, (size_t)nsets, true, ptr.size(), (size_t)acc,
+                                               rowsnp.size(), true, nullptr, &kms)))
+        return rc;
+    if ((rc = fold_null(e, (double)nulls))) return rc;
     HIPCHK(hipEventRecord(e->ev[1], e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     float ms = 0;
@@ -1621,7 +1745,7 @@ int psx_run_configs(psx_engine* e, const int16_t* rows, int64_t n_rows, int32_t 
     e->timing.sweep_ms = ms;
     e->timing.kernel_ms = kms;
     e->timing.kernel_launches = 1;
-    e->timing.configs = (uint64_t)n_rows;
+    e->timing.configs = (uint64_t)nr;
     return 0;
 }
 

@@ -91,3 +91,69 @@ def write_locus(dirpath: str, ld, z, names, rows, prefix="syn"):
             f.write(f"{r[0]},{r[1]},{r[2]}\n")
     # model.h:100-103 needs the z names to be the SNP names of the study
     return dirpath
+
+
+def construct_configs(groups, num_snps):
+    """The -b configs file of utils/construct_configs_all_studies.py:50-158:
+    `groups[s]` lists study s's groups (its important-SNP file's rows cut by
+    sorted group id, :50-65) as local SNP indices; each group contributes
+    either no SNP (-1) or one of its SNPs, offset by the studies before it
+    (:70-78); rows are the Cartesian product of the groups in order, the first
+    varying slowest (:98-106), with each row's non-negative entries sorted in
+    place (special_sort, :131-139).  Returns int16 [n_configs, n_groups]."""
+    arrs = []
+    off = 0
+    for s, gs in enumerate(groups):
+        if s > 0:
+            off += int(num_snps[s - 1])
+        for g in gs:
+            arrs.append(np.concatenate([[-1], np.asarray(g, dtype=np.int64) + off]).astype(np.int16))
+    if not arrs:
+        return np.full((1, 1), -1, dtype=np.int16)
+    grid = np.stack(np.meshgrid(*arrs, indexing="ij"), axis=-1).reshape(-1, len(arrs))
+    # special_sort: sorted non-negative entries back into the non-negative slots
+    pos = grid >= 0
+    key = np.where(pos, grid.astype(np.int32), np.iinfo(np.int32).max)
+    srt = np.sort(key, axis=1)
+    out = np.full(grid.shape, -1, dtype=np.int16)
+    rank = np.cumsum(pos, axis=1) - 1
+    rows_i = np.nonzero(pos)
+    out[rows_i] = srt[rows_i[0], rank[rows_i]].astype(np.int16)
+    return out
+
+
+def read_imp_snps(path):
+    """One study's important-SNP file as construct_configs_all_studies.py:20-26,
+    50-65 reads it (tab separated, column 2 the local index, column 3 the group
+    id; rows taken in file order, cut by the sorted group ids' counts)."""
+    if not os.path.exists(path) or os.path.getsize(path) == 0:
+        return []
+    cols = [l.rstrip("\n").split("\t") for l in open(path) if l.strip()]
+    gid = np.array([float(c[3]) for c in cols])
+    loc = [int(float(c[2])) for c in cols]
+    _, counts = np.unique(gid, return_counts=True)
+    out, o = [], 0
+    for n in counts:
+        out.append(loc[o:o + n])
+        o += n
+    return out
+
+
+def all_configs_rows(union_to_local, m, c):
+    """Every configuration of an exhaustive sweep up to c union SNPs
+    (postcal.cpp:716-1092: union subsets, then the per-study assignments
+    passing checkOR) as -b rows of global indices (study 1 offset by M_0),
+    ascending, -1 padded to 2c columns; the null configuration is the all -1
+    row."""
+    import itertools
+    u2l = np.asarray(union_to_local)
+    U = u2l.shape[1]
+    allowed = [[x for x in (1, 2, 3) if all(not (x >> s) & 1 or u2l[s, u] >= 0 for s in range(2))] for u in range(U)]
+    rows = [[-1] * (2 * c)]
+    for k in range(1, c + 1):
+        for S in itertools.combinations(range(U), k):
+            for xs in itertools.product(*(allowed[u] for u in S)):
+                g = sorted([int(u2l[0, u]) for u, x in zip(S, xs) if x & 1] +
+                           [int(m[0]) + int(u2l[1, u]) for u, x in zip(S, xs) if x & 2])
+                rows.append(g + [-1] * (2 * c - len(g)))
+    return np.array(rows, dtype=np.int16)

@@ -112,6 +112,47 @@ def test_configs_file_path(gpu):
     assert_parity(pc.accum(), O.postcal(seam, "configs", rows))
 
 
+def test_configs_file_listing_every_configuration(gpu):
+    """A -b file listing every configuration of a locus (synth.all_configs_rows)
+    reproduces the exhaustive sweep's accumulators (47,832 rows of a mixed-membership locus,
+    shuffled), and the oracle's configs enumerator
+    (postcal.cpp:400-714) on the same rows; split over three shards
+    (psx_set_shard: contiguous row ranges) and merged, the same again."""
+    import torch
+    ld, z, _, _, u2l = synth.mixed_locus(30, 25, 12, seed=11)
+    seam = E.seam_from_arrays(ld, z, u2l, (5000, 9000), max_causal=3, sharing_param=0.5)
+    rows = synth.all_configs_rows(seam.union_to_local, seam.m, 3)
+    rows = rows[np.random.default_rng(1).permutation(rows.shape[0])]
+    pc = E.PostCal(seam)
+    pc.run_configs(rows)
+    got = pc.accum()
+    assert got.n_configs == rows.shape[0] == seam.count_configs()
+    assert_parity(got, O.postcal(seam, "configs", rows), pip_tol=1e-9, ll_rtol=1e-9)
+    ex = E.PostCal(seam)
+    ex.run_exhaustive()
+    ref = ex.accum()
+    for f in ("post", "no_causal", "shared"):
+        assert np.abs(_sexp(getattr(got, f), got.total) - _sexp(getattr(ref, f), ref.total)).max() <= 1e-12, f
+    for f in ("shared_ll", "notshared_ll"):
+        np.testing.assert_allclose(getattr(got, f), getattr(ref, f), rtol=1e-11, err_msg=f)
+    nb = pc.partials_bytes()
+    buf = torch.empty(3 * nb, dtype=torch.uint8, device="cuda")
+    for r in range(3):
+        x = E.PostCal(seam)
+        x.set_shard(r, 3)
+        x.run_configs(rows)
+        x.export_partials(buf.data_ptr() + r * nb)
+        x.close()
+    torch.cuda.synchronize()
+    m = E.PostCal(seam)
+    m.merge_partials(buf.data_ptr(), 3)
+    g = m.accum()
+    assert g.n_configs == got.n_configs
+    assert np.abs(_sexp(g.post, g.total) - _sexp(got.post, got.total)).max() <= 1e-12
+    for x in (pc, ex, m):
+        x.close()
+
+
 def test_configs_row_order_error(gpu):
     """postcal.cpp:587-590: a row whose entries are not study-major exits 1."""
     seam, _ = loci.seam_for(loci.CONFIGS)

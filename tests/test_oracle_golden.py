@@ -110,3 +110,32 @@ def test_cholesky_seam_equals_eigen_seam():
     for k in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
         np.testing.assert_allclose(a[k], b[k], rtol=1e-11, atol=0, err_msg=k)
     assert abs(a["total"] - b["total"]) <= 1e-11 * abs(a["total"])
+
+
+def test_construct_configs_matches_reference_script():
+    """synth.construct_configs restates utils/construct_configs_all_studies.py;
+    tests/golden/configs_gen/expected_* were written by the reference script
+    itself (make_fixture.py) on the small important-SNP files beside them,
+    including out-of-order groups that exercise its special_sort."""
+    from pipsort_amd import synth
+    d = os.path.join(loci.GOLDEN, "configs_gen")
+    n, g = [int(x) for x in open(os.path.join(d, "expected_dims.txt")).read().split()]
+    exp = np.fromfile(os.path.join(d, "expected_configs_int16"), dtype=np.int16).reshape(n, g)
+    got = synth.construct_configs([synth.read_imp_snps(os.path.join(d, "imp0.tsv")),
+                                   synth.read_imp_snps(os.path.join(d, "imp1.tsv"))], [9, 8])
+    assert got.dtype == np.int16 and np.array_equal(got, exp)
+
+
+def test_all_configs_rows_through_oracle_equal_exhaustive():
+    """A -b file listing every configuration of a locus, run through the
+    oracle's configs enumerator (postcal.cpp:400-714), gives the oracle's
+    exhaustive accumulators (postcal.cpp:716-1092)."""
+    from pipsort_amd import synth
+    ld, z, _, _, u2l = synth.mixed_locus(9, 8, 5, seed=3)
+    seam = E.seam_from_arrays(ld, z, u2l, (5000, 9000), max_causal=3, sharing_param=0.5)
+    rows = synth.all_configs_rows(seam.union_to_local, seam.m, 3)
+    a = O.postcal(seam)
+    b = O.postcal(seam, "configs", rows)
+    assert a["n_configs"] == b["n_configs"] == rows.shape[0]
+    for k in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+        np.testing.assert_allclose(b[k], a[k], rtol=1e-12, atol=0, err_msg=k)
