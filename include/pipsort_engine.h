@@ -223,6 +223,28 @@ int psx_fold_partials_host(const void *src, int32_t count, int64_t image_bytes, 
 int psx_shard_stats(const psx_problem *prob, int32_t k, int32_t rank, int32_t world, uint64_t *union_sets,
                     double *configs);
 
+/* ---- Several GPUs in one process --------------------------------------------
+ * The reference runs its whole-node sweep in one process, 64 OpenMP threads
+ * over the configurations (postcal.cpp:747-769).  A psx_multi holds one handle
+ * per entry of devices[] (entries may repeat: several shards on one GPU); handle
+ * i evaluates shard i of n (psx_set_shard), each driven by its own host thread,
+ * and every run returns with the shards' accumulators folded on devices[0]
+ * (peer copies of the partial images + psx_merge_partials, rank order, the
+ * fold of the multi-process path).  Same semantics as the single-handle calls;
+ * errors name the failing shard (psx_multi_last_error). */
+typedef struct psx_multi psx_multi;
+int psx_multi_create(const psx_problem *prob, const int32_t *devices, int32_t n, psx_multi **out);
+int psx_multi_create_from_ld(const psx_ld_problem *prob, const int32_t *devices, int32_t n, psx_multi **out,
+                             psx_setup_info *info);
+int psx_multi_run_exhaustive(psx_multi *m);                                        /* computeTotalLikelihood */
+int psx_multi_run_configs(psx_multi *m, const int16_t *rows, int64_t n_rows, int32_t n_groups);
+int psx_multi_run_sss(psx_multi *m, int32_t *iterations_out);                     /* sharded SSS walk */
+int psx_multi_get_accum(psx_multi *m, psx_accum *out);
+int psx_multi_get_timing(psx_multi *m, psx_timing *t);
+int32_t psx_multi_count(psx_multi *m);
+const char *psx_multi_last_error(void);
+void psx_multi_destroy(psx_multi *m);
+
 /* Timing of the last psx_run_* on this handle. */
 int psx_get_timing(psx_engine *e, psx_timing *t);
 

@@ -213,8 +213,10 @@ bool import_snp_map(const string& fn, int ncols, vector<string>& first, vector<v
 
 double special_exp(double post, double total) { return post == 0 ? 0 : std::exp(post - total); }  // postcal.h:277-283
 
+bool g_multi = false;  // several devices: errors come from the psx_multi layer
+
 int die_engine(int rc) {
-    std::cout << "engine error (" << rc << "): " << psx_last_error() << std::endl;
+    std::cout << "engine error (" << rc << "): " << (g_multi ? psx_multi_last_error() : psx_last_error()) << std::endl;
     if (rc == PSX_ESINGULAR) {
         std::cout << "Error the matrix is singular and we fail to fix it (low rank lkl)." << std::endl;
         exit(0);  // postcal.cpp:291-294
@@ -288,11 +290,39 @@ int main(int argc, char* argv[]) {
         exit(1);
     }
     auto t_setup0 = std::chrono::steady_clock::now();
-    int device = 0;
-    if (const char* d = getenv("PSX_DEVICE")) device = atoi(d);
-    // the HIP runtime / context comes up on a second thread while the inputs
+    // Devices: PSX_DEVICES="0,1,..." (entries may repeat), else PSX_DEVICE, else
+    // the visible GPUs the sweep can use — one process drives them all, as the
+    // reference's OpenMP threads use the whole node (postcal.cpp:747-769).  Each
+    // extra device costs its own context and Model setup (~0.1-0.2 s) while one
+    // MI355X sweeps ~3e12 configurations/s, so by default an exhaustive run
+    // takes one more device per 5e11 configurations (SSS walks and -b files:
+    // one device unless asked).
+    vector<int32_t> devices;
+    bool defer_devices = false;
+    if (const char* ds = getenv("PSX_DEVICES")) {
+        std::stringstream ss(ds);
+        string tok;
+        while (std::getline(ss, tok, ','))
+            if (!tok.empty()) devices.push_back(atoi(tok.c_str()));
+    } else if (const char* d = getenv("PSX_DEVICE")) {
+        devices.push_back(atoi(d));
+    } else {
+        devices.push_back(0);
+        defer_devices = true;  // decided once the locus size is known
+    }
+    if (devices.empty()) devices.push_back(0);
+    const int device = devices[0];
+    g_multi = devices.size() > 1;
+    // the HIP runtime / contexts come up on a second thread while the inputs
     // are parsed (errors, if any, surface again at psx_create*)
-    std::thread warm([device] { psx_warmup(device); });
+    std::thread warm([devices] {
+        vector<int32_t> seen;
+        for (int32_t d : devices)
+            if (std::find(seen.begin(), seen.end(), d) == seen.end()) {
+                seen.push_back(d);
+                psx_warmup(d);
+            }
+    });
     auto quit = [&warm](int code) {  // input errors below exit as the reference does, after the warm-up
         warm.join();
         exit(code);
@@ -327,11 +357,28 @@ int main(int argc, char* argv[]) {
         if (cnt != m[i]) { printf("Invariant does not hold\n"); quit(1); }
     }
     const int N = m[0] + m[1];
+    if (defer_devices && configsFile == "" && sss_flag != 1) {
+        // configurations of the exhaustive sweep: sum_k e_k(w_u), w_u = 2^{b_u} - 1
+        vector<long double> ek(totalCausalSNP + 1, 0.0L);
+        ek[0] = 1;
+        for (int u = 0; u < U; u++) {
+            const int b = (u2l[0][u] >= 0) + (u2l[1][u] >= 0);
+            for (int k = totalCausalSNP; k >= 1; k--) ek[k] += ek[k - 1] * (long double)((1 << b) - 1);
+        }
+        long double configs = 0;
+        for (long double v : ek) configs += v;
+        int nd = 0;
+        psx_device_count(&nd);
+        const int want = (int)std::min<long double>((long double)std::max(nd, 1), 1.0L + configs / 5e11L);
+        for (int i = 1; i < want; i++) devices.push_back(i);
+        g_multi = devices.size() > 1;
+    }
     vector<int32_t> u2l_flat(2 * U);
     for (int s = 0; s < 2; s++)
         for (int u = 0; u < U; u++) u2l_flat[s * U + u] = u2l[s][u];
     warm.join();
     psx_engine* eng = nullptr;
+    psx_multi* multi = nullptr;
     int rc;
     const char* hs = getenv("PSX_HOST_SETUP");
     if (!(hs && atoi(hs))) {
@@ -357,7 +404,10 @@ int main(int argc, char* argv[]) {
         q.t_squared = tau_sqr;
         q.s_squared = sigma_g_squared;
         psx_setup_info info;
-        rc = psx_create_from_ld(&q, device, &eng, &info);  // model.h:171-265
+        if (g_multi)
+            rc = psx_multi_create_from_ld(&q, devices.data(), (int32_t)devices.size(), &multi, &info);
+        else
+            rc = psx_create_from_ld(&q, device, &eng, &info);  // model.h:171-265
         if (rc == 0)
             for (int i = 0; i < S; i++)
                 std::cout << "study " << i << ": psd shift " << info.psd_added[i] << " ("
@@ -396,7 +446,8 @@ int main(int argc, char* argv[]) {
         prob.gamma = gamma;
         prob.t_squared = tau_sqr;
         prob.s_squared = sigma_g_squared;
-        rc = psx_create(&prob, device, &eng);  // model.h:265
+        rc = g_multi ? psx_multi_create(&prob, devices.data(), (int32_t)devices.size(), &multi)
+                     : psx_create(&prob, device, &eng);  // model.h:265
     }
     if (rc) die_engine(rc);
     auto t_setup1 = std::chrono::steady_clock::now();
@@ -422,14 +473,15 @@ int main(int argc, char* argv[]) {
         }
         void* p = sz ? mmap(nullptr, sz, PROT_READ, MAP_SHARED, fd, 0) : nullptr;
         close(fd);
-        rc = psx_run_configs(eng, (const int16_t*)p, num_configs, num_groups);
+        rc = g_multi ? psx_multi_run_configs(multi, (const int16_t*)p, num_configs, num_groups)
+                     : psx_run_configs(eng, (const int16_t*)p, num_configs, num_groups);
         if (p) munmap(p, sz);
     } else if (sss_flag == 1) {
         int32_t iters = 0;
-        rc = psx_run_sss(eng, &iters);
+        rc = g_multi ? psx_multi_run_sss(multi, &iters) : psx_run_sss(eng, &iters);
         printf("sss iterations = %d\n", iters);
     } else {
-        rc = psx_run_exhaustive(eng);
+        rc = g_multi ? psx_multi_run_exhaustive(multi) : psx_run_exhaustive(eng);
     }
     if (rc) die_engine(rc);
     auto t1 = std::chrono::steady_clock::now();
@@ -442,10 +494,14 @@ int main(int argc, char* argv[]) {
     acc.shared = shared.data();
     acc.shared_ll = sll.data();
     acc.notshared_ll = nsll.data();
-    if ((rc = psx_get_accum(eng, &acc))) die_engine(rc);
+    if ((rc = g_multi ? psx_multi_get_accum(multi, &acc) : psx_get_accum(eng, &acc))) die_engine(rc);
     psx_timing tm;
-    psx_get_timing(eng, &tm);
+    if (g_multi)
+        psx_multi_get_timing(multi, &tm);
+    else
+        psx_get_timing(eng, &tm);
     printf("num total configs = %llu\n", (unsigned long long)acc.n_configs);
+    if (g_multi) printf("devices = %d (one shard each, folded on device %d)\n", (int)devices.size(), device);
     printf("sweep device time = %.3f ms (kernel %.3f ms, merge %.3f ms)\n", tm.sweep_ms, tm.kernel_ms, tm.merge_ms);
     const double total = acc.total;
     {
@@ -496,7 +552,10 @@ int main(int argc, char* argv[]) {
             f << all_snp_pos[u] << "\t" << special_exp(shared[u], total) << "\t" << sll[u] << "\t" << nsll[u]
               << std::endl;
     }
-    psx_destroy(eng);
+    if (g_multi)
+        psx_multi_destroy(multi);
+    else
+        psx_destroy(eng);
     (void)rho;
     (void)cutoff_threshold;
     (void)num_causal_s;

@@ -37,6 +37,9 @@ EXPORTED = [
     "psx_psd_shift", "psx_lowrank_study", "psx_sym_eigen", "psx_lu_det",
     "psx_create_from_ld", "psx_psd_shift_gpu", "psx_lu_det_gpu",
     "psx_run_exhaustive_async", "psx_sync", "psx_run_sss_sharded",
+    "psx_multi_create", "psx_multi_create_from_ld", "psx_multi_run_exhaustive", "psx_multi_run_configs",
+    "psx_multi_run_sss", "psx_multi_get_accum", "psx_multi_get_timing", "psx_multi_count",
+    "psx_multi_last_error", "psx_multi_destroy",
 ]
 
 # psx_allgather_fn (include/pipsort_engine.h): int (*)(void *ctx, const void *send, void *recv, int64_t bytes)
@@ -174,6 +177,16 @@ def load_library(path: str = LIB_PATH):
         "psx_run_exhaustive_async": (c_int, [vp]),
         "psx_sync": (c_int, [vp, P(c_i32)]),
         "psx_run_sss_sharded": (c_int, [vp, ALLGATHER_FN, vp, P(c_i32)]),
+        "psx_multi_create": (c_int, [P(_Problem), P(c_i32), c_i32, P(vp)]),
+        "psx_multi_create_from_ld": (c_int, [P(_LdProblem), P(c_i32), c_i32, P(vp), P(SetupInfo)]),
+        "psx_multi_run_exhaustive": (c_int, [vp]),
+        "psx_multi_run_configs": (c_int, [vp, P(ctypes.c_int16), c_i64, c_i32]),
+        "psx_multi_run_sss": (c_int, [vp, P(c_i32)]),
+        "psx_multi_get_accum": (c_int, [vp, P(_Accum)]),
+        "psx_multi_get_timing": (c_int, [vp, P(Timing)]),
+        "psx_multi_count": (c_i32, [vp]),
+        "psx_multi_last_error": (ctypes.c_char_p, []),
+        "psx_multi_destroy": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("PSX_ENGINE_LIB") and not hasattr(lib, name):
@@ -435,6 +448,72 @@ class Accumulators:
             out[v == 0] = 0.0
             return out
         return se(self.post), se(self.no_causal), se(self.shared)
+
+
+class MultiPostCal:
+    """PostCal over several devices in one process (psx_multi_*): one shard per
+    entry of `devices` (entries may repeat), folded on devices[0]."""
+
+    def __init__(self, seam, devices):
+        self.lib = load_library()
+        self.seam = seam
+        dv = np.ascontiguousarray(devices, dtype=np.int32)
+        h = ctypes.c_void_p()
+        self.setup_info = None
+        if isinstance(seam, ModelInputs):
+            self._p = seam._ld_struct()
+            info = SetupInfo()
+            self._chk(self.lib.psx_multi_create_from_ld(ctypes.byref(self._p), _ptr(dv, ctypes.c_int32), len(dv),
+                                                        ctypes.byref(h), ctypes.byref(info)))
+            self.setup_info = info.as_dict()
+        else:
+            self._p = seam._struct()
+            self._chk(self.lib.psx_multi_create(ctypes.byref(self._p), _ptr(dv, ctypes.c_int32), len(dv),
+                                                ctypes.byref(h)))
+        self.h = h
+
+    def _chk(self, rc):
+        if rc != PSX_OK:
+            raise EngineError(rc, self.lib.psx_multi_last_error().decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.psx_multi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run_exhaustive(self):
+        self._chk(self.lib.psx_multi_run_exhaustive(self.h))
+
+    def run_configs(self, rows):
+        r = np.ascontiguousarray(rows, dtype=np.int16)
+        self._chk(self.lib.psx_multi_run_configs(self.h, _ptr(r, ctypes.c_int16), r.shape[0], r.shape[1]))
+
+    def run_sss(self) -> int:
+        it = ctypes.c_int32(0)
+        self._chk(self.lib.psx_multi_run_sss(self.h, ctypes.byref(it)))
+        return it.value
+
+    def accum(self) -> "Accumulators":
+        N, U = self.seam.N, self.seam.n_union
+        post, noc = np.zeros(N), np.zeros(2)
+        sh, sll, nsll = np.zeros(U), np.zeros(U), np.zeros(U)
+        a = _Accum()
+        a.post, a.no_causal = _ptr(post, ctypes.c_double), _ptr(noc, ctypes.c_double)
+        a.shared, a.shared_ll = _ptr(sh, ctypes.c_double), _ptr(sll, ctypes.c_double)
+        a.notshared_ll = _ptr(nsll, ctypes.c_double)
+        self._chk(self.lib.psx_multi_get_accum(self.h, ctypes.byref(a)))
+        return Accumulators(post, noc, sh, sll, nsll, a.total, int(a.n_configs))
+
+    def timing(self) -> dict:
+        t = Timing()
+        self._chk(self.lib.psx_multi_get_timing(self.h, ctypes.byref(t)))
+        return t.as_dict()
 
 
 class PostCal:

@@ -1,0 +1,101 @@
+"""Several devices in one process (psx_multi_*, the drop-in CLI's PSX_DEVICES):
+one shard per device entry, folded on the first device.  A test box has one
+GPU, so the entries repeat device 0 — the same code path as a node, with the
+peer copies replaced by same-device copies."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import loci
+from oracle import oracle as O
+from pipsort_amd import engine as E
+from pipsort_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(a, b, pip_tol=1e-12, ll_rtol=1e-12):
+    assert a.n_configs == b.n_configs
+    pa, na, sa = a.pips()
+    pb, nb, sb = b.pips()
+    assert max(np.abs(pa - pb).max(), np.abs(na - nb).max(), np.abs(sa - sb).max()) <= pip_tol
+    for f in ("shared_ll", "notshared_ll"):
+        np.testing.assert_allclose(getattr(a, f), getattr(b, f), rtol=ll_rtol, atol=0, err_msg=f)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_multi_handle_matches_single(gpu, n):
+    """Exhaustive (fused k = 3 pass), configs file and the sharded SSS walk over
+    n shards in one process equal one handle; the exhaustive result is also at
+    oracle parity."""
+    ld, z, _, _, u2l = synth.mixed_locus(70, 60, 40, seed=5)
+    seam = E.seam_from_arrays(ld, z, u2l, (5000, 9000), max_causal=3, sharing_param=0.5)
+    one = E.PostCal(seam)
+    many = E.MultiPostCal(seam, [0] * n)
+    one.run_exhaustive()
+    many.run_exhaustive()
+    _same(many.accum(), one.accum())
+    ref = O.postcal(seam)
+    got = many.accum()
+    assert got.n_configs == ref["n_configs"]
+    assert np.abs(got.pips()[0] - np.where(ref["post"] == 0, 0, np.exp(ref["post"] - ref["total"]))).max() <= 1e-9
+    assert many.timing()["configs"] == got.n_configs
+    rows = synth.all_configs_rows(seam.union_to_local, seam.m, 2)
+    one.run_configs(rows)
+    many.run_configs(rows)
+    _same(many.accum(), one.accum())
+    it1, itn = one.run_sss(), many.run_sss()
+    assert it1 == itn
+    _same(many.accum(), one.accum())
+    one.close()
+    many.close()
+
+
+def test_multi_handle_gpu_setup(gpu):
+    """psx_multi_create_from_ld: every device runs the Model setup (PSD shift
+    LU, SYN-v1 M = 300), then the sharded sweep."""
+    ld, z, _, _, u2l = synth.syn_v1(300)
+    mi = E.model_inputs(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    one = E.PostCal(mi)
+    many = E.MultiPostCal(mi, [0, 0])
+    assert many.setup_info["psd_added"] == one.setup_info["psd_added"]
+    one.run_exhaustive()
+    many.run_exhaustive()
+    _same(many.accum(), one.accum())
+
+
+FILES = ("study0_post", "study1_post", "study0_set", "study1_set", "nocausal", "shared_pips")
+
+
+def _cli(tmp_path, src, args, devices):
+    d = tmp_path / f"{src}_{devices.replace(',', '_')}"
+    shutil.copytree(os.path.join(loci.GOLDEN, src), d)
+    env = dict(os.environ, PSX_DEVICES=devices)
+    r = subprocess.run([E.PIPSORT_BIN] + args, cwd=d, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return d, r.stdout
+
+
+@pytest.mark.parametrize("src,args", [
+    ("example", ["-c", "2", "-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "snp_map", "-n", "334324,6771",
+                 "-p", "0.25", "-o", "out"]),
+    ("small_example", ["-q", "1", "-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "eur_afr_small_test_snp_map",
+                       "-n", "7000,7000", "-o", "out"]),
+    ("test_optional_configs", ["-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "eur_afr_small_test_snp_map",
+                               "-n", "7000,7000", "-b", "all_configs_int16", "-d", "72", "-e", "5", "-o", "out"]),
+])
+def test_cli_two_devices_byte_identical(gpu, tmp_path, src, args):
+    """The drop-in CLI driving two devices in one process (PSX_DEVICES=0,0)
+    writes the same files, byte for byte, as one device; on tests/example those
+    are the reference's expected files."""
+    d1, _ = _cli(tmp_path, src, args, "0")
+    d2, out2 = _cli(tmp_path, src, args, "0,0")
+    assert "devices = 2" in out2
+    for f in FILES:
+        assert open(d2 / f"out_{f}.txt").read() == open(d1 / f"out_{f}.txt").read(), f
+    if src == "example":
+        for f in ("study0_post", "study1_post", "study0_set", "study1_set", "nocausal"):
+            assert open(d2 / f"out_{f}.txt").read() == open(d2 / f"expected_{f}.txt").read(), f
