@@ -8,6 +8,12 @@
 #ifndef PSX_K3_WAVES
 #define PSX_K3_WAVES 2
 #endif
+// dispatch rounds of the k = 3 sweep's wave slots per shard the a-chunk is
+// sized for (a build-time A/B knob, tools/build_variant.sh; the product build
+// uses the default)
+#ifndef PSX_K3_ROUNDS
+#define PSX_K3_ROUNDS 3.5
+#endif
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -331,7 +331,7 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
             if (hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0)
                 cus = pr.multiProcessorCount;
         }
-        return 3.5 * (4.0 * PSX_K3_WAVES * cus);
+        return PSX_K3_ROUNDS * (4.0 * PSX_K3_WAVES * cus);
     }();
     ca = (int)std::lround(total_a / (kTarget * world));
     ca = std::min(ca, 4);

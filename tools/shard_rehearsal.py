@@ -68,7 +68,8 @@ def main():
         worst = max(r["step_ms"] for r in ranks)
         out["worlds"][world] = {"max_step_ms": worst, "ranks": ranks}
         print(f"world {world}: max step {worst:.3f} ms; kernel ms per rank "
-              f"{[round(r['kernel_ms'], 3) for r in ranks]}; sweep ms {[round(r['sweep_ms'], 3) for r in ranks]}",
+              f"{[round(r['kernel_ms'], 3) for r in ranks]}; step ms per rank "
+              f"{[round(r['step_ms'], 3) for r in ranks]}; sweep ms {[round(r['sweep_ms'], 3) for r in ranks]}",
               flush=True)
     base = out["worlds"].get(1, {}).get("max_step_ms")
     if base:
