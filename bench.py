@@ -253,9 +253,57 @@ def sss_probe(reps=20):
     return {"workload": "SYN-v1 2-study locus, M=2000 SNPs, -c 5 -p 0.25 -n 10000,8000 (BASELINE configs[4])",
             "gpu_model_setup_and_create_ms": setup_ms, "walk_iterations": iters, "walk_configs": walk_configs,
             "walk_ms": walk_ms, "batch_sets": len(sets), "batch_configs": npat, "batch_ms": batch_ms,
-            "batch_configs_per_s": npat / (batch_ms / 1e3),
+            "batch_configs_per_s": npat / (batch_ms / 1e3), "long_walks": sss_long_walks(),
             "multi_gpu": "sharded under --gpus N (psx_run_sss_sharded: every iteration's batch split over the "
                          "ranks, one all-gather of scores per iteration); this N = 1 line times one GPU"}
+
+
+def sss_long_walks(reps=3):
+    """The seeded walk at configs[4] stops after 2 iterations, so the host side
+    of the walk (neighbourhoods, set map, sampling, one GPU round trip per
+    iteration) is timed on SYN-v1 loci whose walks run long: M = 100 (22
+    iterations, climbing to 5-SNP sets) and M = 200 (100 iterations, the
+    convergence stop of sss_postcal.cpp:265-270), -c 5.  The M = 100 walk is
+    also timed through the oracle's restated walk on one host core (the
+    cpu_baseline leg's port; M = 200 takes it ~70 s)."""
+    from oracle import oracle as O
+    out = []
+    for M in (100, 200):
+        ld, z, _, _, u2l = synth.syn_v1(M)
+        mi = E.model_inputs(ld, z, u2l, (10000, 8000), max_causal=5, sharing_param=0.25)
+        pc = E.PostCal(mi)
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            it = pc.run_sss()
+            dt = (time.perf_counter() - t0) * 1e3
+            if best is None or dt < best[0]:
+                best = (dt, it, pc.timing()["kernel_ms"])
+        n = pc.accum().n_configs
+        pc.close()
+        dt, it, kms = best
+        row = {"locus": f"SYN-v1 M={M} -c 5", "iterations": it, "configs": n, "walk_ms": dt,
+               "kernel_ms": kms, "ms_per_iteration": dt / max(it, 1), "configs_per_s": n / (dt / 1e3)}
+        if M == 100:
+            seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=5, sharing_param=0.25)
+            # the restated walk prints the reference's stop message on stdout,
+            # which carries only the bench line: send fd 1 to stderr meanwhile
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                t0 = time.perf_counter()
+                ref = O.postcal(seam, "sss")
+                row["cpu_port_walk_ms"] = (time.perf_counter() - t0) * 1e3
+            finally:
+                import ctypes
+                ctypes.CDLL(None).fflush(None)  # C stdio's buffered copy of the message
+                os.dup2(saved, 1)
+                os.close(saved)
+            row["cpu_port_cores"] = 1
+            row["cpu_port_configs_match"] = int(ref["n_configs"]) == int(n)
+        out.append(row)
+    return out
 
 
 def configs_probe(reps=3):

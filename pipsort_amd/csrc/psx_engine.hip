@@ -16,7 +16,6 @@
 #include <random>
 #include <string>
 #include <tuple>
-#include <unordered_map>
 #include <vector>
 #include <thread>
 
@@ -670,8 +669,21 @@ void build_csr(const std::vector<int>& sets, int stride, size_t nsets, int U, st
 // k_eval_sets over n sets staged in e->hstage as [sets (n * stride) | forced
 // (n * 2, optional) | CSR ptr | idx | rows (accumulate)]: one upload, the
 // kernel, the deterministic record merges.
+// Wait for an eval_generic_staged(..., finish = false) batch: scores out, kernel time.
+int finish_generic(psx_engine* e, size_t nsets, double* scores, double* kernel_ms) {
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (scores)
+        for (size_t i = 0; i < nsets; i++) scores[i] = e->K + e->hscore[i];
+    if (kernel_ms) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+        *kernel_ms += ms;
+    }
+    return 0;
+}
+
 int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool has_forced, size_t n_ptr, size_t n_idx,
-                        size_t n_rows, bool accumulate, double* scores, double* kernel_ms) {
+                        size_t n_rows, bool accumulate, double* scores, double* kernel_ms, bool finish = true) {
     int rc;
     const size_t n_sets = nsets * stride, n_forced = has_forced ? nsets * 2 : 0;
     const size_t total = n_sets + n_forced + n_ptr + n_idx + n_rows;
@@ -702,16 +714,9 @@ int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool has_forced
     if (scores) {
         if ((rc = ensure_host(e->hscore, e->cap_hscore, nsets))) return rc;
         HIPCHK(hipMemcpyAsync(e->hscore, e->dscore, nsets * sizeof(double), hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(hipStreamSynchronize(e->stream));
-        for (size_t i = 0; i < nsets; i++) scores[i] = e->K + e->hscore[i];
     }
-    if (kernel_ms) {
-        HIPCHK(hipStreamSynchronize(e->stream));
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
-        *kernel_ms += ms;
-    }
-    return 0;
+    if (!finish || (!scores && !kernel_ms)) return 0;
+    return finish_generic(e, nsets, scores, kernel_ms);
 }
 
 int eval_generic(psx_engine* e, const std::vector<int>& sets, int stride, size_t nsets, const int* forced,
@@ -1751,18 +1756,131 @@ int psx_run_configs(psx_engine* e, const int16_t* rows, int64_t n_rows, int32_t 
 
 // sss_postcal.cpp:102-380.  The random walk, neighbourhoods, hash map and
 // sampling run on the host exactly as the reference orders them; every
-// iteration's unseen neighbours are one GPU batch.
+// iteration's unseen neighbours are one GPU batch.  The host side is kept
+// allocation-free per neighbour: neighbourhoods are flat rows, and the
+// reference's unordered_map<vector<int>, double> (postcal.h:43-56) is an
+// open-addressing table keyed by the packed sorted set.
 namespace {
-struct VecHash {  // postcal.h:43-56
-    size_t operator()(const std::vector<int>& v) const noexcept {
-        size_t seed = 0xCBF29CE484222325ULL;
-        for (int x : v) seed ^= (size_t)x + 0x9e3779b97f4a7c15ULL + (seed << 6) + (seed >> 2);
-        return seed;
-    }
+// A sorted union set of <= 6 SNPs as two words of three 21-bit fields
+// (index + 1; 0 = no member).  The empty set packs to {0, 0}.
+struct SetKey {
+    uint64_t lo, hi;
+    bool operator==(const SetKey& o) const { return lo == o.lo && hi == o.hi; }
 };
-}  // namespace
+constexpr int kKeyBits = 21;
+constexpr int kKeyMaxU = (1 << kKeyBits) - 2;
 
-namespace {
+inline SetKey pack_set(const int* v, int k) {
+    uint64_t w[2] = {0, 0};
+    for (int j = 0; j < k; j++) w[j / 3] |= (uint64_t)(v[j] + 1) << (kKeyBits * (j % 3));
+    return {w[0], w[1]};
+}
+
+// SetKey -> score with linear probing at load <= 1/2; the empty set lives in
+// a side slot so {0, 0} can mark unused table slots.  Lookup and insert only,
+// which is all the walk asks of its map.
+class SetMap {
+  public:
+    SetMap() { rehash(1 << 16); }
+    bool find(const SetKey& k, double& v) const {
+        if (k.lo == 0 && k.hi == 0) {
+            v = empty_v_;
+            return has_empty_;
+        }
+        for (size_t i = slot(k);; i = (i + 1) & mask_) {
+            if (keys_[i] == k) {
+                v = vals_[i];
+                return true;
+            }
+            if (keys_[i].lo == 0 && keys_[i].hi == 0) return false;
+        }
+    }
+    void assign(const SetKey& k, double v) {  // hm[k] = v
+        if (k.lo == 0 && k.hi == 0) {
+            has_empty_ = true;
+            empty_v_ = v;
+            return;
+        }
+        if (2 * (n_ + 1) > keys_.size()) rehash(2 * keys_.size());
+        size_t i = slot(k);
+        for (; !(keys_[i].lo == 0 && keys_[i].hi == 0); i = (i + 1) & mask_)
+            if (keys_[i] == k) {
+                vals_[i] = v;
+                return;
+            }
+        keys_[i] = k;
+        vals_[i] = v;
+        n_++;
+    }
+
+  private:
+    static uint64_t mix(uint64_t x) {
+        x ^= x >> 30;
+        x *= 0xbf58476d1ce4e5b9ULL;
+        x ^= x >> 27;
+        x *= 0x94d049bb133111ebULL;
+        return x ^ (x >> 31);
+    }
+    size_t slot(const SetKey& k) const { return mix(k.lo ^ mix(k.hi + 0x9e3779b97f4a7c15ULL)) & mask_; }
+    void rehash(size_t cap) {
+        std::vector<SetKey> ok(cap, SetKey{0, 0});
+        std::vector<double> ov(cap, 0.0);
+        ok.swap(keys_);
+        ov.swap(vals_);
+        mask_ = cap - 1;
+        for (size_t i = 0; i < ok.size(); i++)
+            if (!(ok[i].lo == 0 && ok[i].hi == 0)) {
+                size_t j = slot(ok[i]);
+                while (!(keys_[j].lo == 0 && keys_[j].hi == 0)) j = (j + 1) & mask_;
+                keys_[j] = ok[i];
+                vals_[j] = ov[i];
+            }
+    }
+    std::vector<SetKey> keys_;
+    std::vector<double> vals_;
+    size_t n_ = 0, mask_ = 0;
+    bool has_empty_ = false;
+    double empty_v_ = 0;
+};
+
+// Stage `n` union sets (rows of `stride`, -1 padded, `sz` members each) and
+// the member CSR (union SNP -> record, in record order) into e->hstage in the
+// eval_generic_staged layout; returns the CSR part sizes.
+int stage_sets(psx_engine* e, const int* const* rows, const int* sz, size_t n, int stride, std::vector<int>& cnt,
+               size_t& n_ptr, size_t& n_idx, size_t& n_rows) {
+    int rc;
+    std::fill(cnt.begin(), cnt.end(), 0);
+    n_idx = 0;
+    for (size_t i = 0; i < n; i++)
+        for (int j = 0; j < sz[i]; j++) cnt[rows[i][j]]++;
+    n_rows = 0;
+    for (int u = 0; u < e->U; u++) n_rows += cnt[u] != 0;
+    for (size_t i = 0; i < n; i++) n_idx += sz[i];
+    n_ptr = n_rows + 1;
+    if (e->stage_rec) HIPCHK(hipEventSynchronize(e->stage_ev));
+    if ((rc = ensure_host(e->hstage, e->cap_stage, n * stride + n_ptr + n_idx + n_rows))) return rc;
+    int* hs = e->hstage;
+    int* hptr = hs + n * stride;
+    int* hidx = hptr + n_ptr;
+    int* hrow = hidx + n_idx;
+    int acc = 0, r = 0;
+    hptr[0] = 0;
+    for (int u = 0; u < e->U; u++)
+        if (cnt[u]) {
+            hrow[r++] = u;
+            const int c = cnt[u];
+            cnt[u] = acc;  // now the fill position of u
+            acc += c;
+            hptr[r] = acc;
+        }
+    for (size_t i = 0; i < n; i++) {
+        int* S = hs + i * stride;
+        for (int j = 0; j < stride; j++) S[j] = j < sz[i] ? rows[i][j] : -1;
+        for (int j = 0; j < sz[i]; j++) hidx[cnt[rows[i][j]]++] = (int)(i * stride + j);
+    }
+    return 0;
+}
+
 static int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* iterations_out) {
     HIPCHK(hipSetDevice(e->dev));
     const int rank = allgather ? e->rank : 0, world = allgather ? e->world : 1;
@@ -1771,104 +1889,124 @@ static int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t
     std::memset(&e->timing, 0, sizeof(e->timing));
     const int U = e->U, C = e->maxc;
     if (C > PSX_KMAX) return fail(PSX_ERANGE, "SSS max_causal > 6");
-    std::unordered_map<std::vector<int>, double, VecHash> hm;
+    if (U > kKeyMaxU) return fail(PSX_ERANGE, "SSS: more union SNPs than the set key holds");
+    SetMap hm;
     std::mt19937 gen(12345);
-    std::vector<int> cur;
+    int cur[PSX_KMAX], k = 0;  // the current configuration, ascending
     double old_sum = 0;
     int iter;
     const int stride = std::max(C, 1);
     double kms = 0;
     auto t0 = std::chrono::steady_clock::now();
-    auto sss_total = [&](double& out) -> int {
-        SetRec s;
-        HIPCHK(hipMemcpy(&s, e->dsacc, sizeof(SetRec), hipMemcpyDeviceToHost));
-        out = logval(e, s.m, s.tot);
-        return 0;
-    };
     std::vector<char> in_cur(U, 0);
+    std::vector<int> nb, cnt(U, 0), not_done, bsz;
+    std::vector<const int*> brow;
+    std::vector<int> bpos;
+    std::vector<double> lk, s2, pr;
     for (iter = 0; iter < 1000; iter++) {
-        // sss_postcal.cpp:166-186 nbd = zero ++ minus ++ plus
-        std::vector<std::vector<int>> nbd;
-        int k = (int)cur.size();
+        // sss_postcal.cpp:166-186 nbd = zero ++ minus ++ plus, as rows of
+        // `stride` (sizes k, k - 1 and k + 1 by group)
         std::fill(in_cur.begin(), in_cur.end(), 0);
-        for (int v : cur) in_cur[v] = 1;
-        std::vector<std::vector<int>> minus;
-        for (int i = 0; i < k; i++) {
-            std::vector<int> nc;
-            for (int j = 0; j < k; j++) if (i != j) nc.push_back(cur[j]);
-            minus.push_back(nc);
-        }
+        for (int j = 0; j < k; j++) in_cur[cur[j]] = 1;
+        int minus[PSX_KMAX][PSX_KMAX];
+        for (int i = 0; i < k; i++)
+            for (int j = 0, m = 0; j < k; j++)
+                if (i != j) minus[i][m++] = cur[j];
+        const int num_zero = (U - k) * k, num_minus = k, num_plus = k < C ? U - k : 0;
+        const int n_nbd = num_zero + num_minus + num_plus;
+        nb.resize((size_t)n_nbd * stride);
+        auto put = [&](int* row, const int* v, int kv, int x) {  // sorted {x} ∪ v
+            int j = 0;
+            for (; j < kv && v[j] < x; j++) row[j] = v[j];
+            row[j] = x;
+            for (; j < kv; j++) row[j + 1] = v[j];
+        };
+        int* w = nb.data();
         for (int i = 0; i < U; i++)
             if (!in_cur[i])
-                for (const auto& v : minus) {
-                    std::vector<int> nc;
-                    nc.reserve(k);
-                    nc.push_back(i);
-                    nc.insert(nc.end(), v.begin(), v.end());
-                    std::sort(nc.begin(), nc.end());
-                    nbd.push_back(std::move(nc));
-                }
-        int num_zero = (int)nbd.size();
-        for (auto& v : minus) nbd.push_back(v);
-        int num_minus = k;
-        if (k < C)
+                for (int v = 0; v < k; v++, w += stride) put(w, minus[v], k - 1, i);
+        for (int v = 0; v < k; v++, w += stride)
+            for (int j = 0; j < k - 1; j++) w[j] = minus[v][j];
+        if (num_plus)
             for (int i = 0; i < U; i++)
                 if (!in_cur[i]) {
-                    std::vector<int> nc{i};
-                    nc.insert(nc.end(), cur.begin(), cur.end());
-                    std::sort(nc.begin(), nc.end());
-                    nbd.push_back(std::move(nc));
+                    put(w, cur, k, i);
+                    w += stride;
                 }
-        int num_plus = (int)nbd.size() - num_zero - num_minus;
-        // current configuration (sss_postcal.cpp:195-202): updates only if unseen
-        std::vector<std::vector<int>> batch;
-        std::vector<int> batch_pos;  // -1 == cur
-        if (hm.find(cur) == hm.end()) { batch.push_back(cur); batch_pos.push_back(-1); }
-        std::vector<double> lk(nbd.size(), 0.0);
-        std::vector<int> not_done;
-        for (size_t i = 0; i < nbd.size(); i++) {
-            auto it = hm.find(nbd[i]);
-            if (it != hm.end()) lk[i] = it->second;
-            else { not_done.push_back((int)i); batch.push_back(nbd[i]); batch_pos.push_back((int)i); }
+        auto row_size = [&](int i) { return i < num_zero ? k : i < num_zero + num_minus ? k - 1 : k + 1; };
+        // current configuration (sss_postcal.cpp:195-202): evaluated only if unseen
+        brow.clear();
+        bsz.clear();
+        bpos.clear();
+        double v;
+        if (!hm.find(pack_set(cur, k), v)) {
+            brow.push_back(cur);
+            bsz.push_back(k);
+            bpos.push_back(-1);
         }
-        // evaluate the batch on the GPU (null sets folded host side)
-        std::vector<int> flat;
-        flat.reserve(batch.size() * stride);
-        for (auto& v : batch) for (int j = 0; j < stride; j++) flat.push_back(j < (int)v.size() ? v[j] : -1);
-        std::vector<double> sc(batch.size());
-        double gsum = 0.0;  // the running normaliser over all ranks (world > 1)
-        {
-            std::vector<int> vv;
-            std::vector<size_t> wh;
-            double nulls = 0;
-            for (size_t i = 0; i < batch.size(); i++) {
-                if (batch[i].empty()) { nulls += 1; sc[i] = e->K + e->L0; continue; }
-                wh.push_back(i);
-                vv.insert(vv.end(), flat.begin() + i * stride, flat.begin() + (i + 1) * stride);
+        lk.assign(n_nbd, 0.0);
+        not_done.clear();
+        for (int i = 0; i < n_nbd; i++) {
+            const int* r = nb.data() + (size_t)i * stride;
+            if (hm.find(pack_set(r, row_size(i)), v)) lk[i] = v;
+            else {
+                not_done.push_back(i);
+                brow.push_back(r);
+                bsz.push_back(row_size(i));
+                bpos.push_back(i);
             }
-            // this rank's contiguous slice of the batch (all of it at world 1)
-            const size_t nw = wh.size();
+        }
+        // evaluate the batch on the GPU (null sets folded host side); the
+        // non-null sets keep batch order, nulls score K + L0
+        const size_t nb_all = brow.size();
+        double gsum = 0.0;  // the running normaliser over all ranks (world > 1)
+        double nulls = 0;
+        SetRec st;  // this rank's accumulated normaliser after the batch
+        size_t nw = 0;
+        for (size_t i = 0; i < nb_all; i++) {
+            if (bsz[i] == 0) { nulls += 1; continue; }
+            brow[nw] = brow[i];
+            bsz[nw] = bsz[i];
+            bpos[nw] = bpos[i];
+            nw++;
+        }
+        {
+            // this rank's contiguous slice of the non-null sets (all of it at world 1)
             const size_t lo = nw * rank / world, hi = nw * (rank + 1) / world;
-            std::vector<double> s2(nw);
-            std::vector<int> mine(vv.begin() + lo * stride, vv.begin() + hi * stride);
-            if ((rc = eval_generic(e, mine, stride, hi - lo, nullptr, true, s2.data() + lo, &kms))) return rc;
+            s2.assign(nw, 0.0);
+            if (hi > lo) {
+                size_t n_ptr, n_idx, n_rows;
+                if ((rc = stage_sets(e, brow.data() + lo, bsz.data() + lo, hi - lo, stride, cnt, n_ptr, n_idx,
+                                     n_rows)))
+                    return rc;
+                if ((rc = eval_generic_staged(e, stride, hi - lo, false, n_ptr, n_idx, n_rows, true, s2.data() + lo,
+                                              &kms, false)))
+                    return rc;
+            }
             if (nulls > 0 && rank == 0 && (rc = fold_null(e, nulls))) return rc;
+            // the normaliser rides back with the scores: one synchronisation
+            HIPCHK(hipMemcpyAsync(e->hstat, e->dsacc, sizeof(SetRec), hipMemcpyDeviceToHost, e->stream));
+            if (hi > lo) {
+                if ((rc = finish_generic(e, hi - lo, s2.data() + lo, &kms))) return rc;
+            } else {
+                HIPCHK(hipStreamSynchronize(e->stream));
+            }
+            std::memcpy(&st, e->hstat, sizeof(SetRec));
             if (world > 1) {
                 // one all-gather: [slice length, normaliser (m, s), slice scores]
-                const size_t per = (nw + world - 1) / world, w = 3 + per;
-                std::vector<double> snd(w, 0.0), rcv(w * world, 0.0);
-                SetRec t;
-                HIPCHK(hipMemcpy(&t, e->dsacc, sizeof(SetRec), hipMemcpyDeviceToHost));
+                const size_t per = (nw + world - 1) / world, wd = 3 + per;
+                std::vector<double> snd(wd, 0.0), rcv(wd * world, 0.0);
+                const SetRec& t = st;
                 snd[0] = (double)(hi - lo);
                 snd[1] = (double)t.m;
                 snd[2] = t.tot;
                 std::copy(s2.begin() + lo, s2.begin() + hi, snd.begin() + 3);
-                if (allgather(ctx, snd.data(), rcv.data(), (int64_t)(w * sizeof(double))))
+                if (allgather(ctx, snd.data(), rcv.data(), (int64_t)(wd * sizeof(double))))
                     return fail(PSX_EEXCHANGE, "SSS all-gather callback failed");
                 double mx = -INFINITY;
                 std::vector<double> part(world, 0.0);
                 for (int r = 0; r < world; r++) {
-                    const double* q = rcv.data() + (size_t)r * w;
+                    const double* q = rcv.data() + (size_t)r * wd;
                     const size_t rlo = nw * r / world, rn = nw * (r + 1) / world - rlo;
                     if ((size_t)q[0] != rn) return fail(PSX_EEXCHANGE, "SSS all-gather: ranks disagree on the batch");
                     std::copy(q + 3, q + 3 + rn, s2.begin() + rlo);
@@ -1880,19 +2018,20 @@ static int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t
                     if (part[r] != 0.0) acc += std::exp(part[r] - mx);
                 gsum = acc > 0 ? mx + std::log(acc) : 0.0;
             }
-            for (size_t i = 0; i < nw; i++) sc[wh[i]] = s2[i];
         }
-        for (size_t i = 0; i < batch.size(); i++)
-            if (batch_pos[i] >= 0) lk[batch_pos[i]] = sc[i];
-        double sss_sum = gsum;
-        if (world == 1 && (rc = sss_total(sss_sum))) return rc;
+        for (size_t i = 0; i < nw; i++)
+            if (bpos[i] >= 0) lk[bpos[i]] = s2[i];
+        if (nulls > 0)  // a null neighbour (the empty minus set at k = 1)
+            for (int i : not_done)
+                if (row_size(i) == 0) lk[i] = e->K + e->L0;
+        const double sss_sum = world == 1 ? logval(e, st.m, st.tot) : gsum;
         if (not_done.empty()) break;                                                       // :260-263
         if (iter >= 100 && (1 - std::exp(old_sum - sss_sum)) <= 0.001) break;             // :265-270
-        for (int i : not_done) hm[nbd[i]] = lk[i];                                         // :280-284
+        for (int i : not_done) hm.assign(pack_set(nb.data() + (size_t)i * stride, row_size(i)), lk[i]);  // :280-284
         double wz = 0, wm = 0, wp = 0;
-        size_t zs = nbd.size(), ms = nbd.size(), ps = nbd.size();
+        size_t zs = n_nbd, ms = n_nbd, ps = n_nbd;
         auto group = [&](int b, int en, double& wsum, size_t& smp) {
-            std::vector<double> pr;
+            pr.clear();
             double mx = *std::max_element(lk.begin() + b, lk.begin() + en);
             for (int ii = b; ii < en; ii++) pr.push_back(std::exp(lk[ii] - mx));
             std::discrete_distribution<size_t> dist(pr.begin(), pr.end());
@@ -1901,7 +2040,7 @@ static int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t
         };
         if (num_zero != 0) group(0, num_zero, wz, zs);                                     // :296-306
         if (num_minus != 0) group(num_zero, num_zero + num_minus, wm, ms);                 // :307-317
-        if (num_plus != 0) group(num_zero + num_minus, (int)lk.size(), wp, ps);            // :318-328
+        if (num_plus != 0) group(num_zero + num_minus, n_nbd, wp, ps);                     // :318-328
         std::discrete_distribution<size_t> dist({wz, wm, wp});                             // :330-343
         size_t idx = dist(gen), fin = 0;
         switch (idx) {
@@ -1909,7 +2048,9 @@ static int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t
             case 1: fin = ms + num_zero; break;
             case 2: fin = ps + num_zero + num_minus; break;
         }
-        cur = nbd[fin];
+        const int nk = row_size((int)fin);
+        std::copy(nb.begin() + fin * stride, nb.begin() + fin * stride + nk, cur);
+        k = nk;
         old_sum = sss_sum;
     }
     auto t1 = std::chrono::steady_clock::now();

@@ -179,6 +179,21 @@ def test_sss_synthetic_c5(gpu):
     assert_parity(pc.accum(), O.postcal(seam, "sss"), ll_rtol=1e-11)
 
 
+def test_sss_long_walk_m100_c5(gpu):
+    """A walk that climbs to 5-SNP configurations and runs for many iterations
+    (SYN-v1 M = 100, -c 5: 1.15M configurations), so the set map, the
+    neighbourhood rows and the sampling see every group size; the oracle walk
+    takes the same mt19937(12345) draws."""
+    ld, z, _, _, u2l = synth.syn_v1(100)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=5, sharing_param=0.25)
+    pc = E.PostCal(seam)
+    it = pc.run_sss()
+    ref = O.postcal(seam, "sss")
+    assert it >= 20
+    assert_parity(pc.accum(), ref, pip_tol=1e-9, ll_rtol=1e-9)
+    pc.close()
+
+
 def test_union_batch_scores(gpu):
     """expand_and_compute_lkl scores (max |L| pattern) for ragged sets incl. the null set."""
     seam, _ = loci.seam_for(loci.SMALL, c=3)
