@@ -790,7 +790,37 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         // this a's reference G: the a accumulator sits at it; c / noCausal / the b
         // slots move their shift up to it (values scale down exactly) once per a
         const int G = R[0] + R[1];
-        double aW0 = 0.0, aW1 = 0.0, aW2 = 0.0, aSl = 0.0, aNs = 0.0;
+        // Deferred fold.  Over subsets A of {a, c} (bit 0 a, bit 1 c) let c_s[A] =
+        // E_s[A] (fixed for this a: Ep) and v_s[A] = E_s[A + b] (new every step).
+        // An assignment puts b in study 0 only (weight v_0[A0] c_1[A1]), study 1 only
+        // (c_0[A0] v_1[A1]) or both (v_0[A0] v_1[A1]).  Members a and c sit at a
+        // fixed shift for the whole b-walk, so their marginals need only the sums
+        // V_s = sum_j v_s and ZS[xa][xc] = sum_j v_0[A0] v_1[A1] (one per assignment
+        // of the pair), folded once after the walk.  The rotating b slot takes its
+        // marginals per step: b in one study are dot products with the fixed
+        // vectors uW_s = (m (x) m) c_s (m = [[0, 1], [1, rho]], prior-weighted) and
+        // uL_s = (m1 (x) m1) c_s (m1 = [[0, 1], [1, 1]]); b in both from the 9 products.
+        double uW[2][4], uL[2][4];
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const double* c = Ep[s];
+            uW[s][0] = c[3];
+            uW[s][1] = fma(rho, c[3], c[2]);
+            uW[s][2] = fma(rho, c[3], c[1]);
+            uW[s][3] = fma(rho, fma(rho, c[3], c[1] + c[2]), c[0]);
+            uL[s][0] = c[3];
+            uL[s][1] = c[2] + c[3];
+            uL[s][2] = c[1] + c[3];
+            uL[s][3] = (c[0] + c[1]) + uL[s][1];
+        }
+        double ZS[3][3], V0[4], V1[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) V0[i] = V1[i] = 0.0;
+#pragma unroll
+        for (int xa = 0; xa < 3; xa++)
+#pragma unroll
+            for (int xc = 0; xc < 3; xc++) ZS[xa][xc] = 0.0;
+        int nact = 0;  // masked steps this lane took part in
         {
             const int M = max(mC, G), d = mC - M;
             cW0 = ldexp(cW0, d); cW1 = ldexp(cW1, d); cW2 = ldexp(cW2, d); cSl = ldexp(cSl, d); cNs = ldexp(cNs, d);
@@ -849,8 +879,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             const int bs = (t + j) & 63;
             const int sm_ = sM[bs];
             const double o0 = sW0[bs], o1 = sW1[bs], o2 = sW2[bs], oS = sSl[bs], oN = sNs[bs];
-            // P[s][m] = E_s[m], Q[s][m] = E_s[m | c], m over {a, b}; relative to 2^{R_s}
-            double P[2][4], Q[2][4];
+            // v[s][A] = E_s[A + b] relative to 2^{R_s}: {b}, {a, b}, {b, c}, {a, b, c}
+            double v[2][4];
             int d3s = 0;
 #pragma unroll
             for (int s = 0; s < 2; s++) {
@@ -860,91 +890,47 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 const double mu2 = s ? mcur.y : mcur.x;
                 const int dab = abN[s][bs] - R[s];
                 d3s += d3;
-                P[s][0] = Ep[s][0];
-                P[s][1] = Ep[s][1];
-                P[s][2] = ldexp(abMuB[s][bs], dab);
-                P[s][3] = ldexp(abMu[s][bs], dab);
-                Q[s][0] = Ep[s][2];
-                Q[s][1] = Ep[s][3];
-                Q[s][2] = ldexp(mu2, n2 - R[s]);
-                Q[s][3] = ldexp(mu3, d3);
+                v[s][0] = ldexp(abMuB[s][bs], dab);
+                v[s][1] = ldexp(abMu[s][bs], dab);
+                v[s][2] = ldexp(mu2, n2 - R[s]);
+                v[s][3] = ldexp(mu3, d3);
             }
             dmax = max(dmax, d3s);
-            // ---- member c: bilinear forms over the (a, b) assignments ----
-            double MrP[4], MrQ[4], M1P[4], M1Q[4];
-            MrP[0] = P[1][3];
-            MrP[1] = fma(rho, P[1][3], P[1][2]);
-            MrP[2] = fma(rho, P[1][3], P[1][1]);
-            MrP[3] = fma(rho, MrP[1], fma(rho, P[1][1], P[1][0]));
-            MrQ[0] = Q[1][3];
-            MrQ[1] = fma(rho, Q[1][3], Q[1][2]);
-            MrQ[2] = fma(rho, Q[1][3], Q[1][1]);
-            MrQ[3] = fma(rho, MrQ[1], fma(rho, Q[1][1], Q[1][0]));
-            M1P[0] = P[1][3];
-            M1P[1] = P[1][2] + P[1][3];
-            M1P[2] = P[1][1] + P[1][3];
-            M1P[3] = (P[1][0] + P[1][1]) + M1P[1];
-            M1Q[0] = Q[1][3];
-            M1Q[1] = Q[1][2] + Q[1][3];
-            M1Q[2] = Q[1][1] + Q[1][3];
-            M1Q[3] = (Q[1][0] + Q[1][1]) + M1Q[1];
             auto dot4 = [](const double (&u)[4], const double (&x)[4], double acc0) {
                 return fma(u[3], x[3], fma(u[2], x[2], fma(u[1], x[1], fma(u[0], x[0], acc0))));
             };
-            const double WC0 = dot4(Q[0], MrP, 0.0);
-            const double WC1 = dot4(P[0], MrQ, 0.0);
-            const double WC2 = dot4(Q[0], MrQ, 0.0);
-            const double LC2 = dot4(Q[0], M1Q, 0.0);
-            const double NC = dot4(P[0], M1Q, dot4(Q[0], M1P, 0.0));
-            // ---- members a, b: the 9 (x_a, x_b) with c marginalised ----
-            double S1[4], T1[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                S1[q] = P[1][q] + Q[1][q];
-                T1[q] = fma(rho, Q[1][q], P[1][q]);
-            }
-            double Pl[3][3], Pw[3][3];
+            // ---- member b (this step's slot): b in study 0 only / study 1 only ----
+            const double WB0 = dot4(v[0], uW[1], 0.0);
+            const double WB1 = dot4(v[1], uW[0], 0.0);
+            const double NB = dot4(v[0], uL[1], dot4(v[1], uL[0], 0.0));
+            // ---- b in both studies: the 9 assignments of (a, c); their sums for a and c ----
+            double z[3][3];
 #pragma unroll
             for (int xa = 0; xa < 3; xa++)
 #pragma unroll
-                for (int xb = 0; xb < 3; xb++) {
-                    const int al = (xa != 1) | ((xb != 1) << 1), be = (xa != 0) | ((xb != 0) << 1);
-                    const double X = P[0][al] * Q[1][be];
-                    Pl[xa][xb] = fma(Q[0][al], S1[be], X);
-                    Pw[xa][xb] = fma(Q[0][al], T1[be], X);
+                for (int xc = 0; xc < 3; xc++) {
+                    const int i0 = (xa != 1) | ((xc != 1) << 1), i1 = (xa != 0) | ((xc != 0) << 1);
+                    z[xa][xc] = v[0][i0] * v[1][i1];
+                    ZS[xa][xc] += z[xa][xc];
                 }
-            double WA[3], WB[3];
+            const double Z0 = (z[0][0] + z[0][1]) + (z[1][0] + z[1][1]);  // neither a nor c shared
+            const double Z1 = (z[2][0] + z[2][1]) + (z[0][2] + z[1][2]);  // one of them shared
+            const double WB2 = fma(rho, fma(rho, z[2][2], Z1), Z0);
+            const double LB2 = (Z0 + Z1) + z[2][2];
 #pragma unroll
-            for (int x = 0; x < 3; x++) {
-                WA[x] = fma(rho, Pw[x][2], Pw[x][0] + Pw[x][1]);
-                WB[x] = fma(rho, Pw[2][x], Pw[0][x] + Pw[1][x]);
+            for (int i = 0; i < 4; i++) {
+                V0[i] += v[0][i];
+                V1[i] += v[1][i];
             }
-            const double LA2 = (Pl[2][0] + Pl[2][1]) + Pl[2][2];
-            const double NA = ((Pl[0][0] + Pl[0][1]) + Pl[0][2]) + ((Pl[1][0] + Pl[1][1]) + Pl[1][2]);
-            const double LB2 = (Pl[0][2] + Pl[1][2]) + Pl[2][2];
-            const double NB = ((Pl[0][0] + Pl[1][0]) + Pl[2][0]) + ((Pl[0][1] + Pl[1][1]) + Pl[2][1]);
-            tiny |= (NA < kTinyNs) | (NB < kTinyNs) | (NC < kTinyNs);
-            // ---- folds: a (registers, at G), c (registers, x fC), b (LDS slot, x fS), noCausal ----
+            tiny |= NB < kTinyNs;
+            // ---- b slot (LDS, x fS) ----
             const double fS = ldexp(1.0, G - sm_);
-            sW0[bs] = fma(WB[0], fS, o0);
-            sW1[bs] = fma(WB[1], fS, o1);
-            sW2[bs] = fma(WB[2], fS, o2);
+            sW0[bs] = fma(WB0, fS, o0);
+            sW1[bs] = fma(WB1, fS, o1);
+            sW2[bs] = fma(WB2, fS, o2);
             sSl[bs] = fma(LB2, fS, oS);
             sNs[bs] = fma(NB, fS, oN);
-            aW0 += WA[0];
-            aW1 += WA[1];
-            aW2 += WA[2];
-            aSl += LA2;
-            aNs += NA;
-            cW0 = fma(WC0, fC, cW0);
-            cW1 = fma(WC1, fC, cW1);
-            cW2 = fma(WC2, fC, cW2);
-            cSl = fma(LC2, fC, cSl);
-            cNs = fma(NC, fC, cNs);
-            // noCausal[s]: every member in the other study only
-            nc0 = fma(Q[1][3], f0, nc0);
-            nc1 = fma(Q[0][3], f1, nc1);
-            npat += ALLPRES ? 27.0 : wac * bW[bs];
+            if (!ALLPRES) npat += wac * bW[bs];
         };
         // Steps on which every lane is active run pipelined: the whole walk of an
         // off-diagonal tile, and steps 1..30 of a diagonal tile whose a lies
@@ -1007,13 +993,48 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 double q[2];
                 chain(j, gcur, N, q);
                 finish(j, N, q, mcur, ncur);
+                nact++;
             }
             __builtin_amdgcn_wave_barrier();
         }
+        nact += je - j0;
+        if (ALLPRES) npat += 27.0 * nact;
+        // ---- members a and c: fold the walk's sums.  Per assignment (xa, xc) of the
+        // pair, L = (b in study 0 only) + (b in study 1 only), then b in both from ZS
+        double Cw[3][3], Cu[3][3];  // prior-weighted (b's rho, not a's or c's) / plain
+#pragma unroll
+        for (int xa = 0; xa < 3; xa++)
+#pragma unroll
+            for (int xc = 0; xc < 3; xc++) {
+                const int i0 = (xa != 1) | ((xc != 1) << 1), i1 = (xa != 0) | ((xc != 0) << 1);
+                const double L = fma(V0[i0], Ep[1][i1], Ep[0][i0] * V1[i1]);
+                Cw[xa][xc] = fma(rho, ZS[xa][xc], L);
+                Cu[xa][xc] = L + ZS[xa][xc];
+            }
+        double WA[3], WC[3];
+#pragma unroll
+        for (int x = 0; x < 3; x++) {
+            WA[x] = fma(rho, Cw[x][2], Cw[x][0] + Cw[x][1]);
+            WC[x] = fma(rho, Cw[2][x], Cw[0][x] + Cw[1][x]);
+        }
+        const double LA2 = (Cu[2][0] + Cu[2][1]) + Cu[2][2];
+        const double NA = ((Cu[0][0] + Cu[0][1]) + Cu[0][2]) + ((Cu[1][0] + Cu[1][1]) + Cu[1][2]);
+        const double LC2 = (Cu[0][2] + Cu[1][2]) + Cu[2][2];
+        const double NC = ((Cu[0][0] + Cu[1][0]) + Cu[2][0]) + ((Cu[0][1] + Cu[1][1]) + Cu[2][1]);
+        // a notSharedLL sum far below the shift loses precision: exact rerun
+        if (nact > 0) tiny |= (NA < kTinyNs) | (NC < kTinyNs);
+        cW0 = fma(WC[0], fC, cW0);
+        cW1 = fma(WC[1], fC, cW1);
+        cW2 = fma(WC[2], fC, cW2);
+        cSl = fma(LC2, fC, cSl);
+        cNs = fma(NC, fC, cNs);
+        // noCausal[s]: every member in the other study only
+        nc0 = fma(V1[3], f0, nc0);
+        nc1 = fma(V0[3], f1, nc1);
         if (__builtin_amdgcn_ballot_w64(tiny))
             if (tiny) atomicOr(flag, 1);
         if (A.trace && ai == 0) t_ph[2] = wall_clock64();
-        Acc5 ra = wrec(G, aW0, aW1, aW2, aSl, aNs, rho, A.Ck, A.pit0);
+        Acc5 ra = wrec(G, WA[0], WA[1], WA[2], LA2, NA, rho, A.Ck, A.pit0);
         wave_fold_acc(ra);
         const int qa = sPos[2][ai];
         if (t == 0 && qa >= 0) store_rec(rec + qa, ra);
