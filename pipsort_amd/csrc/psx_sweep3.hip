@@ -46,6 +46,10 @@
 #include "psx_sweep_dev.h"
 #include "psx_sweep_unit.h"
 
+// device-library wave reductions (DPP, result in every lane)
+extern "C" __device__ __attribute__((const)) int __ockl_wfred_max_i32(int);
+extern "C" __device__ __attribute__((const)) double __ockl_wfred_add_f64(double);
+
 namespace psx {
 
 constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52: round-to-nearest-integer add
@@ -732,6 +736,15 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         int R[2];
         double2 gnx = g01[j0 * 64], mnx = m01[j0 * 64];
         int2 nnx = bnn[j0 * 64];
+        // the next a's Sigma~ row entries, one a ahead: staged into LDS (this
+        // lane's own entries) once this a's prologue is done
+        const bool nxt = ai + 1 < a1 - a0;
+        double nGab[2], nGac[2];
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            nGab[s] = (nxt && okb) ? A.G[s][(size_t)(ua + 1) * ldg + ubl] : 0.0;
+            nGac[s] = (nxt && okc) ? A.G[s][(size_t)(ua + 1) * ldg + uc] : 0.0;
+        }
         __syncthreads();  // previous a's (a, b) terms and slots fully consumed
 #pragma unroll
         for (int s = 0; s < 2; s++) {
@@ -745,7 +758,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             double muA;
             split3(ha, rPa, tab, nA, muA);
             {
-                const double Gab = ai ? (okb ? A.G[s][(size_t)ua * ldg + ubl] : 0.0) : g1ab[s][t];
+                const double Gab = g1ab[s][t];
                 const double Abb = okb ? A.Ad[s][ubl] : 1.0;
                 const double yb = okb ? A.ys[s][ubl] : 0.0;
                 const double l = Gab * iAaa;
@@ -769,7 +782,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 abMuB[s][t] = ldexp(muB, nB - nAB);
                 abN[s][t] = nAB;
             }
-            const double Gac = ai ? (okc ? A.G[s][(size_t)ua * ldg + uc] : 0.0) : g1ac[s][t];
+            const double Gac = g1ac[s][t];
             l1[s] = Gac * iAaa;
             D1[s] = fma(-l1[s], Gac, Acc[s]);
             const double w1 = fma(-l1[s], ya, yc[s]);
@@ -835,9 +848,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         // round-to-nearest magic offset by R: N = round(256 (h3 - R)), so n3 - R = N >> 8
         const double cmag[2] = {kMagic - 256.0 * R[0], kMagic - 256.0 * R[1]};
         {
-            int Gm = G;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) Gm = max(Gm, __shfl_xor(Gm, o));
+            const int Gm = __ockl_wfred_max_i32(G);  // DPP wave reduction, no LDS round trips
             const int Ms = max(sM[t], Gm), d = sM[t] - Ms;
             sW0[t] = ldexp(sW0[t], d);
             sW1[t] = ldexp(sW1[t], d);
@@ -847,6 +858,13 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             sM[t] = Ms;
         }
         __syncthreads();  // (a, b) terms and slot shifts visible
+        if (nxt) {
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                g1ab[s][t] = nGab[s];
+                g1ac[s][t] = nGac[s];
+            }
+        }
         if (A.trace && ai == 0) t_ph[1] = wall_clock64();
 
         // The b-walk.  chain(j) is step j's dependent {a, b, c} extension up to
@@ -1034,10 +1052,22 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         if (__builtin_amdgcn_ballot_w64(tiny))
             if (tiny) atomicOr(flag, 1);
         if (A.trace && ai == 0) t_ph[2] = wall_clock64();
-        Acc5 ra = wrec(G, WA[0], WA[1], WA[2], LA2, NA, rho, A.Ck, A.pit0);
-        wave_fold_acc(ra);
-        const int qa = sPos[2][ai];
-        if (t == 0 && qa >= 0) store_rec(rec + qa, ra);
+        {
+            // the a record: every lane's five sums share its shift G, so the wave
+            // folds them at the largest G among lanes with content (a lane's
+            // notSharedLL is >= 2^-900 of its own G, so nothing that matters is
+            // lost) with DPP wave sums
+            const bool has = (WA[0] + WA[1] + WA[2] + LA2 + NA) != 0.0;
+            const int Gw = __ockl_wfred_max_i32(has ? G : EMPTY);
+            const int dg = has ? G - Gw : -2000;
+            const double W0 = __ockl_wfred_add_f64(ldexp(WA[0], dg));
+            const double W1 = __ockl_wfred_add_f64(ldexp(WA[1], dg));
+            const double W2 = __ockl_wfred_add_f64(ldexp(WA[2], dg));
+            const double Sl = __ockl_wfred_add_f64(ldexp(LA2, dg));
+            const double Ns = __ockl_wfred_add_f64(ldexp(NA, dg));
+            const int qa = sPos[2][ai];
+            if (t == 0 && qa >= 0) store_rec(rec + qa, wrec(Gw, W0, W1, W2, Sl, Ns, rho, A.Ck, A.pit0));
+        }
         if (A.trace && ai == 0) t_ph[3] = wall_clock64();
     }
     __syncthreads();
