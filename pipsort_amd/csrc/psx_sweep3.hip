@@ -260,8 +260,25 @@ struct Sweep3Smem {
     double g1ab[2][64], g1ac[2][64];  // the first a's Sigma~ row entries
     int sPos[3][64];                   // record positions: c, b slot, a
 };
+// LDS of the fast k = 3 variant: the per-b terms of both studies side by side
+// (one 16-byte read per term and step; lane t reads slot (t + j) & 63, so the
+// reads are conflict-free), and the b-slot accumulators with their per-a scale
+// factor sF = 2^(Gm - sM) (Gm: the wave's largest a shift)
+struct Sweep3FastSmem {
+    double tab[256];
+    double bH[2][64], bR[2][64];
+    double2 abG[64], abI[64], abIW[64], abH[64], abR[64], abMu[64], abMuB[64];
+    int2 abN[64];
+    double sF[64];
+    double bW[64];
+    double sW0[64], sW1[64], sW2[64], sSl[64], sNs[64];
+    int sM[64];
+    double g1ab[2][64], g1ac[2][64];  // this a's Sigma~ row entries
+    int sPos[3][64];                   // record positions: c, b slot, a
+};
 union SweepSmem {  // a block runs either a k = 3 unit or a level-2 unit
     Sweep3Smem s3;
+    Sweep3FastSmem f3;
     SweepUnitSmem u2;
 };
 
@@ -644,28 +661,21 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                                                  Acc5* __restrict__ rec, SetRec* __restrict__ srec, int rec_stride,
                                                  int* __restrict__ flag, const int* __restrict__ pos, SweepSmem& sm,
                                                  bool& redo) {
-    double (&tab)[256] = sm.s3.tab;
-    double (&bH)[2][64] = sm.s3.bH;
-    double (&bR)[2][64] = sm.s3.bR;
-    double (&abG)[2][64] = sm.s3.abG;
-    double (&abIW)[2][64] = sm.s3.abD;  // fast variant: I_ab * w_ab / 2 (the pivot itself is not needed)
-    double (&abI)[2][64] = sm.s3.abI;
-    double (&abW)[2][64] = sm.s3.abW;
-    double (&abH)[2][64] = sm.s3.abH;
-    double (&abR)[2][64] = sm.s3.abR;
-    double (&abMu)[2][64] = sm.s3.abMu;
-    double (&abMuB)[2][64] = sm.s3.abMuB;
-    int (&abN)[2][64] = sm.s3.abN;
-    double (&bW)[64] = sm.s3.bW;
-    double (&sW0)[64] = sm.s3.sP0;  // b slots: W0, W1, W2 (own rho deferred), sharedLL, notSharedLL
-    double (&sW1)[64] = sm.s3.sP1;
-    double (&sW2)[64] = sm.s3.sSh;
-    double (&sSl)[64] = sm.s3.sSl;
-    double (&sNs)[64] = sm.s3.sNs;
-    int (&sM)[64] = sm.s3.sM;
-    double (&g1ab)[2][64] = sm.s3.g1ab;
-    double (&g1ac)[2][64] = sm.s3.g1ac;
-    int (&sPos)[3][64] = sm.s3.sPos;
+    Sweep3FastSmem& F = sm.f3;
+    double (&tab)[256] = F.tab;
+    double (&bH)[2][64] = F.bH;
+    double (&bR)[2][64] = F.bR;
+    double (&bW)[64] = F.bW;
+    double (&sW0)[64] = F.sW0;  // b slots: W0, W1, W2 (own rho deferred), sharedLL, notSharedLL
+    double (&sW1)[64] = F.sW1;
+    double (&sW2)[64] = F.sW2;
+    double (&sSl)[64] = F.sSl;
+    double (&sNs)[64] = F.sNs;
+    double (&sF)[64] = F.sF;
+    int (&sM)[64] = F.sM;
+    double (&g1ab)[2][64] = F.g1ab;
+    double (&g1ac)[2][64] = F.g1ac;
+    int (&sPos)[3][64] = F.sPos;
 
     const int t = threadIdx.x;
     const unsigned long long t_start = A.trace ? wall_clock64() : 0ull;
@@ -746,6 +756,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             nGac[s] = (nxt && okc) ? A.G[s][(size_t)(ua + 1) * ldg + uc] : 0.0;
         }
         __syncthreads();  // previous a's (a, b) terms and slots fully consumed
+        double pG[2], pI[2], pIW[2], pH[2], pR[2], pMu[2], pMuB[2];
+        int pN[2];
 #pragma unroll
         for (int s = 0; s < 2; s++) {
             const double chia = (ALLPRES || ((pa >> s) & 1u)) ? 1.0 : 0.0;
@@ -772,15 +784,14 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 double muAB, muB;
                 split3(hab, rPab, tab, nAB, muAB);
                 split3(bH[s][t], bR[s][t] * (2.0 / A.rsd[s]), tab, nB, muB);
-                abG[s][t] = Gab;
-                abI[s][t] = rab * rab;
-                abW[s][t] = 0.5 * wab;
-                abIW[s][t] = rab * rab * (0.5 * wab);
-                abH[s][t] = hab;
-                abR[s][t] = rPab * (0.5 * A.rsd[s]);
-                abMu[s][t] = muAB;
-                abMuB[s][t] = ldexp(muB, nB - nAB);
-                abN[s][t] = nAB;
+                pG[s] = Gab;
+                pI[s] = rab * rab;
+                pIW[s] = rab * rab * (0.5 * wab);  // I_ab w_ab / 2 (the pivot itself is not needed)
+                pH[s] = hab;
+                pR[s] = rPab * (0.5 * A.rsd[s]);
+                pMu[s] = muAB;
+                pMuB[s] = ldexp(muB, nB - nAB);
+                pN[s] = nAB;
             }
             const double Gac = g1ac[s][t];
             l1[s] = Gac * iAaa;
@@ -799,6 +810,14 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             Ep[s][2] = ldexp(muC[s], nC[s] - n1);
             Ep[s][3] = mu1;
         }
+        F.abG[t] = make_double2(pG[0], pG[1]);
+        F.abI[t] = make_double2(pI[0], pI[1]);
+        F.abIW[t] = make_double2(pIW[0], pIW[1]);
+        F.abH[t] = make_double2(pH[0], pH[1]);
+        F.abR[t] = make_double2(pR[0], pR[1]);
+        F.abMu[t] = make_double2(pMu[0], pMu[1]);
+        F.abMuB[t] = make_double2(pMuB[0], pMuB[1]);
+        F.abN[t] = make_int2(pN[0], pN[1]);
         const double wac = wc * memb_weight(pa);
         // this a's reference G: the a accumulator sits at it; c / noCausal / the b
         // slots move their shift up to it (values scale down exactly) once per a
@@ -847,6 +866,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         const double fC = ldexp(1.0, G - mC), f0 = ldexp(1.0, R[1] - m0), f1 = ldexp(1.0, R[0] - m1);
         // round-to-nearest magic offset by R: N = round(256 (h3 - R)), so n3 - R = N >> 8
         const double cmag[2] = {kMagic - 256.0 * R[0], kMagic - 256.0 * R[1]};
+        double gF;
         {
             const int Gm = __ockl_wfred_max_i32(G);  // DPP wave reduction, no LDS round trips
             const int Ms = max(sM[t], Gm), d = sM[t] - Ms;
@@ -856,6 +876,10 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             sSl[t] = ldexp(sSl[t], d);
             sNs[t] = ldexp(sNs[t], d);
             sM[t] = Ms;
+            // a lane's contribution to slot b is scaled by 2^(G - sM[b]) = sF[b] * gF
+            // (powers of two: the product is exact down to the underflow either form has)
+            sF[t] = ldexp(1.0, Gm - Ms);
+            gF = ldexp(1.0, G - Gm);
         }
         __syncthreads();  // (a, b) terms and slot shifts visible
         if (nxt) {
@@ -877,26 +901,27 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         bool tiny = false;
         auto chain = [&](int j, double2 g, int (&N)[2], double (&q)[2]) {
             const int bs = (t + j) & 63;
+            const double2 aG = F.abG[bs], aI = F.abI[bs], aIW = F.abIW[bs], aH = F.abH[bs], aR = F.abR[bs];
 #pragma unroll
             for (int s = 0; s < 2; s++) {
                 // x = the unnormalised L entry of c against b; D_ab I_ab = 1 folds the pivot away
                 const double Gbc = s ? g.y : g.x;
-                const double x = fma(-l1[s], abG[s][bs], Gbc);
-                const double lcb = x * abI[s][bs];
+                const double x = fma(-l1[s], s ? aG.y : aG.x, Gbc);
+                const double lcb = x * (s ? aI.y : aI.x);
                 const double D3 = fma(-x, lcb, D1[s]);
-                const double w3 = fma(-x, abIW[s][bs], w1h[s]);
+                const double w3 = fma(-x, s ? aIW.y : aIW.x, w1h[s]);
                 const double r3 = rsq2x(D3);
                 const double t3 = w3 * r3;
-                const double h3 = fma(t3, t3, abH[s][bs]);
-                double rP3 = abR[s][bs] * r3;
+                const double h3 = fma(t3, t3, s ? aH.y : aH.x);
+                double rP3 = (s ? aR.y : aR.x) * r3;
                 if (!ALLPRES && !((pcm >> s) & 1u)) rP3 = 0.0;  // c absent from study s
                 split3r(h3, rP3, cmag[s], N[s], q[s]);
             }
         };
         auto finish = [&](int j, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
             const int bs = (t + j) & 63;
-            const int sm_ = sM[bs];
-            const double o0 = sW0[bs], o1 = sW1[bs], o2 = sW2[bs], oS = sSl[bs], oN = sNs[bs];
+            const double2 aMuB = F.abMuB[bs], aMu = F.abMu[bs];
+            const int2 aN = F.abN[bs];
             // v[s][A] = E_s[A + b] relative to 2^{R_s}: {b}, {a, b}, {b, c}, {a, b, c}
             double v[2][4];
             int d3s = 0;
@@ -906,10 +931,10 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 const double mu3 = tab[N[s] & 255] * q[s];
                 const int n2 = s ? ncur.y : ncur.x;
                 const double mu2 = s ? mcur.y : mcur.x;
-                const int dab = abN[s][bs] - R[s];
+                const int dab = (s ? aN.y : aN.x) - R[s];
                 d3s += d3;
-                v[s][0] = ldexp(abMuB[s][bs], dab);
-                v[s][1] = ldexp(abMu[s][bs], dab);
+                v[s][0] = ldexp(s ? aMuB.y : aMuB.x, dab);
+                v[s][1] = ldexp(s ? aMu.y : aMu.x, dab);
                 v[s][2] = ldexp(mu2, n2 - R[s]);
                 v[s][3] = ldexp(mu3, d3);
             }
@@ -942,12 +967,14 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             }
             tiny |= NB < kTinyNs;
             // ---- b slot (LDS, x fS) ----
-            const double fS = ldexp(1.0, G - sm_);
-            sW0[bs] = fma(WB0, fS, o0);
-            sW1[bs] = fma(WB1, fS, o1);
-            sW2[bs] = fma(WB2, fS, o2);
-            sSl[bs] = fma(LB2, fS, oS);
-            sNs[bs] = fma(NB, fS, oN);
+            const double fS = sF[bs] * gF;
+            // LDS float adds: no read round trip; one lane per slot per step, and a
+            // wave's LDS instructions execute in issue order (deterministic)
+            __hip_atomic_fetch_add(&sW0[bs], WB0 * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&sW1[bs], WB1 * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&sW2[bs], WB2 * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&sSl[bs], LB2 * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&sNs[bs], NB * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (!ALLPRES) npat += wac * bW[bs];
         };
         // Steps on which every lane is active run pipelined: the whole walk of an
