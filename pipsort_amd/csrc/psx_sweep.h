@@ -99,6 +99,7 @@ int launch_scale_y(const double* y, int n, double* ys, hipStream_t st);
 int launch_build_skewT(const double* G, int ldg, int pad, double* skew, hipStream_t st);
 // {b, c} subset weights of every skewT entry (the a-independent half of a k = 3
 // step), computed once per locus with the sweep kernel's own arithmetic
+constexpr int kTileRowPad = 4;  // zero rows after the last tile of mu01 / bcn / g01
 int launch_build_bc3(const Sweep3Args& A, int ntile, double2* mu01, int2* n, hipStream_t st);
 // out[i] = (a[i], b[i])
 int launch_interleave2(const double* a, const double* b, size_t n, double2* out, hipStream_t st);

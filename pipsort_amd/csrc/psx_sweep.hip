@@ -588,10 +588,16 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
     }
     {  // the a-independent {b, c} weights of every k = 3 step
         Sweep3Args S3 = sweep3_args(C, a, U, ldg);
-        SWCHK(hipMalloc(&C.d_mu01, sizeof(double2) * (size_t)ntile * 4096));
-        SWCHK(hipMalloc(&C.d_bcn, sizeof(int2) * (size_t)ntile * 4096));
+        // kTileRowPad rows past the last tile: the pipelined b-walk loads up to
+        // three steps ahead without clamping (rows it never uses)
+        const size_t nrow = (size_t)ntile * 4096, npad = (size_t)kTileRowPad * 64;
+        SWCHK(hipMalloc(&C.d_mu01, sizeof(double2) * (nrow + npad)));
+        SWCHK(hipMalloc(&C.d_bcn, sizeof(int2) * (nrow + npad)));
+        SWCHK(hipMalloc(&C.d_g01, sizeof(double2) * (nrow + npad)));
+        SWCHK(hipMemsetAsync(C.d_mu01 + nrow, 0, sizeof(double2) * npad, st));
+        SWCHK(hipMemsetAsync(C.d_bcn + nrow, 0, sizeof(int2) * npad, st));
+        SWCHK(hipMemsetAsync(C.d_g01 + nrow, 0, sizeof(double2) * npad, st));
         if (launch_build_bc3(S3, ntile, C.d_mu01, C.d_bcn, st)) SWCHK(hipGetLastError());
-        SWCHK(hipMalloc(&C.d_g01, sizeof(double2) * (size_t)ntile * 4096));
         if (launch_interleave2(C.d_skewT[0], C.d_skewT[1], (size_t)ntile * 4096, C.d_g01, st)) SWCHK(hipGetLastError());
     }
     C.skew_ldg = ldg;

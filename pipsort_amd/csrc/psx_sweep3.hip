@@ -987,27 +987,33 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         else if ((va < 64 * K || va >= 64 * K + 64) && 64 * K >= pad)
             je = j0 + ((min(j1, 32) - j0) & ~1);
         if (je > j0) {
-            // unrolled by two: the chained state alternates between (NA, qA) and (NB, qB)
-            double2 g_next = g01[min(j0 + 1, je - 1) * 64];
+            // unrolled by two: the chained state alternates between (NA, qA) and (NB, qB).
+            // Loads run up to three rows ahead unclamped (the buffers carry
+            // kTileRowPad rows past the last tile; what lies past je is not used),
+            // so they address off one lane offset with immediate row offsets
+            const double2* gb = A.g01 + (size_t)tile * 4096;
+            const double2* mb = A.mu01 + (size_t)tile * 4096;
+            const int2* nb = A.bcn + (size_t)tile * 4096;
+            double2 g_next = gb[(j0 + 1) * 64 + t];
             double2 m_cur = mnx;
             int2 n_cur = nnx;
             int NA[2], NB[2];
             double qA[2], qB[2];
             chain(j0, gnx, NA, qA);
             for (int j = j0; j < je; j += 2) {
-                const int r1 = min(j + 1, je - 1), r2 = min(j + 2, je - 1), r3 = min(j + 3, je - 1);
-                const double2 m_nxt = m01[r1 * 64];
-                const int2 n_nxt = bnn[r1 * 64];
-                const double2 g_after = g01[r2 * 64];
-                chain(r1, g_next, NB, qB);
+                const int o = j * 64 + t;
+                const double2 m_nxt = mb[o + 64];
+                const int2 n_nxt = nb[o + 64];
+                const double2 g_after = gb[o + 128];
+                chain(j + 1, g_next, NB, qB);
                 finish(j, NA, qA, m_cur, n_cur);
                 // b-slot ownership rotates across lanes every step: the workgroup is
                 // one wave and LDS executes a wave's instructions in issue order
                 __builtin_amdgcn_wave_barrier();
-                m_cur = m01[r2 * 64];
-                n_cur = bnn[r2 * 64];
-                g_next = g01[r3 * 64];
-                chain(r2, g_after, NA, qA);  // (the last pair's repeat is unused)
+                m_cur = mb[o + 128];
+                n_cur = nb[o + 128];
+                g_next = gb[o + 192];
+                chain(j + 2, g_after, NA, qA);  // (the last pair's is not used)
                 finish(j + 1, NB, qB, m_nxt, n_nxt);
                 __builtin_amdgcn_wave_barrier();
             }
