@@ -416,36 +416,42 @@ __device__ void eval_single(const DevProb& P, int u, Acc5& a, SetRec& r) {
 //                shard + every tiled-level unit record (srec[0, nsrec))
 //   block 1 + u: acc[u] = level-1 record of u (if in this shard), then u's
 //                records of level A and level B (dense per-SNP runs)
+// One wave per block: the merge of pass i runs beside sweep i + 1, whose
+// one-wave blocks hold every wave slot; a one-wave merge block takes the first
+// slot any sweep block frees (a wider block waits for several free slots on
+// one CU at once and was starved for the whole sweep).
 // Fixed fold order: deterministic.
-__global__ __launch_bounds__(256) void k_merge_pass_l1(DevProb P, int lo, int hi, const Acc5* __restrict__ recA,
+constexpr int kMergeThreads = 64;
+__global__ __launch_bounds__(kMergeThreads) void k_merge_pass_l1(DevProb P, int lo, int hi, const Acc5* __restrict__ recA,
                                                        const int* __restrict__ dptrA, const Acc5* __restrict__ recB,
                                                        const int* __restrict__ dptrB, const SetRec* __restrict__ srec,
                                                        long nsrec, SetRec extra, Acc5* __restrict__ acc,
                                                        SetRec* __restrict__ sacc, int* __restrict__ flag,
                                                        int* __restrict__ sticky) {
+    constexpr int T = kMergeThreads;
     const int tid = threadIdx.x;
     if (blockIdx.x == 0) {
-        __shared__ SetRec ss[4];
         SetRec a = psx::set_zero();
-        for (int u = lo + tid; u < hi; u += 256) {
+        for (int u = lo + tid; u < hi; u += T) {
             Acc5 dummy;
             SetRec r;
             eval_single(P, u, dummy, r);
             psx::fold_set(a, r);
         }
         long i = tid;
-        for (; i + 768 < nsrec; i += 1024) {  // four independent loads in flight per thread
-            const SetRec r0 = srec[i], r1 = srec[i + 256], r2 = srec[i + 512], r3 = srec[i + 768];
-            psx::fold_set(a, r0); psx::fold_set(a, r1); psx::fold_set(a, r2); psx::fold_set(a, r3);
+        for (; i + 7 * T < nsrec; i += 8 * T) {  // eight independent loads in flight per lane
+            SetRec r[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) r[q] = srec[i + q * T];
+#pragma unroll
+            for (int q = 0; q < 8; q++) psx::fold_set(a, r[q]);
         }
-        for (; i < nsrec; i += 256) psx::fold_set(a, srec[i]);
+        for (; i < nsrec; i += T) psx::fold_set(a, srec[i]);
         psx::wave_fold_set(a);
-        if ((tid & 63) == 0) ss[tid >> 6] = a;
-        __syncthreads();
         if (tid == 0) {
             SetRec g = psx::set_zero();
             psx::fold_set(g, extra);
-            for (int w = 0; w < 4; w++) psx::fold_set(g, ss[w]);
+            psx::fold_set(g, a);
             // hand the pass's EXACT flag to the host in the status record and re-arm
             // it for the next pass (the kernels that raise it have completed)
             // (atomic exchange: with pipelined passes the next pass's sweep may
@@ -456,7 +462,6 @@ __global__ __launch_bounds__(256) void k_merge_pass_l1(DevProb P, int lo, int hi
         }
         return;
     }
-    __shared__ Acc5 sh[4];
     const int u = blockIdx.x - 1;
     if (u >= P.U) return;
     const int a0 = dptrA ? dptrA[u] : 0, na = dptrA ? dptrA[u + 1] - a0 : 0;
@@ -464,24 +469,25 @@ __global__ __launch_bounds__(256) void k_merge_pass_l1(DevProb P, int lo, int hi
     const int n = na + nb;
     Acc5 a = psx::acc_zero();
     int i = tid;
-    for (; i + 256 < n; i += 512) {  // two independent loads in flight per thread
-        const Acc5 x0 = i < na ? recA[a0 + i] : recB[b0 + i - na];
-        const int j = i + 256;
-        const Acc5 x1 = j < na ? recA[a0 + j] : recB[b0 + j - na];
-        psx::fold_acc(a, x0);
-        psx::fold_acc(a, x1);
+    for (; i + 3 * T < n; i += 4 * T) {  // four independent loads in flight per lane
+        Acc5 x[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int j = i + q * T;
+            x[q] = j < na ? recA[a0 + j] : recB[b0 + j - na];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) psx::fold_acc(a, x[q]);
     }
-    for (; i < n; i += 256) psx::fold_acc(a, i < na ? recA[a0 + i] : recB[b0 + i - na]);
+    for (; i < n; i += T) psx::fold_acc(a, i < na ? recA[a0 + i] : recB[b0 + i - na]);
     psx::wave_fold_acc(a);
-    if ((tid & 63) == 0) sh[tid >> 6] = a;
-    __syncthreads();
     if (tid == 0) {
         Acc5 g = {0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0, 0.0};
         if (u >= lo && u < hi) {
             SetRec dummy;
             eval_single(P, u, g, dummy);
         }
-        for (int w = 0; w < 4; w++) psx::fold_acc(g, sh[w]);
+        psx::fold_acc(g, a);
         acc[u] = g;
     }
 }
@@ -1069,7 +1075,7 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     const SetRec extra = e->rank == 0 ? null_rec(e, 1.0) : psx::set_zero();
     psx::SweepPlan* mA = low ? low : top;
     psx::SweepPlan* mB = low ? top : nullptr;
-    hipLaunchKernelGGL(k_merge_pass_l1, dim3(e->U + 1), dim3(256), 0, X, e->dp, lo, hi, psx::plan_records(*mA, par),
+    hipLaunchKernelGGL(k_merge_pass_l1, dim3(e->U + 1), dim3(kMergeThreads), 0, X, e->dp, lo, hi, psx::plan_records(*mA, par),
                        mA->d_dptr, mB ? psx::plan_records(*mB, par) : nullptr, mB ? mB->d_dptr : nullptr, dpass,
                        (long)(nl + nt), extra, e->dacc, e->dsacc, pflag, e->dflag + 1);
     HIPCHK(hipGetLastError());
@@ -2124,7 +2130,8 @@ int psx_set_stream(psx_engine* e, void* stream) {
 int psx_merge_partials(psx_engine* e, const void* src, int32_t count) {
     HIPCHK(hipSetDevice(e->dev));
     if (count < 1) return fail(PSX_EINVAL, "count < 1");
-    hipLaunchKernelGGL(k_merge_partials, dim3((e->U + 255) / 256), dim3(256), 0, e->stream, (const Acc5*)src, e->U,
+    // one-wave blocks: they take the first wave slots a running sweep frees
+    hipLaunchKernelGGL(k_merge_partials, dim3((e->U + 63) / 64), dim3(64), 0, e->stream, (const Acc5*)src, e->U,
                        e->ldg, count, e->dacc, e->dsacc, e->dflag);
     HIPCHK(hipGetLastError());
     if (!e->external_stream) HIPCHK(hipStreamSynchronize(e->stream));
