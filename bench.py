@@ -40,6 +40,7 @@ from pipsort_amd import synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (spec)
+VALU_ISSUE_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12  # 1024 SIMDs x 16 lanes x 2.4 GHz (one wave64 op / 4 cycles)
 
 WORKLOADS = {
     # name: (M, c, p, n, description)
@@ -615,7 +616,7 @@ def main():
                          + (f" / {world} (this rank's shard)" if world > 1 else ""))
         else:
             flops = tm["flops"]
-            flops_src = "model: 281 FP64 operations per 3-SNP union set (PMC-calibrated, earlier build)"
+            flops_src = "model: 159 FP64 operations per 3-SNP union set (PMC-calibrated, r02zd build)"
         achieved = flops / avg_kernel_s / 1e12 if avg_kernel_s > 0 else 0.0
         roofline = {"bound": "valu_fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": achieved / FP64_PEAK_TFLOPS,
@@ -624,6 +625,15 @@ def main():
                     "kernel_ms": avg_kernel_s * 1e3,
                     "flops_per_launch": flops, "flops_source": flops_src,
                     "pmc_kernel_src_sha": (pmc or {}).get("kernel_src_sha"), "kernel_src_sha": kernel_src_sha()}
+        if pmc and pmc.get("valu_insts_per_launch") and avg_kernel_s > 0:
+            # the issue roof that actually binds: every wave64 VALU instruction (FP64,
+            # integer or select alike) holds its 16-lane SIMD for 4 cycles, so the
+            # chip issues at most 1024 SIMDs x 16 lanes x 2.4 GHz lane operations / s
+            lane_ops = pmc["valu_insts_per_launch"] * 64.0 / world
+            t_ops = lane_ops / avg_kernel_s / 1e12
+            roofline["valu_issue"] = {"achieved": t_ops, "peak": VALU_ISSUE_PEAK_TOPS, "unit": "T lane-op/s",
+                                      "frac": t_ops / VALU_ISSUE_PEAK_TOPS,
+                                      "source": "PMC SQ_INSTS_VALU x 64 per launch / kernel_ms"}
         if pmc and world == 1:
             roofline["valu_busy"] = pmc.get("valu_busy")
             roofline["fp64_valu_share"] = pmc.get("fp64_valu_share")

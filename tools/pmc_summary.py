@@ -46,6 +46,7 @@ if "SQ_INSTS_VALU" in c and "GRBM_GUI_ACTIVE" in c:
     # the kernel's cycle count is GRBM_GUI_ACTIVE / 8.
     out["gpu_cycles_per_launch"] = c["GRBM_GUI_ACTIVE"] / 8.0
     out["valu_busy"] = 4.0 * c["SQ_INSTS_VALU"] / (1024.0 * c["GRBM_GUI_ACTIVE"] / 8.0)
+    out["valu_insts_per_launch"] = c["SQ_INSTS_VALU"]  # wave64 VALU instructions of one launch
     f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
                                       "SQ_INSTS_VALU_TRANS_F64"))
     if f64:
