@@ -565,7 +565,7 @@ struct psx_engine {
     // caller's exchange) on `stream`; record buffers alternate by pass parity
     hipStream_t cstream = nullptr;
 
-    static constexpr int kBufs = 3;  // record buffer sets: sweep i waits for merge i - 3
+    static constexpr int kBufs = psx::kRecBufs;  // record buffer sets: sweep i waits for merge i - kBufs
     hipEvent_t mdone[kBufs] = {};
     bool mdone_rec[kBufs] = {};
     int a_par = kBufs - 1;
@@ -1047,7 +1047,9 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
         if (e->mdone_rec[par]) HIPCHK(hipEventSynchronize(e->mdone[par]));
     }
     SetRec* const dpass = e->dpass + par * npass;
-    int* const pflag = e->dflag + (par ? 1 + par : 0);  // EXACT flag word of this buffer set ([1]: sticky word)
+    // EXACT flag word of this buffer set ([1]: sticky word); the words share one image slot
+    static_assert(sizeof(int) * (psx_engine::kBufs + 1) <= sizeof(Acc5), "flag words fit the status slot");
+    int* const pflag = e->dflag + (par ? 1 + par : 0);
     // no zeroing pass: the merge overwrites every per-SNP slot and the scalars,
     // padding slots stay zero from psx_create, and the EXACT flag word was
     // re-armed by the merge that last used it (or psx_create)

@@ -50,6 +50,16 @@ struct SweepStats {           // indexed by causal-set level k
     int exact_reruns;         // levels re-swept with the exact notSharedLL variant
 };
 
+// Record buffer sets of the pipelined asynchronous passes: sweep i reuses the
+// buffers of pass i - kRecBufs, so the host may run kRecBufs - 1 passes ahead of
+// the device before it blocks.  Each set is one plan's records (~90 MB at
+// M = 1000, c = 3).  12 sets (a longer lead against host stalls) measured 3 %
+// slower at world 8 than 3 on the same box (profiles/r02zf_ab_*): 3.
+#ifndef PSX_REC_BUFS
+#define PSX_REC_BUFS 3
+#endif
+constexpr int kRecBufs = PSX_REC_BUFS;
+
 // One decomposition of a level into wave units, with its record CSR.
 struct SweepPlan {
     int k = 0, U = 0, ldg = 0, rank = 0, world = 1, ca = 0;
@@ -58,7 +68,7 @@ struct SweepPlan {
     double alg_bytes = 0, flops = 0;
     int4* d_units = nullptr;     // {a0, a1, B, T}
     Acc5* d_rec = nullptr;       // records in CSR (per-SNP) order
-    Acc5* d_rec_alt[2] = {nullptr, nullptr};  // more record buffers (pipelined asynchronous passes)
+    Acc5* d_rec_alt[kRecBufs - 1] = {};  // more record buffers (pipelined asynchronous passes)
     size_t rec_len = 0;          // records per buffer
     SetRec* d_srec = nullptr;    // [n_units]
     int* d_csr = nullptr;        // ptr[n_rows+1], row_snp[n_rows], pos[n_units * rec_stride]
@@ -91,6 +101,9 @@ struct Sweep3Args {
     unsigned long long* trace = nullptr;  // diagnostics (PSX_UNIT_TRACE): per unit {start, end, hw id, unit}
     int* redo_count = nullptr;            // units redone by the robust variant (cumulative)
 };
+// most a per k = 3 unit (plan_units3c): the fast kernel stages the unit's
+// per-a scalars in LDS
+constexpr int kMaxChunkA3 = 4;
 struct Level2Blocks;  // psx_sweep_dev.h
 int launch_sweep3(bool allpres, const Sweep3Args& A, int n_units, const int4* units, Acc5* rec, SetRec* srec,
                   int rec_stride, int* flag, const int* pos, hipStream_t st, const Level2Blocks* l2, hipEvent_t ev0 = nullptr,
@@ -139,8 +152,8 @@ int sweep_level(SweepPlanCache& cache, int k, int U, int ldg, int rank, int worl
 // k = 3 fast kernel (set records into srec2), else right after it.
 int sweep_prepare(SweepPlanCache& cache, int k, int U, int ldg, int rank, int world, hipStream_t stream,
                   const SweepArgs& a, bool exact, SweepPlan** out);
-// parity selects the record buffer (0: d_rec, 1, 2: d_rec_alt, allocated on
-// first use); flag overrides the cache's EXACT flag word; timed = false skips the
+// parity selects the record buffer (0: d_rec, 1 .. kRecBufs - 1: d_rec_alt,
+// allocated on first use); flag overrides the cache's EXACT flag word; timed = false skips the
 // plan's own timing events (asynchronous passes time the kernel themselves).
 // ev0 / ev1 (optional): start / stop events recorded by the top-level kernel's
 // own dispatch (hipExtLaunchKernel), used by pipelined asynchronous passes.

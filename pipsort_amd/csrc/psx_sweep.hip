@@ -334,7 +334,7 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
         return PSX_K3_ROUNDS * (4.0 * PSX_K3_WAVES * cus);
     }();
     ca = (int)std::lround(total_a / (kTarget * world));
-    ca = std::min(ca, 4);
+    ca = std::min(ca, kMaxChunkA3);
     ca = std::max(1, std::min(64, ca));
     // Every union triple x < y < z belongs to exactly one unit family, by which
     // of its members share a 64-block:
@@ -693,7 +693,7 @@ static void mark_last(SweepPlanCache& C, SweepPlan& P) {
 
 Acc5* plan_records(SweepPlan& P, int parity) {
     if (!parity) return P.d_rec;
-    if (parity < 0 || parity > 2) {
+    if (parity < 0 || parity >= kRecBufs) {
         g_sweep_err = "bad record buffer index";
         return nullptr;
     }
@@ -796,7 +796,9 @@ int sweep_stats_plan(SweepPlan& P, int k, SweepStats* stats) {
 void sweep_free(SweepPlanCache& C) {
     for (auto& kv : C.plans) {
         SweepPlan& P = kv.second;
-        hipFree(P.d_units); hipFree(P.d_rec); hipFree(P.d_rec_alt[0]); hipFree(P.d_rec_alt[1]); hipFree(P.d_srec); hipFree(P.d_csr);
+        hipFree(P.d_units); hipFree(P.d_rec); hipFree(P.d_srec);
+        hipFree(P.d_csr);
+        for (Acc5* r : P.d_rec_alt) hipFree(r);
         for (int i = 0; i < 3; i++) if (P.ev[i]) hipEventDestroy(P.ev[i]);
     }
     C.plans.clear();

@@ -60,6 +60,19 @@ constexpr double kQ2 = kQ1 * kQ1 / 2.0;
 constexpr double kQ3 = kQ2 * kQ1 / 3.0;
 constexpr double kQ4 = kQ3 * kQ1 / 4.0;
 
+// an opaque point in the instruction stream for a loaded value: no use of it can
+// be scheduled before this statement (the wait for the load lands here)
+__device__ __forceinline__ void pin_vgpr(double2& v) {
+    double x = v.x, y = v.y;
+    asm volatile("" : "+v"(x), "+v"(y));
+    v = make_double2(x, y);
+}
+__device__ __forceinline__ void pin_vgpr(int2& v) {
+    int x = v.x, y = v.y;
+    asm volatile("" : "+v"(x), "+v"(y));
+    v = make_int2(x, y);
+}
+
 // lane-local accumulator with a lazy shift: value = 2^m * s
 struct LAcc {
     int m;
@@ -266,7 +279,10 @@ struct Sweep3Smem {
 // factor sF = 2^(Gm - sM) (Gm: the wave's largest a shift)
 struct Sweep3FastSmem {
     double tab[256];
-    double bH[2][64], bR[2][64];
+    double2 bAd[64], bY[64], bMuB[64];  // b-slot constants of the unit (both studies): A_bb, y_b, {b} weight
+    int2 bNB[64];
+    double2 aAd[kMaxChunkA3], aY[kMaxChunkA3];  // the unit's a: A_aa, y_a (both studies), presence
+    unsigned aP[kMaxChunkA3];
     double2 abG[64], abI[64], abIW[64], abH[64], abR[64], abMu[64], abMuB[64];
     int2 abN[64];
     double sF[64];
@@ -663,8 +679,6 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                                                  bool& redo) {
     Sweep3FastSmem& F = sm.f3;
     double (&tab)[256] = F.tab;
-    double (&bH)[2][64] = F.bH;
-    double (&bR)[2][64] = F.bR;
     double (&bW)[64] = F.bW;
     double (&sW0)[64] = F.sW0;  // b slots: W0, W1, W2 (own rho deferred), sharedLL, notSharedLL
     double (&sW1)[64] = F.sW1;
@@ -688,16 +702,24 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     const int tile = C * (C + 1) / 2 + K;
     const double rho = A.rho;
 
-    // ---- unit prologue (as the robust variant) -------------------------------------
+    // ---- unit prologue: every global load of the unit's constants is issued
+    // here, once (the a prologues below then read LDS only) -------------------------
     for (int i = t; i < 256; i += 64) tab[i] = A.tab[i];
     const int vbl = 64 * K + t, ubl = vbl - pad;
     const bool okb = vbl >= pad;
-    const unsigned pbl = okb ? A.pres[ubl] : 0u;
+    const int ib = okb ? ubl : 0;  // clamped index: the loads are unconditional
+    const unsigned pbl = okb ? A.pres[ib] : 0u;
+    double Abb[2], yb[2];
 #pragma unroll
     for (int s = 0; s < 2; s++) {
-        const BTerms b = b_terms<ALLPRES>(A, s, vbl);
-        bH[s][t] = b.H;
-        bR[s][t] = b.R;
+        Abb[s] = okb ? A.Ad[s][ib] : 1.0;
+        yb[s] = okb ? A.ys[s][ib] : 0.0;
+    }
+    if (t < a1 - a0) {  // the unit's a (at most kMaxChunkA3)
+        const int u = a0 + t - pad;
+        F.aAd[t] = make_double2(A.Ad[0][u], A.Ad[1][u]);
+        F.aY[t] = make_double2(A.ys[0][u], A.ys[1][u]);
+        F.aP[t] = A.pres[u];
     }
     bW[t] = memb_weight(pbl);
     sM[t] = EMPTY;
@@ -705,16 +727,17 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
 
     const int vc = 64 * C + t, uc = vc - pad;
     const bool okc = vc >= pad;
-    const unsigned pcm = okc ? A.pres[uc] : 0u;
+    const int ic = okc ? uc : 0;
+    const unsigned pcm = okc ? A.pres[ic] : 0u;
     double Acc[2], yc[2], chic[2], muC[2];
     int nC[2];
 #pragma unroll
     for (int s = 0; s < 2; s++) {
         chic[s] = (okc && (ALLPRES || ((pcm >> s) & 1u))) ? 1.0 : 0.0;
-        Acc[s] = okc ? A.Ad[s][uc] : 1.0;
-        yc[s] = okc ? A.ys[s][uc] : 0.0;
-        muC[s] = okc ? A.muS[s][uc] * chic[s] : 0.0;
-        nC[s] = okc ? A.nS[s][uc] : 0;
+        Acc[s] = okc ? A.Ad[s][ic] : 1.0;
+        yc[s] = okc ? A.ys[s][ic] : 0.0;
+        muC[s] = okc ? A.muS[s][ic] * chic[s] : 0.0;
+        nC[s] = okc ? A.nS[s][ic] : 0;
     }
     const double wc = memb_weight(pcm);
 
@@ -732,37 +755,60 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         sPos[2][t] = (t < a1 - a0) ? pos[rbase + 128 + t] : -1;
 #pragma unroll
         for (int s = 0; s < 2; s++) {
-            g1ab[s][t] = okb ? A.G[s][(size_t)(a0 - pad) * ldg + ubl] : 0.0;
-            g1ac[s][t] = okc ? A.G[s][(size_t)(a0 - pad) * ldg + uc] : 0.0;
+            const double* row = A.G[s] + (size_t)(a0 - pad) * ldg;
+            const double gb = row[ib], gc = row[ic];
+            g1ab[s][t] = okb ? gb : 0.0;
+            g1ac[s][t] = okc ? gc : 0.0;
         }
+    }
+    __syncthreads();  // exp2 table staged
+    {
+        // the {b} weight of every slot: unit-constant (the a prologues rescale it)
+        int nB[2];
+        double muB[2];
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const double chib = (okb && (ALLPRES || ((pbl >> s) & 1u))) ? 1.0 : 0.0;
+            const double r = rsqrt_nr(Abb[s]);
+            split3(yb[s] * yb[s] * r * r, r * A.rsd[s] * chib, tab, nB[s], muB[s]);
+        }
+        F.bAd[t] = make_double2(Abb[0], Abb[1]);
+        F.bY[t] = make_double2(yb[0], yb[1]);
+        F.bMuB[t] = make_double2(muB[0], muB[1]);
+        F.bNB[t] = make_int2(nB[0], nB[1]);
     }
 
     unsigned long long t_ph[4] = {0ull, 0ull, 0ull, 0ull};  // diagnostics: phases of the first a
     if (A.trace) t_ph[0] = wall_clock64();
     for (int ai = 0; ai < a1 - a0; ai++) {
         const int va = a0 + ai, ua = va - pad;
-        const unsigned pa = A.pres[ua];
         double l1[2], D1[2], w1h[2], Ep[2][4];  // Ep: {}, {a}, {c}, {a,c} relative to 2^R
         int R[2];
+        // global loads of this a, all consumed late (no wait in the prologue): the
+        // walk's first tile row, and the next a's Sigma~ row entries, staged into
+        // LDS (this lane's own entries) once this a's prologue is done
         double2 gnx = g01[j0 * 64], mnx = m01[j0 * 64];
         int2 nnx = bnn[j0 * 64];
-        // the next a's Sigma~ row entries, one a ahead: staged into LDS (this
-        // lane's own entries) once this a's prologue is done
         const bool nxt = ai + 1 < a1 - a0;
         double nGab[2], nGac[2];
 #pragma unroll
         for (int s = 0; s < 2; s++) {
-            nGab[s] = (nxt && okb) ? A.G[s][(size_t)(ua + 1) * ldg + ubl] : 0.0;
-            nGac[s] = (nxt && okc) ? A.G[s][(size_t)(ua + 1) * ldg + uc] : 0.0;
+            const double* row = A.G[s] + (size_t)(nxt ? ua + 1 : ua) * ldg;
+            nGab[s] = row[ib];
+            nGac[s] = row[ic];
         }
         __syncthreads();  // previous a's (a, b) terms and slots fully consumed
+        const unsigned pa = F.aP[ai];
+        const double2 aAd = F.aAd[ai], aY = F.aY[ai];
+        const double2 bAd = F.bAd[t], bY = F.bY[t], bMuB = F.bMuB[t];
+        const int2 bNB = F.bNB[t];
         double pG[2], pI[2], pIW[2], pH[2], pR[2], pMu[2], pMuB[2];
         int pN[2];
 #pragma unroll
         for (int s = 0; s < 2; s++) {
             const double chia = (ALLPRES || ((pa >> s) & 1u)) ? 1.0 : 0.0;
-            const double ya = A.ys[s][ua];
-            const double ra = rsqrt_nr(A.Ad[s][ua]);
+            const double ya = s ? aY.y : aY.x;
+            const double ra = rsqrt_nr(s ? aAd.y : aAd.x);
             const double iAaa = ra * ra;
             const double ha = ya * ya * iAaa;
             const double rPa = ra * A.rsd[s] * chia;
@@ -771,19 +817,18 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             split3(ha, rPa, tab, nA, muA);
             {
                 const double Gab = g1ab[s][t];
-                const double Abb = okb ? A.Ad[s][ubl] : 1.0;
-                const double yb = okb ? A.ys[s][ubl] : 0.0;
                 const double l = Gab * iAaa;
-                const double Dab = fma(-l, Gab, Abb);
+                const double Dab = fma(-l, Gab, s ? bAd.y : bAd.x);
                 const double rab = rsqrt_nr(Dab);
-                const double wab = fma(-l, ya, yb);
+                const double wab = fma(-l, ya, s ? bY.y : bY.x);
                 const double hab = fma(wab * wab, rab * rab, ha);
                 const bool chib = okb && (ALLPRES || ((pbl >> s) & 1u));
                 const double rPab = chib ? rPa * rab * A.rsd[s] : 0.0;
-                int nAB, nB;
-                double muAB, muB;
+                int nAB;
+                double muAB;
                 split3(hab, rPab, tab, nAB, muAB);
-                split3(bH[s][t], bR[s][t] * (2.0 / A.rsd[s]), tab, nB, muB);
+                const int nB = s ? bNB.y : bNB.x;
+                const double muB = s ? bMuB.y : bMuB.x;
                 pG[s] = Gab;
                 pI[s] = rab * rab;
                 pIW[s] = rab * rab * (0.5 * wab);  // I_ab w_ab / 2 (the pivot itself is not needed)
@@ -885,8 +930,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         if (nxt) {
 #pragma unroll
             for (int s = 0; s < 2; s++) {
-                g1ab[s][t] = nGab[s];
-                g1ac[s][t] = nGac[s];
+                g1ab[s][t] = okb ? nGab[s] : 0.0;
+                g1ac[s][t] = okc ? nGac[s] : 0.0;
             }
         }
         if (A.trace && ai == 0) t_ph[1] = wall_clock64();
@@ -1002,9 +1047,9 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             chain(j0, gnx, NA, qA);
             for (int j = j0; j < je; j += 2) {
                 const int o = j * 64 + t;
-                const double2 m_nxt = mb[o + 64];
-                const int2 n_nxt = nb[o + 64];
-                const double2 g_after = gb[o + 128];
+                double2 m_nxt = mb[o + 64];
+                int2 n_nxt = nb[o + 64];
+                double2 g_after = gb[o + 128];
                 chain(j + 1, g_next, NB, qB);
                 finish(j, NA, qA, m_cur, n_cur);
                 // b-slot ownership rotates across lanes every step: the workgroup is
@@ -1013,9 +1058,20 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 m_cur = mb[o + 128];
                 n_cur = nb[o + 128];
                 g_next = gb[o + 192];
+                // the row loads at the top of this pair of steps are first used here
+                // (and this half's loads first in the next pair): pinned, so the
+                // scheduler cannot hoist a use to where it would wait for a load
+                // issued only ~80 instructions earlier (the tile rows come from the
+                // MALL).  Same-box A/B: world 1 1.043 -> 1.016 ms.
+                pin_vgpr(m_nxt);
+                pin_vgpr(n_nxt);
+                pin_vgpr(g_after);
                 chain(j + 2, g_after, NA, qA);  // (the last pair's is not used)
                 finish(j + 1, NB, qB, m_nxt, n_nxt);
                 __builtin_amdgcn_wave_barrier();
+                pin_vgpr(m_cur);
+                pin_vgpr(n_cur);
+                pin_vgpr(g_next);
             }
             if (je < j1) {
                 gnx = g01[je * 64];

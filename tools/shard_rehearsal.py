@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--workload", default="syn1000c3")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--reverse", action="store_true", help="run the ranks' shards in reverse order")
+    ap.add_argument("--sync", action="store_true", help="synchronous passes (merge not overlapped with the next sweep)")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     seam = bench.build_inputs(args.workload)
@@ -41,11 +43,14 @@ def main():
         mine = torch.empty(nb, dtype=torch.uint8, device="cuda")
         gathered = torch.empty(nb * world, dtype=torch.uint8, device="cuda")
         ranks = []
-        for rank in range(world):
+        for rank in (range(world - 1, -1, -1) if args.reverse else range(world)):
             pc.set_shard(rank, world)
 
             def step():
-                pc.run_exhaustive_async()
+                if args.sync:
+                    pc.run_exhaustive()
+                else:
+                    pc.run_exhaustive_async()
                 if world > 1:
                     pc.export_partials(mine.data_ptr())
                     # one copy kernel stands in for the RCCL all-gather
@@ -65,6 +70,7 @@ def main():
             t = pc.timing()
             ranks.append({"rank": rank, "step_ms": dt, "kernel_ms": t["kernel_ms"] / max(t["kernel_launches"], 1),
                           "sweep_ms": t["sweep_ms"]})
+        ranks.sort(key=lambda r: r["rank"])
         worst = max(r["step_ms"] for r in ranks)
         out["worlds"][world] = {"max_step_ms": worst, "ranks": ranks}
         print(f"world {world}: max step {worst:.3f} ms; kernel ms per rank "
