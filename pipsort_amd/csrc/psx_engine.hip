@@ -2197,6 +2197,25 @@ int psx_shard_stats(const psx_problem* p, int32_t k, int32_t rank, int32_t world
     return 0;
 }
 
+int psx_plan_units_k3(int32_t n_union, int32_t rank, int32_t world, int32_t* units, int32_t cap) {
+    if (n_union < 3 || world < 1 || rank < 0 || rank >= world || cap < 0) return fail(PSX_EINVAL, "bad arguments");
+    const int U = n_union, ldg = (U + 63) / 64 * 64;
+    std::vector<unsigned char> pres(ldg, 3);
+    std::vector<psx::PlanUnit> mine;
+    int ca = 0;
+    double sets = 0, cfg = 0, bytes = 0;
+    psx::plan_units3c(U, ldg, rank, world, pres.data(), mine, ca, sets, cfg, bytes);
+    for (int i = 0; i < (int)mine.size() && i < cap; i++) {
+        const psx::PlanUnit& u = mine[i];
+        int32_t* o = units + 4 * (size_t)i;
+        o[0] = u.a0;
+        o[1] = u.a1;
+        o[2] = u.B | (u.j0 << 16);
+        o[3] = u.T | (u.j1 << 16);
+    }
+    return (int)mine.size();
+}
+
 int psx_get_timing(psx_engine* e, psx_timing* t) {
     *t = e->timing;
     return 0;

@@ -33,7 +33,7 @@ EXPORTED = [
     "psx_set_shard", "psx_run_exhaustive", "psx_run_configs", "psx_run_sss",
     "psx_eval_union_batch", "psx_reset", "psx_get_accum", "psx_partials_bytes",
     "psx_export_partials", "psx_merge_partials", "psx_get_timing", "psx_count_configs",
-    "psx_fold_partials_host", "psx_shard_stats", "psx_set_stream",
+    "psx_fold_partials_host", "psx_shard_stats", "psx_plan_units_k3", "psx_set_stream",
     "psx_psd_shift", "psx_lowrank_study", "psx_sym_eigen", "psx_lu_det",
     "psx_create_from_ld", "psx_psd_shift_gpu", "psx_lu_det_gpu",
     "psx_run_exhaustive_async", "psx_sync", "psx_run_sss_sharded",
@@ -167,6 +167,7 @@ def load_library(path: str = LIB_PATH):
         "psx_fold_partials_host": (c_int, [vp, c_i32, c_i64, vp]),
         "psx_set_stream": (c_int, [vp, vp]),
         "psx_shard_stats": (c_int, [P(_Problem), c_i32, c_i32, c_i32, P(c_u64), P(dbl)]),
+        "psx_plan_units_k3": (c_int, [c_i32, c_i32, c_i32, P(c_i32), c_i32]),
         "psx_psd_shift": (c_int, [P(dbl), c_i32, P(dbl)]),
         "psx_lowrank_study": (c_int, [P(dbl), P(dbl), c_i32, P(dbl), P(dbl)]),
         "psx_sym_eigen": (c_int, [P(dbl), c_i32, P(dbl), P(dbl)]),
@@ -420,6 +421,17 @@ def fold_partials_host(images: np.ndarray) -> np.ndarray:
     _check(load_library().psx_fold_partials_host(imgs.ctypes.data_as(ctypes.c_void_p), imgs.shape[0],
                                                  imgs.shape[1], out.ctypes.data_as(ctypes.c_void_p)))
     return out
+
+
+def plan_units_k3(n_union: int, rank: int = 0, world: int = 1) -> np.ndarray:
+    """The k = 3 fast sweep's work units of one shard (host-only diagnostics):
+    int32 [n, 4] rows {a0, a1, K | j0 << 16, C | j1 << 16} in dispatch order."""
+    lib = load_library()
+    n = lib.psx_plan_units_k3(n_union, rank, world, None, 0)
+    _check(min(n, 0))
+    out = np.zeros((max(n, 1), 4), dtype=np.int32)
+    _check(min(lib.psx_plan_units_k3(n_union, rank, world, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n), 0))
+    return out[:n]
 
 
 # partial image record layout (psx_math.h Acc5 / SetRec)

@@ -151,3 +151,35 @@ def test_host_lu_det_matches_numpy_and_underflows_like_gsl():
     # index-order product of U_ii = 0.64 sticks at the smallest subnormal; 0.19 flushes to 0
     assert E.lu_det(0.6 ** np.abs(idx[:, None] - idx[None, :])) == 5e-324
     assert E.lu_det(0.9 ** np.abs(idx[:, None] - idx[None, :])) == 0.0
+
+
+@pytest.mark.parametrize("U", [3, 65, 300, 1000])
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_k3_units_cover_every_walk_step_once(U, world):
+    """The k = 3 work units of all shards (after the tail refinement cuts the
+    last dispatch round into single-a units and b-walk halves) cover every
+    (a, tile, b-walk step) of the block-pattern decomposition exactly once."""
+    ldg = (U + 63) // 64 * 64
+    pad = ldg - U
+    seen = {}
+    n_units = 0
+    for r in range(world):
+        units = E.plan_units_k3(U, r, world)
+        n_units += len(units)
+        for a0, a1, z, w in units:
+            K, C, j0, j1 = z & 0xFFFF, w & 0xFFFF, z >> 16, w >> 16
+            assert K <= C and pad <= a0 < a1 and j0 < j1 <= 64
+            if K == C:  # folded diagonal walk: half steps, even bounds
+                assert j0 % 2 == 0 and j1 % 2 == 0
+            for a in range(a0, a1):
+                seen.setdefault((a, K, C), []).append((j0, j1))
+    nblk = ldg // 64
+    want = {(a, K, C) for C in range(nblk) if 64 * C + 64 > pad for K in range(C + 1)
+            for a in range(pad, 64 * K if K < C else ldg)}
+    assert set(seen) == want
+    for key, ranges in seen.items():
+        ranges.sort()
+        assert ranges[0][0] == 0 and ranges[-1][1] == 64, (key, ranges)
+        for (x0, x1), (y0, y1) in zip(ranges, ranges[1:]):
+            assert x1 == y0, (key, ranges)
+    assert n_units >= 1

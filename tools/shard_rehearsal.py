@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--reverse", action="store_true", help="run the ranks' shards in reverse order")
     ap.add_argument("--sync", action="store_true", help="synchronous passes (merge not overlapped with the next sweep)")
+    ap.add_argument("--no-exchange", action="store_true", help="world > 1 without the export / all-gather / merge")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     seam = bench.build_inputs(args.workload)
@@ -51,7 +52,7 @@ def main():
                     pc.run_exhaustive()
                 else:
                     pc.run_exhaustive_async()
-                if world > 1:
+                if world > 1 and not args.no_exchange:
                     pc.export_partials(mine.data_ptr())
                     # one copy kernel stands in for the RCCL all-gather
                     gathered.view(world, nb).copy_(mine.view(1, nb).expand(world, nb))
