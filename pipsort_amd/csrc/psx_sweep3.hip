@@ -992,19 +992,20 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             const double WB1 = dot4(v[1], uW[0], 0.0);
             const double NB = dot4(v[0], uL[1], dot4(v[1], uL[0], 0.0));
             // ---- b in both studies: the 9 assignments of (a, c); their sums for a and c ----
-            double z[3][3];
 #pragma unroll
             for (int xa = 0; xa < 3; xa++)
 #pragma unroll
                 for (int xc = 0; xc < 3; xc++) {
                     const int i0 = (xa != 1) | ((xc != 1) << 1), i1 = (xa != 0) | ((xc != 0) << 1);
-                    z[xa][xc] = v[0][i0] * v[1][i1];
-                    ZS[xa][xc] += z[xa][xc];
+                    ZS[xa][xc] = fma(v[0][i0], v[1][i1], ZS[xa][xc]);
                 }
-            const double Z0 = (z[0][0] + z[0][1]) + (z[1][0] + z[1][1]);  // neither a nor c shared
-            const double Z1 = (z[2][0] + z[2][1]) + (z[0][2] + z[1][2]);  // one of them shared
-            const double WB2 = fma(rho, fma(rho, z[2][2], Z1), Z0);
-            const double LB2 = (Z0 + Z1) + z[2][2];
+            // Z0: (xa, xc) in {0,1}^2 -> (i0, i1) = (3,0), (1,2), (2,1), (0,3)
+            const double Z0 = fma(v[0][0], v[1][3], fma(v[0][2], v[1][1], fma(v[0][1], v[1][2], v[0][3] * v[1][0])));
+            // Z1: one of a, c in both studies -> (3,1), (1,3), (3,2), (2,3)
+            const double Z1 = fma(v[0][2], v[1][3], fma(v[0][3], v[1][2], fma(v[0][1], v[1][3], v[0][3] * v[1][1])));
+            const double z22 = v[0][3] * v[1][3];
+            const double WB2 = fma(rho, fma(rho, z22, Z1), Z0);
+            const double LB2 = (Z0 + Z1) + z22;
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 V0[i] += v[0][i];
