@@ -442,6 +442,12 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
         return -1;
     }
     P.ca = ca;
+    if (variant)  // the fast kernel stages a unit's a scalars in LDS arrays of kMaxChunkA3
+        for (const PlanUnit& u : mine)
+            if (u.a1 - u.a0 > kMaxChunkA3 || u.a1 <= u.a0) {
+                g_sweep_err = "k = 3 unit a-range outside 1.." + std::to_string(kMaxChunkA3);
+                return -1;
+            }
     P.rec_stride = (k == 3) ? 128 + ca : 128;
     P.n_units = (int)mine.size();
     P.union_sets = (uint64_t)sets;
