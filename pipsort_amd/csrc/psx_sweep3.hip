@@ -49,6 +49,7 @@
 // device-library wave reductions (DPP, result in every lane)
 extern "C" __device__ __attribute__((const)) int __ockl_wfred_max_i32(int);
 extern "C" __device__ __attribute__((const)) double __ockl_wfred_add_f64(double);
+extern "C" __device__ __attribute__((const)) double __ockl_wfred_min_f64(double);
 
 namespace psx {
 
@@ -71,6 +72,24 @@ __device__ __forceinline__ void pin_vgpr(int2& v) {
     int x = v.x, y = v.y;
     asm volatile("" : "+v"(x), "+v"(y));
     v = make_int2(x, y);
+}
+
+// A unit's set record across the wave by DPP reductions: each (shift, sum) pair
+// is taken at the wave's largest shift among lanes holding a value (empty lanes
+// carry EMPTY), then summed; a term more than ~1074 bits below that shift
+// vanishes, as in the pairwise fold it replaces.  The result is in every lane.
+__device__ __forceinline__ void wave_pair_dpp(int& m, double& s) {
+    const int M = __ockl_wfred_max_i32(s != 0.0 ? m : EMPTY);
+    const double S = __ockl_wfred_add_f64(s != 0.0 ? ldexp(s, m - M) : 0.0);
+    m = S != 0.0 ? M : EMPTY;
+    s = S;
+}
+__device__ __forceinline__ void wave_fold_set_dpp(SetRec& r) {
+    wave_pair_dpp(r.m, r.tot);
+    wave_pair_dpp(r.m0, r.nc0);
+    wave_pair_dpp(r.m1, r.nc1);
+    r.score = __ockl_wfred_min_f64(r.score);
+    r.npat = __ockl_wfred_add_f64(r.npat);
 }
 
 // lane-local accumulator with a lazy shift: value = 2^m * s
@@ -1174,7 +1193,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     sr.pad = 0;
     sr.score = 1e300;
     sr.npat = npat;
-    wave_fold_set(sr);
+    wave_fold_set_dpp(sr);
     if (t == 0) store_rec(srec + unit, sr);
     redo = __builtin_amdgcn_ballot_w64(dmax > kMaxRefGap) != 0;
     if (A.trace && t == 0) {
