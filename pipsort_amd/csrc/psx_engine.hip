@@ -423,8 +423,9 @@ __device__ void eval_single(const DevProb& P, int u, Acc5& a, SetRec& r) {
 // Fixed fold order: deterministic.
 constexpr int kMergeThreads = 64;
 __global__ __launch_bounds__(kMergeThreads) void k_merge_pass_l1(DevProb P, int lo, int hi, const Acc5* __restrict__ recA,
-                                                       const int* __restrict__ dptrA, const Acc5* __restrict__ recB,
-                                                       const int* __restrict__ dptrB, const SetRec* __restrict__ srec,
+                                                       const int* __restrict__ dptrA, const int* __restrict__ gidxA,
+                                                       const Acc5* __restrict__ recB, const int* __restrict__ dptrB,
+                                                       const int* __restrict__ gidxB, const SetRec* __restrict__ srec,
                                                        long nsrec, SetRec extra, Acc5* __restrict__ acc,
                                                        SetRec* __restrict__ sacc, int* __restrict__ flag,
                                                        int* __restrict__ sticky) {
@@ -474,12 +475,13 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_pass_l1(DevProb P, int 
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const int j = i + q * T;
-            x[q] = j < na ? recA[a0 + j] : recB[b0 + j - na];
+            x[q] = j < na ? recA[gidxA ? gidxA[a0 + j] : a0 + j] : recB[gidxB ? gidxB[b0 + j - na] : b0 + j - na];
         }
 #pragma unroll
         for (int q = 0; q < 4; q++) psx::fold_acc(a, x[q]);
     }
-    for (; i < n; i += T) psx::fold_acc(a, i < na ? recA[a0 + i] : recB[b0 + i - na]);
+    for (; i < n; i += T)
+        psx::fold_acc(a, i < na ? recA[gidxA ? gidxA[a0 + i] : a0 + i] : recB[gidxB ? gidxB[b0 + i - na] : b0 + i - na]);
     psx::wave_fold_acc(a);
     if (tid == 0) {
         Acc5 g = {0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -1078,7 +1080,8 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     psx::SweepPlan* mA = low ? low : top;
     psx::SweepPlan* mB = low ? top : nullptr;
     hipLaunchKernelGGL(k_merge_pass_l1, dim3(e->U + 1), dim3(kMergeThreads), 0, X, e->dp, lo, hi, psx::plan_records(*mA, par),
-                       mA->d_dptr, mB ? psx::plan_records(*mB, par) : nullptr, mB ? mB->d_dptr : nullptr, dpass,
+                       mA->d_dptr, mA->d_gidx, mB ? psx::plan_records(*mB, par) : nullptr, mB ? mB->d_dptr : nullptr,
+                       mB ? mB->d_gidx : nullptr, dpass,
                        (long)(nl + nt), extra, e->dacc, e->dsacc, pflag, e->dflag + 1);
     HIPCHK(hipGetLastError());
     if (async) {

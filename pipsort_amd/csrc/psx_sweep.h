@@ -67,13 +67,14 @@ struct SweepPlan {
     uint64_t union_sets = 0;
     double alg_bytes = 0, flops = 0;
     int4* d_units = nullptr;     // {a0, a1, B, T}
-    Acc5* d_rec = nullptr;       // records in CSR (per-SNP) order
+    Acc5* d_rec = nullptr;       // records, unit-major: slot i of unit u at u * rec_stride + i
     Acc5* d_rec_alt[kRecBufs - 1] = {};  // more record buffers (pipelined asynchronous passes)
     size_t rec_len = 0;          // records per buffer
     SetRec* d_srec = nullptr;    // [n_units]
-    int* d_csr = nullptr;        // ptr[n_rows+1], row_snp[n_rows], pos[n_units * rec_stride]
-    const int* d_pos = nullptr;  // record slot -> CSR position (inside d_csr)
-    const int* d_dptr = nullptr; // [U+1] dense per-SNP record runs (inside d_csr)
+    int* d_csr = nullptr;        // ptr[n_rows+1], row_snp[n_rows], pos[n_units * rec_stride], dptr[U+1], gidx
+    const int* d_pos = nullptr;  // record slot -> buffer position, -1: no SNP (inside d_csr)
+    const int* d_dptr = nullptr; // [U+1] per-SNP runs of CSR positions (inside d_csr)
+    const int* d_gidx = nullptr; // CSR position -> record slot (records are unit-major; the merges gather)
     int csr_ptr_len = 0, csr_idx_len = 0;
     int variant = 0;             // 1: the k = 3 fast kernel's decomposition
     double fused_bytes = 0, fused_flops = 0;  // in-launch level-2 work of the last launch

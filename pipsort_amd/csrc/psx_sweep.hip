@@ -118,14 +118,16 @@ __global__ __launch_bounds__(256) void k_merge_members(const Acc5* __restrict__ 
     }
 }
 
-// Records written in CSR order (psx_sweep plans): row r's records are the
-// contiguous run [ptr[r], ptr[r+1]); 256 threads fold it in a fixed order.
+// Row r's records are CSR positions [ptr[r], ptr[r+1]), each gathered from
+// record slot gidx[q] (unit-major record buffers; null: the position itself);
+// 256 threads fold them in a fixed order.
 __global__ __launch_bounds__(256) void k_merge_rows(const Acc5* __restrict__ rec, const int* __restrict__ ptr,
-                                                   const int* __restrict__ row_snp, Acc5* __restrict__ acc) {
+                                                   const int* __restrict__ row_snp, const int* __restrict__ gidx,
+                                                   Acc5* __restrict__ acc) {
     __shared__ Acc5 sh[4];
     const int row = blockIdx.x;
     Acc5 a = acc_zero();
-    for (int i = ptr[row] + (int)threadIdx.x; i < ptr[row + 1]; i += 256) fold_acc(a, rec[i]);
+    for (int i = ptr[row] + (int)threadIdx.x; i < ptr[row + 1]; i += 256) fold_acc(a, rec[gidx ? gidx[i] : i]);
     wave_fold_acc(a);
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = a;
     __syncthreads();
@@ -497,9 +499,13 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     P.n_rows = (int)rows.size();
     P.csr_ptr_len = (int)ptr.size();
     P.csr_idx_len = (int)idx.size();
-    // kernels write record slot i straight to its CSR position pos[i] (-1: no SNP)
+    // Records are unit-major: the kernels write record slot i at position i
+    // (pos[i] = -1: no SNP), so a unit's 64 c (b) records are contiguous and the
+    // stores coalesce; the merges gather each SNP's records through idx, in
+    // record order (same fold order as a per-SNP layout; same-box A/B against
+    // writing each record at its CSR position: world 1 -0.4 %, world 8 -1 %)
     std::vector<int> pos(key.size(), -1);
-    for (size_t q = 0; q < idx.size(); q++) pos[idx[q]] = (int)q;
+    for (size_t i = 0; i < key.size(); i++) pos[i] = key[i] >= 0 ? (int)i : -1;
     // dense per-SNP pointers (rows are in increasing SNP order): SNP u's run is
     // [dptr[u], dptr[u+1]), empty when u has no record
     std::vector<int> dptr(U + 1, 0);
@@ -512,13 +518,15 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     packed.insert(packed.end(), rows.begin(), rows.end());
     packed.insert(packed.end(), pos.begin(), pos.end());
     packed.insert(packed.end(), dptr.begin(), dptr.end());
-    P.rec_len = idx.size();
-    if (!idx.empty()) SWCHK(hipMalloc(&P.d_rec, sizeof(Acc5) * idx.size()));
+    packed.insert(packed.end(), idx.begin(), idx.end());
+    P.rec_len = key.size();
+    if (P.rec_len) SWCHK(hipMalloc(&P.d_rec, sizeof(Acc5) * P.rec_len));
     if (!packed.empty()) {
         SWCHK(hipMalloc(&P.d_csr, sizeof(int) * packed.size()));
         SWCHK(hipMemcpy(P.d_csr, packed.data(), sizeof(int) * packed.size(), hipMemcpyHostToDevice));
         P.d_pos = P.d_csr + ptr.size() + rows.size();
         P.d_dptr = P.d_pos + pos.size();
+        P.d_gidx = P.d_dptr + dptr.size();
     }
     return 0;
 }
@@ -663,7 +671,7 @@ int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, h
     if (P.n_units == 0) return 0;
     if (P.n_rows > 0) {
         hipLaunchKernelGGL(k_merge_rows, dim3(P.n_rows), dim3(256), 0, st, P.d_rec, P.d_csr,
-                           P.d_csr + P.csr_ptr_len, acc);
+                           P.d_csr + P.csr_ptr_len, P.d_gidx, acc);
         SWCHK(hipGetLastError());
     }
     SetRec none = set_zero();

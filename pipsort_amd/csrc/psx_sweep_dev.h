@@ -144,7 +144,7 @@ __device__ __forceinline__ void store_rec(T* dst, const T& v) {
     *dst = v;
 }
 
-// record slot i goes to its CSR position pos[i] (merges then read contiguous runs)
+// record slot i goes to buffer position pos[i] (-1: no SNP; the merges gather by SNP)
 __device__ __forceinline__ void put_rec(Acc5* rec, const int* pos, size_t i, const Acc5& v) {
     const int q = pos[i];
     if (q >= 0) store_rec(rec + q, v);
