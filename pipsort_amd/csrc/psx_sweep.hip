@@ -478,11 +478,14 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     for (int i = 0; i < P.n_units; i++) {
         const PlanUnit& u = mine[i];
         int* kk = key.data() + (size_t)i * P.rec_stride;
+        // the k = 3 fast kernel writes a diagonal tile's c and b-slot records of one
+        // SNP as one (c) record
+        const bool one = variant && k == 3 && u.B == u.T;
         for (int t = 0; t < 64; t++) {
             int c = 64 * u.T + t - pad;
             if (c >= 0 && c < U) kk[t] = c;
             int b = 64 * u.B + t - pad;
-            if (b >= 0 && b < U) kk[64 + t] = b;
+            if (!one && b >= 0 && b < U) kk[64 + t] = b;
         }
         if (k == 3)
             for (int a = u.a0; a < u.a1; a++) kk[128 + (a - u.a0)] = a - pad;

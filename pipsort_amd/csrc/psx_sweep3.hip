@@ -646,7 +646,6 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
         if (t == 0 && qa >= 0) store_rec(rec + qa, ra);
     }
     __syncthreads();
-    if (sPos[0][t] >= 0) store_rec(rec + sPos[0][t], lacc_rec(accC, A.Ck, A.pit0));
     {
         LAcc sl;
         sl.m = sM[t];
@@ -655,7 +654,11 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
         sl.sh = sSh[t];
         sl.sl = sSl[t];
         sl.ns = sNs[t];
-        if (sPos[1][t] >= 0) store_rec(rec + sPos[1][t], lacc_rec(sl, A.Ck, A.pit0));
+        Acc5 rc = lacc_rec(accC, A.Ck, A.pit0);
+        const Acc5 rb = lacc_rec(sl, A.Ck, A.pit0);
+        if (diag) fold_acc(rc, rb);  // one SNP: c = b slot t (the plan keys one record)
+        if (sPos[0][t] >= 0) store_rec(rec + sPos[0][t], rc);
+        if (!diag && sPos[1][t] >= 0) store_rec(rec + sPos[1][t], rb);
     }
     SetRec sr;
     sr.tot = totC * A.pit0;
@@ -1180,9 +1183,15 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         if (A.trace && ai == 0) t_ph[3] = wall_clock64();
     }
     __syncthreads();
-    if (sPos[0][t] >= 0) store_rec(rec + sPos[0][t], wrec(mC, cW0, cW1, cW2, cSl, cNs, rho, A.Ck, A.pit0));
-    if (sPos[1][t] >= 0)
-        store_rec(rec + sPos[1][t], wrec(sM[t], sW0[t], sW1[t], sW2[t], sSl[t], sNs[t], rho, A.Ck, A.pit0));
+    {
+        // a diagonal tile's lane t and b slot t are one SNP: one record (the plan
+        // keys no b records there), folded here instead of in the merge
+        Acc5 rc = wrec(mC, cW0, cW1, cW2, cSl, cNs, rho, A.Ck, A.pit0);
+        const Acc5 rb = wrec(sM[t], sW0[t], sW1[t], sW2[t], sSl[t], sNs[t], rho, A.Ck, A.pit0);
+        if (diag) fold_acc(rc, rb);
+        if (sPos[0][t] >= 0) store_rec(rec + sPos[0][t], rc);
+        if (!diag && sPos[1][t] >= 0) store_rec(rec + sPos[1][t], rb);
+    }
     SetRec sr;
     sr.tot = ((cW0 + cW1) + rho * cW2) * A.pit0;  // every assignment of the lane's sets
     sr.m = (sr.tot != 0.0) ? mC + A.Ck : EMPTY;
