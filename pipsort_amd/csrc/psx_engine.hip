@@ -333,6 +333,85 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
     }
 }
 
+// Configs rows (psx_run_configs, postcal.cpp:400-714): every row is one union
+// set with ONE forced assignment (c0, c1), so a lane per row factors just the
+// two forced subsets (psx::ldlt_terms: the same eliminations k_eval_sets runs
+// with the other members zeroed out) instead of a wave per row factoring all
+// 2^k subsets.  Same records as k_eval_sets with the forced filter: the values
+// are equal, the shifts are taken at the assignment's own exponent np (where
+// k_eval_sets uses the full-set exponents) — the same (shift, sum) numbers.
+__global__ __launch_bounds__(64) void k_eval_rows(DevProb P, const int* __restrict__ sets, int stride,
+                                                  const int* __restrict__ forced, long nsets,
+                                                  SetRec* __restrict__ srec, Acc5* __restrict__ mrec) {
+    constexpr int KM = PSX_KMAX;
+    const long set = (long)blockIdx.x * 64 + threadIdx.x;
+    if (set >= nsets) return;
+    const int* S = sets + (size_t)set * stride;
+    int mem[KM];
+    int k = 0;
+    for (int j = 0; j < stride && j < KM; j++)
+        if (S[j] >= 0) mem[k++] = S[j];
+    int S0 = 0, S1 = 0;
+    for (int j = 0; j < k; j++) {
+        const unsigned pr = P.pres[mem[j]];
+        if (pr & 1u) S0 |= 1 << j;
+        if (pr & 2u) S1 |= 1 << j;
+    }
+    const int c0 = forced[2 * set], c1 = forced[2 * set + 1];
+    const int Ck = P.Ck[k];
+    SetRec rr = psx::set_zero();
+    Acc5 a = psx::acc_zero();
+    double wll = 0.0, w = 0.0;
+    int G = 0;
+    // the forced assignment is one of k_eval_sets' 3^k (every member in a study
+    // where it is present) or the row adds nothing
+    const bool valid = k > 0 && ((c0 | c1) == (1 << k) - 1) && !(c0 & ~S0) && !(c1 & ~S1);
+    if (valid) {
+        double mu[2], f[2];
+        int n[2];
+        for (int s = 0; s < 2; s++) {
+            const int cs = s ? c1 : c0;
+            int idx[KM];
+            int t = 0;
+            for (int j = 0; j < k; j++)
+                if ((cs >> j) & 1) idx[t++] = mem[j];
+            double q, Pd;
+            psx::ldlt_terms(P.G[s], P.ldg, P.Ad[s], P.y[s], P.dval[s], idx, t, q, Pd);
+            psx::split_exp(0.5 * q * PSX_LOG2E, 1.0 / sqrt(Pd), n[s], mu[s]);
+            f[s] = 0.5 * q - 0.5 * log(Pd);
+        }
+        const int nsh = __popc(c0 & c1);
+        const double mup = mu[0] * mu[1];
+        const int np = n[0] + n[1];
+        G = np + 2;  // k_eval_sets' "+ 2" headroom, at this assignment's exponent
+        wll = ldexp(mup, -2);
+        w = wll * P.pit[k][nsh];
+        rr.m = G + Ck;
+        rr.tot = w;
+        rr.m0 = rr.m1 = np + Ck;
+        rr.nc0 = c0 == 0 ? mup * P.pit[k][0] : 0.0;
+        rr.nc1 = c1 == 0 ? mup * P.pit[k][0] : 0.0;
+        rr.score = f[0] + f[1] + P.prior[k][nsh];
+        rr.npat = 1.0;
+        a.mP = G + Ck;
+        a.mS = G;
+        a.mN = G;
+    }
+    srec[set] = rr;
+    for (int j = 0; j < k; j++) {
+        Acc5 r = a;
+        if (valid) {
+            const int x = ((c0 >> j) & 1) | (((c1 >> j) & 1) << 1);
+            r.post0 = (x & 1) ? w : 0.0;
+            r.post1 = (x & 2) ? w : 0.0;
+            r.shared = x == 3 ? w : 0.0;
+            r.sll = x == 3 ? wll : 0.0;
+            r.nsll = x == 3 ? 0.0 : wll;  // notSharedLL: 2^{np - (np + 2)} mup
+        }
+        mrec[(size_t)set * stride + j] = r;
+    }
+}
+
 // merge `count` concatenated partial images (rank order) into acc / sacc.
 // Image layout: Acc5[ldg] followed by one Acc5-sized slot holding the SetRec.
 __global__ void k_merge_partials(const Acc5* __restrict__ parts, int U, int ldg, int count, Acc5* __restrict__ acc,
@@ -707,8 +786,12 @@ int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool has_forced
     const int* dforced = has_forced ? e->dgen + n_sets : nullptr;
     const int* dcsr = e->dgen + n_sets + n_forced;
     if (kernel_ms) HIPCHK(hipEventRecord(e->ev[2], e->stream));
-    hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)nsets), dim3(64), 0, e->stream, e->dp, dsets, stride, dforced,
-                       e->dsrec, e->dmrec, scores ? e->dscore : nullptr);
+    if (has_forced && !scores)  // configs rows: one forced assignment per set, a lane per set
+        hipLaunchKernelGGL(k_eval_rows, dim3((unsigned)((nsets + 63) / 64)), dim3(64), 0, e->stream, e->dp, dsets,
+                           stride, dforced, (long)nsets, e->dsrec, e->dmrec);
+    else
+        hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)nsets), dim3(64), 0, e->stream, e->dp, dsets, stride, dforced,
+                           e->dsrec, e->dmrec, scores ? e->dscore : nullptr);
     HIPCHK(hipGetLastError());
     if (kernel_ms) HIPCHK(hipEventRecord(e->ev[3], e->stream));
     if (accumulate) {
