@@ -40,7 +40,42 @@ from pipsort_amd import synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (spec)
-VALU_ISSUE_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12  # 1024 SIMDs x 16 lanes x 2.4 GHz (one wave64 op / 4 cycles)
+SIMDS = 256 * 4
+CLOCK_HZ = 2.4e9          # peak engine clock (spec)
+# SIMD cycles per wave64 VALU instruction on gfx950, measured by tools/valu_lat.hip
+# with 4 waves per SIMD, 8 independent chains each (profiles/r03a_valu_issue.txt):
+# FP64 FMA / MUL / ADD and v_ldexp_f64 4.2 (the 16-lane FP64 pipe), v_rsq_f64
+# 16.15, 32-bit integer / f32 ops 2.28 (the 32-lane pipe: half the FP64 cost)
+VALU_CYCLES = {"fp64": 4.20, "fp64_trans": 16.15, "int32": 2.28, "other": 4.20}
+
+
+def valu_issue_roof(pmc, kernel_s, world):
+    """VALU issue roof of the dominant kernel with measured cycle weights per
+    instruction class (PMC counts of the same build): FP64 FMA / MUL / ADD and
+    FP64 transcendentals from their own counters, 32-bit integer ops from
+    SQ_INSTS_VALU_INT32, the rest of SQ_INSTS_VALU (v_ldexp_f64, 64-bit moves /
+    shifts / compares, DPP moves) at the FP64 rate (v_ldexp_f64 measured 4.2).
+    Achieved = SIMD cycles the launch's instructions need / (1024 SIMDs x launch
+    time); frac against the 2.4 GHz peak clock, and at the clock the chip held
+    during the PMC run (GRBM_GUI_ACTIVE / 8 per launch time)."""
+    c = pmc["counters_per_dispatch"]
+    fp64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64"))
+    trans = c.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
+    int32 = c.get("SQ_INSTS_VALU_INT32", 0.0)
+    other = max(0.0, c["SQ_INSTS_VALU"] - fp64 - trans - int32)
+    cyc = (VALU_CYCLES["fp64"] * fp64 + VALU_CYCLES["fp64_trans"] * trans + VALU_CYCLES["int32"] * int32
+           + VALU_CYCLES["other"] * other) / world
+    need_s = cyc / SIMDS / CLOCK_HZ  # launch time at full issue, peak clock
+    out = {"achieved": need_s / kernel_s * CLOCK_HZ / 1e9, "peak": CLOCK_HZ / 1e9, "unit": "G SIMD-cycles/s per SIMD",
+           "frac": need_s / kernel_s,
+           "simd_cycles_per_launch": cyc, "cycle_weights": VALU_CYCLES,
+           "mix_per_launch": {"fp64": fp64 / world, "fp64_trans": trans / world, "int32": int32 / world,
+                              "other": other / world},
+           "source": "PMC instruction classes (profiles/pmc_latest.json) x cycles per instruction measured by "
+                     "tools/valu_lat.hip (profiles/r03a_valu_issue.txt) / (1024 SIMDs x kernel_ms)"}
+    if pmc.get("gpu_cycles_per_launch") and world == 1:
+        out["frac_at_measured_clock"] = cyc / SIMDS / pmc["gpu_cycles_per_launch"]
+    return out
 
 WORKLOADS = {
     # name: (M, c, p, n, description)
@@ -74,11 +109,33 @@ def build_inputs(name):
     return E.model_inputs(*args, **kw)
 
 
+def host_cores():
+    """Host cores this process may use: its CPU affinity set (what
+    sched_getaffinity reports), and the cgroup CPU quota if one is set
+    (/sys/fs/cgroup/cpu.max, in CPUs; None when unlimited)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return n, quota
+
+
+def cores_note(threads):
+    n, quota = host_cores()
+    return (f"{threads} host threads = the {n} CPUs of this process's affinity set"
+            + (f" (cgroup CPU quota {quota:g})" if quota is not None else " (no cgroup CPU quota)"))
+
+
 def cpu_baseline(seam, budget_s=15.0, threads=None):
     """Oracle literal (N x N, postcal.cpp:214-304) per-configuration cost on the
-    host cores, on a random sample of this workload's configurations."""
+    host cores (every CPU of the affinity set), on a random sample of this
+    workload's configurations."""
     from oracle import oracle as O
-    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    threads = threads or host_cores()[0]
     U = seam.n_union
     k = int(seam.max_causal)
     rng = np.random.default_rng(0)
@@ -119,7 +176,7 @@ def cpu_baseline(seam, budget_s=15.0, threads=None):
     n = sum(done)
     return {"value": n / dt, "unit": "configs/s", "cores": threads, "kind": "port",
             "sample": f"{n} random {k}-SNP configurations of this workload, oracle literal N x N "
-                      f"restatement of lowrank_likelihood (postcal.cpp:214-304), {threads} host threads, "
+                      f"restatement of lowrank_likelihood (postcal.cpp:214-304), {cores_note(threads)}, "
                       f"{dt:.1f} s"}
 
 
@@ -153,7 +210,7 @@ def cpu_baseline_example(threads=None):
     L values are checked against the reference's expected_study*_post.txt."""
     from oracle import oracle as O
     import loci
-    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    threads = threads or host_cores()[0]
     seam = build_seam("example")
     levels = example_patterns(seam)
     O.load()
@@ -215,8 +272,8 @@ def cpu_baseline_example(threads=None):
     return {"value": n / dt, "unit": "configs/s", "cores": threads, "kind": "port", "wall_s": dt, "configs": n,
             "pips_match_reference_expected": ok,
             "sample": f"full tests/example c=2 sweep ({n} configurations), oracle literal N x N restatement of "
-                      f"lowrank_likelihood (postcal.cpp:214-304), {threads} host threads of "
-                      f"{os.cpu_count()} visible; PIPs checked against expected_study*_post.txt (6 digits)"}
+                      f"lowrank_likelihood (postcal.cpp:214-304), {cores_note(threads)}; PIPs checked against "
+                      f"expected_study*_post.txt (6 digits)"}
 
 
 def sss_probe(reps=20):
@@ -414,14 +471,30 @@ def example_wall():
         for f in os.listdir(src):
             if not f.startswith("expected_"):
                 os.symlink(os.path.join(src, f), os.path.join(d, f))
-        t0 = time.time()
+        t0 = time.time_ns()
+        env = dict(os.environ, PSX_TIMING="1", PSX_T0=str(t0))
         r = subprocess.run([E.PIPSORT_BIN, "-c", "2", "-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "snp_map",
-                            "-n", "334324,6771", "-p", "0.25", "-o", "out"], cwd=d, capture_output=True, text=True)
-        wall = time.time() - t0
+                            "-n", "334324,6771", "-p", "0.25", "-o", "out"], cwd=d, capture_output=True, text=True,
+                           env=env)
+        t1 = time.time_ns()
+        wall = (t1 - t0) / 1e9
         same = all(open(os.path.join(d, f"out_{f}.txt")).read() ==
                    open(os.path.join(src, f"expected_{f}.txt")).read()
                    for f in ("study0_post", "study1_post", "study0_set", "study1_set", "nocausal"))
-    return wall if r.returncode == 0 else None, same
+    phases = None
+    for line in r.stderr.splitlines():
+        if line.startswith("psx-timing "):
+            phases = json.loads(line[len("psx-timing "):])
+    if phases:
+        # process exit (teardown of the HIP runtime, unmapping) until the parent sees it
+        phases["exit_ms"] = t1 / 1e6 - phases.pop("end_epoch_ms")
+        phases["sum_ms"] = sum(v for k, v in phases.items() if k.endswith("_ms"))
+        phases["note"] = ("to_main = exec + dynamic loading; the HIP runtime and context come up on a second "
+                          "thread during parsing (hip_runtime, context_and_code_load), wait_for_gpu is what the "
+                          "main thread still waits for them after parsing; sum_ms adds the main-thread phases")
+        # the concurrent warm-up phases are not on the main thread's path
+        phases["sum_ms"] -= phases["hip_runtime_ms"] + phases["context_and_code_load_ms"]
+    return (wall if r.returncode == 0 else None), same, phases
 
 
 KERNEL_SOURCES = ("psx_sweep3.hip", "psx_sweep_dev.h", "psx_sweep_unit.h", "psx_math.h", "psx_sweep.h")
@@ -626,14 +699,7 @@ def main():
                     "flops_per_launch": flops, "flops_source": flops_src,
                     "pmc_kernel_src_sha": (pmc or {}).get("kernel_src_sha"), "kernel_src_sha": kernel_src_sha()}
         if pmc and pmc.get("valu_insts_per_launch") and avg_kernel_s > 0:
-            # the issue roof that actually binds: every wave64 VALU instruction (FP64,
-            # integer or select alike) holds its 16-lane SIMD for 4 cycles, so the
-            # chip issues at most 1024 SIMDs x 16 lanes x 2.4 GHz lane operations / s
-            lane_ops = pmc["valu_insts_per_launch"] * 64.0 / world
-            t_ops = lane_ops / avg_kernel_s / 1e12
-            roofline["valu_issue"] = {"achieved": t_ops, "peak": VALU_ISSUE_PEAK_TOPS, "unit": "T lane-op/s",
-                                      "frac": t_ops / VALU_ISSUE_PEAK_TOPS,
-                                      "source": "PMC SQ_INSTS_VALU x 64 per launch / kernel_ms"}
+            roofline["valu_issue"] = valu_issue_roof(pmc, avg_kernel_s, world)
         if pmc and world == 1:
             roofline["valu_busy"] = pmc.get("valu_busy")
             roofline["fp64_valu_share"] = pmc.get("fp64_valu_share")
@@ -683,9 +749,10 @@ def main():
                 out["configs_file"] = configs_probe()
             except Exception as ex:  # noqa: BLE001  (a side measurement must not lose the line)
                 out["configs_file"] = {"error": f"{type(ex).__name__}: {ex}"}
-            w, same = example_wall()
+            w, same, phases = example_wall()
             out["example_wall_s"] = w
             out["example_outputs_match_reference"] = same
+            out["example_wall_phases"] = phases
             if not args.no_cpu_baseline:
                 # BASELINE configs[0] on the same box: the north star's >= 100x is
                 # cpu_baseline_example.wall_s / example_wall_s

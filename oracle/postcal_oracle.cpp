@@ -819,6 +819,53 @@ class PostCal {
 // postcal.h:277-283 special_exp
 static double special_exp(double post, double total) { return post == 0 ? 0 : std::exp(post - total); }
 
+// postcal.cpp:1166-1236: the stdout credible-set listing of findOptimalSetGreedy.
+// Every SNP's exp(post - total) as util.h:12-27's data(number, index, 0), each
+// study's range sorted by by_number (|number| descending, std::sort); the ranks
+// of study s are then read from items[i] for i < M_s (postcal.cpp:1187-1189 as
+// written: the first range for every study), and the walk to the -r mass prints
+// the UNRANKED SNP start + index with its pip when the ranked pip passes the -a
+// threshold (postcal.cpp:1209-1225).
+struct RankData {
+    double number;
+    int index1, index2;
+};
+static void print_listing(const Problem& P, const Accum& A, double total, double inputRho, double threshold) {
+    vector<RankData> items;
+    for (int i = 0; i < P.N; i++) items.push_back(RankData{std::exp(A.post[i] - total), i, 0});
+    printf("\n");
+    vector<int> rank(P.N, 0);
+    int start_offset = 0, end_offset = 0;
+    for (int s = 0; s < P.S; s++) {
+        end_offset += P.m[s];
+        printf("start offset = %d\n", start_offset);
+        printf("end offset = %d\n", end_offset);
+        std::sort(items.begin() + start_offset, items.begin() + end_offset,
+                  [](RankData const& l, RankData const& r) { return std::abs(l.number) > std::abs(r.number); });
+        printf("sort complete %d\n", s);
+        for (int i = 0; i < P.m[s]; i++) rank[start_offset + i] = items[i].index1;
+        start_offset = end_offset;
+    }
+    std::cout << "threshold is " << threshold << "\n";
+    start_offset = end_offset = 0;
+    for (int s = 0; s < P.S; s++) {
+        end_offset += P.m[s];
+        double rho = 0;
+        int index = 0;
+        while (rho < inputRho) {
+            rho += special_exp(A.post[rank[start_offset + index]], total);
+            if (special_exp(A.post[rank[start_offset + index]], total) > threshold) {
+                double pip = special_exp(A.post[start_offset + index], total);
+                if (pip > 0.01) printf("%d %f\n", start_offset + index, pip);
+            }
+            index++;
+            if (index >= P.m[s]) break;
+        }
+        start_offset = end_offset;
+    }
+    printf("\n");
+}
+
 // postcal.cpp:1128-1164 (finalisation that affects files), model.h:282-310 and
 // postcal.h:288-336 (file writers)
 static void write_outputs(const Problem& P, const Inputs& in, const Accum& A, double totalLog,
@@ -1117,7 +1164,7 @@ static vector<int> read_sigma(const string& ss) {  // pipsort.cpp:46-66
 
 int main(int argc, char** argv) {
     int maxc = 3, oc, sss_flag = 0, num_groups = 0, num_configs = 0, literal = 0;
-    double gamma = 0.01, p = 0.75, t2 = 0.52, s2 = 5.2;
+    double gamma = 0.01, p = 0.75, t2 = 0.52, s2 = 5.2, rho = 0.95, cutoff = 0;
     string ldf, zf, mapf, out, ss, configs;
     while ((oc = getopt(argc, argv, "vhl:o:z:m:p:r:c:k:g:f:t:s:n:a:b:d:e:q:xL:")) != -1) {
         if (optarg == NULL || *optarg == '\0') { printf("optarg is NULL\n"); exit(1); }
@@ -1137,6 +1184,8 @@ int main(int argc, char** argv) {
             case 's': s2 = atof(optarg); break;
             case 'q': sss_flag = std::stoi(optarg); break;
             case 'L': literal = atoi(optarg); break;
+            case 'r': rho = atof(optarg); break;
+            case 'a': cutoff = atof(optarg); break;  /* pipsort.cpp:171-176 (':' and '?' fall into 'a') */
             default: break;
         }
     }
@@ -1174,6 +1223,7 @@ int main(int argc, char** argv) {
     std::cout << "Time to eval all= " << std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count()
               << "[µs]" << std::endl;
     printf("configs evaluated = %ld\n", pc.A.n_eval);
+    orc::print_listing(P, pc.A, tot, rho, cutoff);
     orc::write_outputs(P, in, pc.A, tot, out);
     return 0;
 }

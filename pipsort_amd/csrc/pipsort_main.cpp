@@ -6,6 +6,7 @@
 // through into -n, options without an argument abort with "optarg is NULL"),
 // same input formats and the same output files.
 #include <fcntl.h>
+#include <sched.h>
 #include <getopt.h>
 #include <thread>
 #include <sys/mman.h>
@@ -118,6 +119,14 @@ const char* extract_double(const char* s, const char* end, double& v) {
     return p;
 }
 
+// host threads this process may run on (its CPU affinity set)
+unsigned affinity_cores() {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) return std::max(1, CPU_COUNT(&set));
+    return std::max(1u, std::thread::hardware_concurrency());
+}
+
 void parse_chunk(const char* s, const char* end, ParsedChunk& out) {
     // a thread-local vector, moved out at the end: the chunks' vector headers sit
     // side by side in one array, and pushing into them per token would make the
@@ -156,8 +165,8 @@ bool import_data(const string& fn, vector<double>& out) {
     munmap(p, len + 1);
     const char* s = buf.c_str();
     const char* end = s + len;
-    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    const size_t nt = len < (size_t)(1 << 20) ? 1 : hw;
+    // every core of the affinity set, but at least 512 KB of text per thread
+    const size_t nt = std::max<size_t>(1, std::min<size_t>(affinity_cores(), len >> 19));
     // chunk boundaries at whitespace, so no token is split
     vector<const char*> cut(nt + 1);
     cut[0] = s;
@@ -222,6 +231,82 @@ double special_exp(double post, double total) { return post == 0 ? 0 : std::exp(
 
 bool g_multi = false;  // several devices: errors come from the psx_multi layer
 
+// Phase timing of one run (PSX_TIMING=1: one "psx-timing {json}" line on
+// stderr at exit).  Wall-clock epoch milliseconds, so a parent that records its
+// own time before spawning the process (PSX_T0 = epoch ns) sees process start
+// + dynamic loading as the gap to main.
+double epoch_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::system_clock::now().time_since_epoch()).count();
+}
+struct PhaseTimes {
+    double main = 0, parse0 = 0, parse1 = 0, rt0 = 0, rt1 = 0, warm1 = 0, joined = 0, setup1 = 0, sweep1 = 0,
+           accum1 = 0, write1 = 0, end = 0;
+} g_ph;
+
+void print_phases() {
+    if (!getenv("PSX_TIMING")) return;
+    const char* t0 = getenv("PSX_T0");
+    const double spawn = t0 ? atof(t0) / 1e6 : g_ph.main;
+    fprintf(stderr,
+            "psx-timing {\"to_main_ms\": %.3f, \"args_ms\": %.3f, \"parse_ms\": %.3f, \"hip_runtime_ms\": %.3f, "
+            "\"context_and_code_load_ms\": %.3f, \"wait_for_gpu_ms\": %.3f, \"gpu_setup_ms\": %.3f, "
+            "\"sweep_ms\": %.3f, \"readback_ms\": %.3f, \"write_ms\": %.3f, \"teardown_ms\": %.3f, "
+            "\"end_epoch_ms\": %.3f}\n",
+            g_ph.main - spawn, g_ph.parse0 - g_ph.main, g_ph.parse1 - g_ph.parse0, g_ph.rt1 - g_ph.rt0, g_ph.warm1 - g_ph.rt1,
+            g_ph.joined - g_ph.parse1, g_ph.setup1 - g_ph.joined, g_ph.sweep1 - g_ph.setup1,
+            g_ph.accum1 - g_ph.sweep1, g_ph.write1 - g_ph.accum1, g_ph.end - g_ph.write1, g_ph.end);
+}
+
+// postcal.cpp:1166-1236 (stdout only): per study, the SNPs ranked by
+// exp(post - total) with util.h:23-27's by_number (|x| descending) through the
+// same std::sort, then the walk to the -r credible mass printing "index pip" for
+// ranked PIPs above the -a threshold.  Reproduces the reference's indexing as
+// written: study s's ranks are read from items[0 .. M_s) (study 0's sorted
+// range), and the printed pip is the unranked SNP's at start + index.
+struct RankItem {
+    double number;
+    int index1, index2;
+};
+void print_credible_listing(const vector<double>& post, double total, const vector<int>& m, double input_rho,
+                            double threshold) {
+    const int N = (int)post.size();
+    vector<RankItem> items;
+    items.reserve(N);
+    for (int i = 0; i < N; i++) items.push_back(RankItem{std::exp(post[i] - total), i, 0});
+    printf("\n");
+    vector<int> rank(N, 0);
+    int start = 0, end = 0;
+    for (int s = 0; s < 2; s++) {
+        end += m[s];
+        printf("start offset = %d\n", start);
+        printf("end offset = %d\n", end);
+        std::sort(items.begin() + start, items.begin() + end,
+                  [](const RankItem& l, const RankItem& r) { return std::fabs(l.number) > std::fabs(r.number); });
+        printf("sort complete %d\n", s);
+        for (int i = 0; i < m[s]; i++) rank[start + i] = items[i].index1;
+        start = end;
+    }
+    std::cout << "threshold is " << threshold << "\n";
+    start = end = 0;
+    for (int s = 0; s < 2; s++) {
+        end += m[s];
+        double r = 0;
+        int index = 0;
+        while (r < input_rho) {
+            const double ranked = special_exp(post[rank[start + index]], total);
+            r += ranked;
+            if (ranked > threshold) {
+                const double pip = special_exp(post[start + index], total);
+                if (pip > 0.01) printf("%d %f\n", start + index, pip);
+            }
+            index++;
+            if (index >= m[s]) break;
+        }
+        start = end;
+    }
+    printf("\n");
+}
+
 int die_engine(int rc) {
     std::cout << "engine error (" << rc << "): " << (g_multi ? psx_multi_last_error() : psx_last_error()) << std::endl;
     if (rc == PSX_ESINGULAR) {
@@ -238,6 +323,7 @@ int die_engine(int rc) {
 }  // namespace
 
 int main(int argc, char* argv[]) {
+    g_ph.main = epoch_ms();
     int totalCausalSNP = 3;  // pipsort.cpp:69-77
     double gamma = 0.01, sharing_param = 0.75, rho = 0.95, tau_sqr = 0.52, sigma_g_squared = 5.2;
     double cutoff_threshold = 0;
@@ -297,16 +383,20 @@ int main(int argc, char* argv[]) {
         exit(1);
     }
     auto t_setup0 = std::chrono::steady_clock::now();
-    // Devices: PSX_DEVICES="0,1,..." (entries may repeat), else PSX_DEVICE, else
-    // the visible GPUs the sweep can use — one process drives them all, as the
-    // reference's OpenMP threads use the whole node (postcal.cpp:747-769).  Each
-    // extra device costs its own context and Model setup (~0.1-0.2 s) while one
-    // MI355X sweeps ~3e12 configurations/s, so by default an exhaustive run
-    // takes one more device per 5e11 configurations (SSS walks and -b files:
-    // one device unless asked).
+    // Devices: PSX_DEVICE (default 0) runs the sweep on one GPU.  Several GPUs
+    // in one process (psx_multi, the analogue of the reference's whole-node
+    // OpenMP threads, postcal.cpp:747-769) are opt-in: PSX_DEVICES="0,1,.."
+    // (entries may repeat), or PSX_DEVICES=auto, which takes one more visible
+    // device per 5e11 configurations of an exhaustive sweep (each extra device
+    // costs its own context and Model setup, ~0.1-0.2 s, while one MI355X
+    // sweeps ~4.5e12 configurations/s; SSS walks and -b files stay on one).
     vector<int32_t> devices;
     bool defer_devices = false;
-    if (const char* ds = getenv("PSX_DEVICES")) {
+    const char* ds = getenv("PSX_DEVICES");
+    if (ds && string(ds) == "auto") {
+        devices.push_back(0);
+        defer_devices = true;  // decided once the locus size is known
+    } else if (ds) {
         std::stringstream ss(ds);
         string tok;
         while (std::getline(ss, tok, ','))
@@ -315,7 +405,6 @@ int main(int argc, char* argv[]) {
         devices.push_back(atoi(d));
     } else {
         devices.push_back(0);
-        defer_devices = true;  // decided once the locus size is known
     }
     if (devices.empty()) devices.push_back(0);
     const int device = devices[0];
@@ -323,18 +412,24 @@ int main(int argc, char* argv[]) {
     // the HIP runtime / contexts come up on a second thread while the inputs
     // are parsed (errors, if any, surface again at psx_create*)
     std::thread warm([devices] {
+        g_ph.rt0 = epoch_ms();
+        int nd = 0;
+        psx_device_count(&nd);  // the HIP runtime
+        g_ph.rt1 = epoch_ms();
         vector<int32_t> seen;
         for (int32_t d : devices)
             if (std::find(seen.begin(), seen.end(), d) == seen.end()) {
                 seen.push_back(d);
                 psx_warmup(d);
             }
+        g_ph.warm1 = epoch_ms();
     });
     auto quit = [&warm](int code) {  // input errors below exit as the reference does, after the warm-up
         warm.join();
         exit(code);
     };
     // ---- Model (model.h:86-264) ----
+    g_ph.parse0 = epoch_ms();
     vector<vector<double>> sig(S), zs(S);
     vector<vector<string>> names(S);
     vector<int> m(S);
@@ -383,7 +478,9 @@ int main(int argc, char* argv[]) {
     vector<int32_t> u2l_flat(2 * U);
     for (int s = 0; s < 2; s++)
         for (int u = 0; u < U; u++) u2l_flat[s * U + u] = u2l[s][u];
+    g_ph.parse1 = epoch_ms();
     warm.join();
+    g_ph.joined = epoch_ms();
     psx_engine* eng = nullptr;
     psx_multi* multi = nullptr;
     int rc;
@@ -457,6 +554,7 @@ int main(int argc, char* argv[]) {
                      : psx_create(&prob, device, &eng);  // model.h:265
     }
     if (rc) die_engine(rc);
+    g_ph.setup1 = epoch_ms();
     auto t_setup1 = std::chrono::steady_clock::now();
     std::cout << "Time for setup = " << std::chrono::duration_cast<std::chrono::microseconds>(t_setup1 - t_setup0).count()
               << "[µs]" << std::endl;
@@ -491,6 +589,7 @@ int main(int argc, char* argv[]) {
         rc = g_multi ? psx_multi_run_exhaustive(multi) : psx_run_exhaustive(eng);
     }
     if (rc) die_engine(rc);
+    g_ph.sweep1 = epoch_ms();
     auto t1 = std::chrono::steady_clock::now();
     std::cout << "Time to eval all= " << std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count()
               << "[µs]" << std::endl;
@@ -502,6 +601,7 @@ int main(int argc, char* argv[]) {
     acc.shared_ll = sll.data();
     acc.notshared_ll = nsll.data();
     if ((rc = g_multi ? psx_multi_get_accum(multi, &acc) : psx_get_accum(eng, &acc))) die_engine(rc);
+    g_ph.accum1 = epoch_ms();
     psx_timing tm;
     if (g_multi)
         psx_multi_get_timing(multi, &tm);
@@ -533,6 +633,7 @@ int main(int argc, char* argv[]) {
     vector<char> causalSet(N, '0');
     for (int i = 0; i < N; i++)
         if (special_exp(post[i], total) > 0.05) causalSet[i] = '1';  // postcal.cpp:1158-1164
+    print_credible_listing(post, total, m, rho, cutoff_threshold);
     // ---- finishUp (model.h:282-310) + printPost2File (postcal.h:288-336) ----
     int so = 0;
     for (int s = 0; s < 2; s++) {
@@ -559,12 +660,20 @@ int main(int argc, char* argv[]) {
             f << all_snp_pos[u] << "\t" << special_exp(shared[u], total) << "\t" << sll[u] << "\t" << nsll[u]
               << std::endl;
     }
+    std::cout.flush();
+    g_ph.write1 = epoch_ms();
     if (g_multi)
         psx_multi_destroy(multi);
     else
         psx_destroy(eng);
-    (void)rho;
-    (void)cutoff_threshold;
     (void)num_causal_s;
-    return 0;
+    g_ph.end = epoch_ms();
+    print_phases();
+    // Every output is written and the engine destroyed (its device work done,
+    // its memory freed).  Returning from main would now run the HIP runtime's
+    // static teardown, ~0.1 s on MI355X (bench example_wall_phases.exit_ms) — a
+    // third of the whole tests/example run; the kernel reclaims the process's
+    // device resources at exit either way, so leave directly, exit status 0.
+    fflush(nullptr);
+    _exit(0);
 }

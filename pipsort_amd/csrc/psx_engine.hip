@@ -21,6 +21,7 @@
 
 #include "../../include/pipsort_engine.h"
 #include "../../include/pipsort_model.h"
+#include "psx_configs.h"
 #include "psx_math.h"
 #include "psx_setup.h"
 #include "psx_sweep.h"
@@ -653,6 +654,9 @@ struct psx_engine {
     hipEvent_t aev[2 * kRing] = {};
     int a_head = 0, a_pending = 0, a_count = 0;
     double a_kms = 0;
+    // configs-file enumerator (psx_configs.hip): index maps on the device, workspace
+    int* d_cfg_maps = nullptr;  // l2u[N] | u2l[2 * U]
+    psx::CfgWork cfg;
     // timing
     hipEvent_t ev[4];
     psx_timing timing;
@@ -671,6 +675,8 @@ psx_engine::~psx_engine() {
     if (hscore) hipHostFree(hscore);
     hipFree(dgen); hipFree(dscore); hipFree(dsrec); hipFree(dmrec); hipFree(dpass);
     psx::sweep_free(plans);
+    psx::configs_free(cfg);
+    hipFree(d_cfg_maps);
     for (auto& kv : glevels) {
         GenLevel& g = kv.second;
         hipFree(g.d_sets); hipFree(g.d_csr); hipFree(g.d_srec); hipFree(g.d_mrec);
@@ -1461,6 +1467,12 @@ int psx_warmup(int device) {
     hipError_t le = hipGetLastError();
     hipError_t se = hipDeviceSynchronize();
     hipFree(d);
+    // and the other translation units' device code (each its own code object),
+    // which Model setup and the first pass would otherwise load on first use
+    if (le == hipSuccess && se == hipSuccess &&
+        (psx::warm_module_setup() || psx::warm_module_sweep() || psx::warm_module_sweep3() ||
+         psx::warm_module_configs()))
+        return fail(PSX_EHIP, "warm-up: device code of a translation unit did not load");
     if (le != hipSuccess || se != hipSuccess)
         return fail(PSX_EHIP, std::string("warm-up: ") + hipGetErrorString(le != hipSuccess ? le : se));
     return 0;
@@ -1668,188 +1680,57 @@ int psx_run_configs(psx_engine* e, const int16_t* rows, int64_t n_rows, int32_t 
     std::memset(&e->timing, 0, sizeof(e->timing));
     if (n_rows < 0 || n_groups < 0 || (n_rows > 0 && (!rows || n_groups == 0)))
         return fail(PSX_EINVAL, "bad configs rows");
-    // this rank's contiguous slice of the rows (psx_set_shard)
+    // the row walk's index maps (model.h:134-139), once per engine: global index
+    // -> union position (study 1 after study 0's m0 entries), union -> local
+    if (!e->d_cfg_maps) {
+        std::vector<int> maps;
+        maps.reserve((size_t)e->N + 2 * (size_t)e->U);
+        for (int s = 0; s < 2; s++)
+            for (int u = 0; u < e->U; u++)
+                if (e->u2l[s * e->U + u] >= 0) maps.push_back(u);  // local order = union order (Invariant)
+        if ((int)maps.size() != e->N) return fail(PSX_EINVAL, "snp map does not cover the studies");
+        maps.insert(maps.end(), e->u2l.begin(), e->u2l.end());
+        HIPCHK(hipMalloc(&e->d_cfg_maps, maps.size() * sizeof(int)));
+        HIPCHK(hipMemcpy(e->d_cfg_maps, maps.data(), maps.size() * sizeof(int), hipMemcpyHostToDevice));
+    }
+    psx::CfgMaps C{e->d_cfg_maps, e->d_cfg_maps + e->N, e->U, e->N, e->m[0], e->m[1]};
+    psx::CfgProb P;
+    for (int s = 0; s < 2; s++) {
+        P.G[s] = e->dp.G[s];
+        P.Ad[s] = e->dp.Ad[s];
+        P.y[s] = e->dp.y[s];
+        P.dval[s] = e->dp.dval[s];
+    }
+    P.pres = e->dp.pres;
+    P.ldg = e->dp.ldg;
+    std::memcpy(P.Ck, e->dp.Ck, sizeof(P.Ck));
+    std::memcpy(P.pit, e->dp.pit, sizeof(P.pit));
+    std::memcpy(P.prior, e->dp.prior, sizeof(P.prior));
+    // every rank validates every row (a bad row fails all ranks alike, before any
+    // collective), and evaluates its contiguous slice (psx_set_shard)
     const int64_t r0 = n_rows * e->rank / e->world, r1 = n_rows * (e->rank + 1) / e->world;
-    const int stride = PSX_KMAX;
-    if ((r1 - r0) * stride >= (int64_t)INT32_MAX) return fail(PSX_ERANGE, "configs file too large for one pass");
-    // idx_to_union_pos_map (model.h:134-139)
-    std::vector<int> l2u[2];
-    for (int s = 0; s < 2; s++)
-        for (int u = 0; u < e->U; u++)
-            if (e->u2l[s * e->U + u] >= 0) l2u[s].push_back(u);
-    const int off1 = e->m[0];
-    // One row of computeTotalLikelihoodGivenConfigs (postcal.cpp:441-590):
-    // global indices -> union positions (sorted, unique), then the walk that
-    // assigns each entry to (study, member) and rejects rows out of order.
-    // Returns k (0: null row), -1 index out of range, -2 > PSX_KMAX members,
-    // -3 the walk failed (postcal.cpp:587-590).
-    auto parse = [&](const int16_t* in, int* locs, int* b) -> int {
-        int n = 0;
-        bool over = false;
-        for (int i = 0; i < n_groups; i++) {
-            const int g = in[i];
-            if (g < 0) continue;
-            if (g >= e->N) return -1;
-            const int st = g >= off1 ? 1 : 0;  // postcal.cpp:500-504
-            const int u = l2u[st][g - (st ? off1 : 0)];
-            int j = n;  // insertion into the sorted unique list
-            bool dup = false;
-            for (int q = 0; q < n; q++) dup |= locs[q] == u;
-            if (dup) continue;
-            if (n == stride) { over = true; continue; }
-            while (j > 0 && locs[j - 1] > u) { locs[j] = locs[j - 1]; j--; }
-            locs[j] = u;
-            n++;
-        }
-        if (over) return -2;
-        if (n == 0) return 0;  // postcal.cpp:459-488
-        b[0] = b[1] = 0;
-        int aux = 0;
-        while (aux < n_groups && in[aux] < 0) aux++;
-        int cum = 0;
-        for (int i = 0; i < 2; i++) {
-            cum += e->m[i];
-            const int offi = i ? off1 : 0;
-            for (int j = 0; j < n; j++) {
-                const int loc = e->u2l[i * e->U + locs[j]];
-                if (loc >= 0) {
-                    const int gidx = offi + loc;
-                    if (gidx >= cum) break;
-                    if (aux < n_groups && in[aux] == gidx) {
-                        aux++;
-                        b[i] |= 1 << j;
-                        while (aux < n_groups && in[aux] < 0) aux++;
-                    }
-                }
-            }
-            if (aux == n_groups) break;
-        }
-        return aux == n_groups ? n : -3;
-    };
     HIPCHK(hipEventRecord(e->ev[0], e->stream));
-    // Host preprocessing, parallel over contiguous row chunks and allocation-free
-    // per row.  Pass 1 validates and counts (non-null rows, records per union
-    // SNP); pass 2 writes the sets, forced masks and the record CSR straight into
-    // the pinned staging buffer at offsets fixed by the chunk order, so the
-    // result is identical to a serial pass (deterministic merges).
-    const int64_t nr = r1 - r0;
-    const int T = (int)std::max<int64_t>(1, std::min<int64_t>(
-        std::min(16u, std::max(1u, std::thread::hardware_concurrency())), (nr + 4095) / 4096));
-    std::vector<int64_t> c_sets(T, 0), c_nulls(T, 0), c_err(T, INT64_MAX);
-    std::vector<int> c_code(T, 0);
-    std::vector<std::vector<int>> c_hist(T);
-    auto chunk = [&](int t, int64_t& a, int64_t& b) {
-        a = r0 + nr * t / T;
-        b = r0 + nr * (t + 1) / T;
-    };
-    auto pass1 = [&](int t) {
-        int64_t a, b;
-        chunk(t, a, b);
-        std::vector<int>& h = c_hist[t];
-        h.assign(e->U, 0);
-        int locs[PSX_KMAX], bb[2];
-        // counts in registers, stored once: the per-chunk slots share cache lines
-        // (incrementing them per row cost 60 ms of false sharing at 4.8M rows)
-        int64_t sets = 0, nulls = 0;
-        for (int64_t r = a; r < b; r++) {
-            const int k = parse(rows + r * n_groups, locs, bb);
-            if (k < 0) { c_err[t] = r; c_code[t] = k; break; }
-            if (k == 0) { nulls++; continue; }
-            sets++;
-            for (int j = 0; j < k; j++) h[locs[j]]++;
-        }
-        c_sets[t] = sets;
-        c_nulls[t] = nulls;
-    };
-    {
-        std::vector<std::thread> th;
-        for (int t = 1; t < T; t++) th.emplace_back(pass1, t);
-        pass1(0);
-        for (auto& x : th) x.join();
+    psx::CfgResult res;
+    const char* err = nullptr;
+    if (psx::configs_pass(e->cfg, rows, n_rows, n_groups, r0, r1, C, P, e->dacc, e->dsacc, e->stream, e->ev[2],
+                          e->ev[3], &res, &err))
+        return fail(PSX_EHIP, std::string("configs file: ") + err);
+    if (res.fail_row >= 0) {  // the first failing row in row order
+        reset_acc(e);
+        if (res.fail_code == 1) return fail(PSX_EINVAL, "configs row index outside the SNP range");
+        if (res.fail_code == 2) return fail(PSX_ERANGE, "configs row has more than 6 union SNPs");
+        return fail(PSX_EORDER, "This did not work as expected (postcal.cpp:587-590)");
     }
-    for (int t = 0; t < T; t++)  // the first failing row in row order
-        if (c_err[t] != INT64_MAX) {
-            if (c_code[t] == -1) return fail(PSX_EINVAL, "configs row index outside the SNP range");
-            if (c_code[t] == -2) return fail(PSX_ERANGE, "configs row has more than 6 union SNPs");
-            return fail(PSX_EORDER, "This did not work as expected (postcal.cpp:587-590)");
-        }
-    int64_t nsets = 0, nulls = 0;
-    std::vector<int64_t> set_off(T, 0);
-    for (int t = 0; t < T; t++) {
-        set_off[t] = nsets;
-        nsets += c_sets[t];
-        nulls += c_nulls[t];
-    }
-    // CSR of records (set * stride + member) by union SNP, in record order
-    std::vector<int> cnt(e->U, 0);
-    for (int t = 0; t < T; t++)
-        for (int u = 0; u < e->U; u++) cnt[u] += c_hist[t][u];
-    std::vector<int> ptr(1, 0), rowsnp;
-    std::vector<int64_t> start(e->U, 0);
-    int64_t acc = 0;
-    for (int u = 0; u < e->U; u++)
-        if (cnt[u]) {
-            start[u] = acc;
-            rowsnp.push_back(u);
-            acc += cnt[u];
-            ptr.push_back((int)acc);
-        }
-    // per-chunk fill offsets: chunk t's records of SNP u follow chunks < t
-    std::vector<std::vector<int64_t>> c_start(T, std::vector<int64_t>(e->U, 0));
-    for (int u = 0; u < e->U; u++) {
-        int64_t run = start[u];
-        for (int t = 0; t < T; t++) {
-            c_start[t][u] = run;
-            run += c_hist[t][u];
-        }
-    }
-    const size_t n_sets = (size_t)nsets * stride, n_forced = (size_t)nsets * 2;
-    const size_t total = n_sets + n_forced + ptr.size() + (size_t)acc + rowsnp.size();
-    if (e->stage_rec) HIPCHK(hipEventSynchronize(e->stage_ev));
-    if (nsets > 0 && (rc = ensure_host(e->hstage, e->cap_stage, total))) return rc;
-    int* const hsets = e->hstage;
-    int* const hforced = hsets + n_sets;
-    int* const hptr = hforced + n_forced;
-    int* const hidx = hptr + ptr.size();
-    int* const hrows = hidx + acc;
-    auto pass2 = [&](int t) {
-        int64_t a, b;
-        chunk(t, a, b);
-        std::vector<int64_t>& fill = c_start[t];
-        int64_t si = set_off[t];
-        int locs[PSX_KMAX], bb[2];
-        for (int64_t r = a; r < b; r++) {
-            const int k = parse(rows + r * n_groups, locs, bb);
-            if (k <= 0) continue;
-            int* S = hsets + si * stride;
-            for (int j = 0; j < stride; j++) S[j] = j < k ? locs[j] : -1;
-            hforced[2 * si] = bb[0];
-            hforced[2 * si + 1] = bb[1];
-            for (int j = 0; j < k; j++) hidx[fill[locs[j]]++] = (int)(si * stride + j);
-            si++;
-        }
-    };
-    if (nsets > 0) {
-        std::memcpy(hptr, ptr.data(), ptr.size() * sizeof(int));
-        std::memcpy(hrows, rowsnp.data(), rowsnp.size() * sizeof(int));
-        std::vector<std::thread> th;
-        for (int t = 1; t < T; t++) th.emplace_back(pass2, t);
-        pass2(0);
-        for (auto& x : th) x.join();
-    }
-    double kms = 0;
-    if (nsets > 0 && (rc = eval_generic_staged(e, stride, (size_t)nsets, true, ptr.size(), (size_t)acc,
-                                               rowsnp.size(), true, nullptr, &kms)))
-        return rc;
-    if ((rc = fold_null(e, (double)nulls))) return rc;
+    if ((rc = fold_null(e, (double)res.nulls))) return rc;
     HIPCHK(hipEventRecord(e->ev[1], e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    float ms = 0;
+    float ms = 0, kms = 0;
     HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
+    if (res.nsets > 0) HIPCHK(hipEventElapsedTime(&kms, e->ev[2], e->ev[3]));
     e->timing.sweep_ms = ms;
     e->timing.kernel_ms = kms;
-    e->timing.kernel_launches = 1;
-    e->timing.configs = (uint64_t)nr;
+    e->timing.kernel_launches = res.nsets > 0 ? 1 : 0;
+    e->timing.configs = (uint64_t)(r1 - r0);
     return 0;
 }
 

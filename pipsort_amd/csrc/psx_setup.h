@@ -28,6 +28,9 @@ int lu_det_device(double* dA, int n, int* dswp, double* ddiag, hipStream_t st, d
 int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, double* dS, double* dy,
                    LdStudyResult* res, std::string* err);
 
+// this translation unit's device code, loaded ahead of first use (psx_warmup)
+int warm_module_setup();
+
 }  // namespace psx
 
 #endif

@@ -689,4 +689,10 @@ int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, dou
     return rc;
 }
 
+// load this translation unit's device code on the current device (psx_warmup)
+int warm_module_setup() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void*)k_get_diag) == hipSuccess ? 0 : -1;
+}
+
 }  // namespace psx

@@ -173,5 +173,9 @@ int launch_merge_sets(const SetRec* rec, long n, const SetRec& extra, SetRec* ac
                       bool init = false, int* zero_flag = nullptr);
 const char* sweep_error();
 
+// device code of the sweep translation units, loaded ahead of first use (psx_warmup)
+int warm_module_sweep();
+int warm_module_sweep3();
+
 }  // namespace psx
 #endif

@@ -835,4 +835,10 @@ void sweep_free(SweepPlanCache& C) {
     C.d_flag = nullptr;
 }
 
+// load this translation unit's device code on the current device (psx_warmup)
+int warm_module_sweep() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void*)k_merge_sets) == hipSuccess ? 0 : -1;
+}
+
 }  // namespace psx

@@ -60,6 +60,13 @@ constexpr double kQ1 = PSX_LN2 / 256.0;
 constexpr double kQ2 = kQ1 * kQ1 / 2.0;
 constexpr double kQ3 = kQ2 * kQ1 / 3.0;
 constexpr double kQ4 = kQ3 * kQ1 / 4.0;
+// the walk's cubic: Chebyshev interpolant of 2^{f/256} on |f| <= 1/2 (nodes
+// cos((2i+1) pi / 8) / 2), max relative error 1.8e-14 (the Taylor quartic above:
+// 3.8e-17); it saves the walk two FP64 operations per union set (-2.2 %, r03)
+constexpr double kC0 = 0.9999999999999825;
+constexpr double kC1 = 0.002707606174062277;
+constexpr double kC2 = 3.665566156758823e-06;
+constexpr double kC3 = 3.3083029835781016e-09;
 
 // an opaque point in the instruction stream for a loaded value: no use of it can
 // be scheduled before this statement (the wait for the load lands here)
@@ -141,16 +148,16 @@ __device__ __forceinline__ void split3a(double h, double rP, int& N, double& q) 
 }
 
 // split3a with the rounding offset by an integer R (cmag = kMagic - 256 R):
-// N = round(256 (h - R)), so the caller's exponent is N >> 8 = n - R directly
+// N = round(256 (h - R)), so the caller's exponent is N >> 8 = n - R directly;
+// the fraction's exponential by the walk's cubic (kC*)
 __device__ __forceinline__ void split3r(double h, double rP, double cmag, int& N, double& q) {
     const double xr = fma(h, 256.0, cmag);
     N = __double2loint(xr);
     const double kf = xr - cmag;
     const double f = fma(h, 256.0, -kf);
-    double p = fma(kQ4, f, kQ3);
-    p = fma(p, f, kQ2);
-    p = fma(p, f, kQ1);
-    p = fma(p, f, 1.0);
+    double p = fma(kC3, f, kC2);
+    p = fma(p, f, kC1);
+    p = fma(p, f, kC0);
     q = p * rP;
 }
 
@@ -1304,6 +1311,12 @@ __global__ void k_scale_y(const double* __restrict__ y, int n, double* __restric
 int launch_scale_y(const double* y, int n, double* ys, hipStream_t st) {
     hipLaunchKernelGGL(k_scale_y, dim3((n + 255) / 256), dim3(256), 0, st, y, n, ys);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// load this translation unit's device code on the current device (psx_warmup)
+int warm_module_sweep3() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void*)k_scale_y) == hipSuccess ? 0 : -1;
 }
 
 }  // namespace psx

@@ -104,6 +104,62 @@ def test_pipsort_cli_reproduces_reference_goldens(gpu, tmp_path):
         assert np.abs(np.array(a) - np.array(b)).max() <= PIP_TOL
 
 
+def _listing(stdout):
+    """The credible-set block of findOptimalSetGreedy's stdout (postcal.cpp:1166-1236)."""
+    lines = stdout.splitlines()
+    i = lines.index("start offset = 0")
+    j = next(k for k in range(i, len(lines)) if lines[k].startswith("threshold is"))
+    k = j + 1
+    while k < len(lines) and lines[k] != "":
+        k += 1
+    return lines[i - 1:k + 1]
+
+
+@pytest.mark.parametrize("src,extra", [
+    ("example", ["-c", "2", "-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "snp_map", "-n", "334324,6771",
+                 "-p", "0.25"]),
+    ("example", ["-c", "2", "-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "snp_map", "-n", "334324,6771",
+                 "-p", "0.25", "-r", "0.9999999", "-a", "1e-4"]),
+    ("small_example", ["-c", "3", "-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "eur_afr_small_test_snp_map",
+                       "-n", "7000,7000", "-r", "0.999"]),
+])
+def test_cli_credible_listing_matches_oracle(gpu, tmp_path, src, extra):
+    """The stdout credible-set listing (rank sort per study, "threshold is",
+    the "index pip" lines of the -r / -a walk) is the oracle CLI's restatement
+    of postcal.cpp:1166-1236, line for line."""
+    d = tmp_path / src
+    shutil.copytree(os.path.join(loci.GOLDEN, src), d)
+    r = subprocess.run([E.PIPSORT_BIN] + extra + ["-o", "gpu"], cwd=d, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    O.load()
+    o = subprocess.run([O.CLI] + extra + ["-o", "orc"], cwd=d, capture_output=True, text=True, timeout=600)
+    assert o.returncode == 0, o.stdout + o.stderr
+    got, want = _listing(r.stdout), _listing(o.stdout)
+    assert got == want
+    assert len(got) >= 8
+
+
+def test_cli_phase_timing_line(gpu, tmp_path):
+    """PSX_TIMING=1: the CLI's phase breakdown (stderr) covers its own wall time."""
+    import json
+    import time
+    d = tmp_path / "example"
+    shutil.copytree(os.path.join(loci.GOLDEN, "example"), d)
+    t0 = time.time_ns()
+    r = subprocess.run([E.PIPSORT_BIN, "-c", "2", "-l", "ldfiles.txt", "-z", "zfiles.txt", "-m", "snp_map", "-n",
+                        "334324,6771", "-p", "0.25", "-o", "out"], cwd=d, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PSX_TIMING="1", PSX_T0=str(t0)))
+    t1 = time.time_ns()
+    assert r.returncode == 0, r.stdout + r.stderr
+    ph = json.loads(next(l for l in r.stderr.splitlines() if l.startswith("psx-timing "))[len("psx-timing "):])
+    main_path = sum(v for k, v in ph.items() if k.endswith("_ms") and k not in
+                    ("hip_runtime_ms", "context_and_code_load_ms", "end_epoch_ms"))
+    wall_ms = (t1 - t0) / 1e6
+    exit_ms = t1 / 1e6 - ph["end_epoch_ms"]
+    assert all(v >= -1.0 for k, v in ph.items() if k.endswith("_ms") and k != "end_epoch_ms")
+    assert abs(main_path + exit_ms - wall_ms) <= 0.05 * wall_ms + 1.0
+
+
 def test_configs_file_path(gpu):
     seam, L = loci.seam_for(loci.CONFIGS)
     rows = np.fromfile(os.path.join(L["dir"], "all_configs_int16"), dtype=np.int16).reshape(72, 5)
