@@ -223,11 +223,14 @@ int psx_fold_partials_host(const void *src, int32_t count, int64_t image_bytes, 
 int psx_shard_stats(const psx_problem *prob, int32_t k, int32_t rank, int32_t world, uint64_t *union_sets,
                     double *configs);
 
-/* Host-only diagnostics: the k = 3 fast sweep's work units of shard `rank` of
- * `world` for a union of n_union SNPs present in both studies, in dispatch
- * order, as int4 {a0, a1, K | j0 << 16, C | j1 << 16} (v space; a diagonal
- * tile's j counts half steps).  Writes at most `cap` units; returns the count
- * (or a negative error). */
+/* Host-side diagnostics (no kernel runs): the k = 3 fast sweep's work units of
+ * shard `rank` of `world` for a union of n_union SNPs present in both studies,
+ * in dispatch order, as int4 {a0, a1, K | j0 << 16, C | j1 << 16} (v space; a
+ * diagonal tile's j counts half steps).  The a-chunk sizes follow the CU count
+ * of the current HIP device (hipGetDeviceProperties; a fixed default without
+ * one), so the decomposition depends on the device; every plan covers each
+ * walk step once.  Writes at most `cap` units; returns the count (or a
+ * negative error). */
 int psx_plan_units_k3(int32_t n_union, int32_t rank, int32_t world, int32_t *units, int32_t cap);
 
 /* ---- Several GPUs in one process --------------------------------------------

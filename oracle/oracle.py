@@ -118,7 +118,7 @@ def member_sums(seam, u, threads=None):
     n = np.ascontiguousarray(seam.sample_sizes, dtype=np.int32)
     out = np.zeros(5)
     npat = ctypes.c_long(0)
-    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    threads = threads or len(os.sched_getaffinity(0))
     D = ctypes.c_double
     rc = lib.oracle_member_sums(2, _p(m, ctypes.c_int), _p(B, D), _p(sp, D), u2l.shape[1], _p(u2l, ctypes.c_int),
                                 _p(n, ctypes.c_int), float(seam.sharing_param), float(seam.gamma),

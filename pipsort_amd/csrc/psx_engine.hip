@@ -136,9 +136,13 @@ __global__ void k_to_union(const double* __restrict__ S, int M, const int* __res
 // the per-lane arrays stay in VGPRs (no scratch); members outside a lane's
 // subset enter its LDL^T as zero rows, which leaves the in-subset arithmetic
 // (and its rounding) exactly that of psx::ldlt_terms.
+// span (optional, device [lo, hi)): block b evaluates set lo + b of `sets`, the
+// blocks past hi - lo exit (a batch whose size the device decided); outputs
+// stay indexed by b
 __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restrict__ sets, int stride,
                                                   const int* __restrict__ forced, SetRec* __restrict__ srec,
-                                                  Acc5* __restrict__ mrec, double* __restrict__ score) {
+                                                  Acc5* __restrict__ mrec, double* __restrict__ score,
+                                                  const int* __restrict__ span = nullptr) {
     constexpr int KM = PSX_KMAX;
     __shared__ double s_g[2][KM][KM];
     __shared__ double s_ad[2][KM], s_y[2][KM];
@@ -148,7 +152,12 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
     __shared__ int s_mem[KM];
     const int set = blockIdx.x;
     const int lane = threadIdx.x;
-    const int* S = sets + (size_t)set * stride;
+    int base = 0;
+    if (span) {
+        base = span[0];
+        if (set >= span[1] - base) return;
+    }
+    const int* S = sets + (size_t)(base + set) * stride;
     const int v = lane < stride && lane < KM ? S[lane] : -1;
     const unsigned long long bal = __ballot(v >= 0);
     const int k = __popcll(bal);
@@ -1347,23 +1356,35 @@ int create_impl(const psx_problem* p, const psx_ld_problem* ld, int device, psx_
                 spsq += r.spsq;
             } else {
                 // Sigma' not (comfortably) positive definite: the reference's eigen
-                // route, model.h:213-259 (host restatement), then B^T B on the GPU
+                // route (model.h:213-259) on the GPU, B and S' left in dB / dsp
+                // (PSX_HOST_EIGEN=1: the host restatement instead, for tests)
                 std::vector<double> sig(ld->ld + boff, ld->ld + boff + (size_t)M * M);
                 for (int i = 0; i < M; i++) sig[(size_t)i * M + i] += r.added;
-                hB.resize((size_t)M * M);
-                hS.resize(M);
-                if (psx_lowrank_study(sig.data(), ld->z + soff, M, hB.data(), hS.data())) {
-                    cleanup();
-                    return bail(fail(PSX_EINVAL, "eigen route failed"));
+                const char* he = getenv("PSX_HOST_EIGEN");
+                if (he && atoi(he)) {
+                    hB.resize((size_t)M * M);
+                    hS.resize(M);
+                    if (psx_lowrank_study(sig.data(), ld->z + soff, M, hB.data(), hS.data())) {
+                        cleanup();
+                        return bail(fail(PSX_EINVAL, "eigen route failed"));
+                    }
+                    for (int i = 0; i < M; i++) spsq += hS[i] * hS[i];
+                    Bs = hB.data();
+                    Ss = hS.data();
+                } else {
+                    double sq = 0;
+                    if (psx::eigen_lowrank_device(sig.data(), ld->z + soff, M, e->stream, dS, dB, dsp, &sq, &err)) {
+                        cleanup();
+                        return bail(fail(PSX_EHIP, "GPU eigen route: " + err));
+                    }
+                    spsq += sq;
+                    Bs = Ss = nullptr;  // already on the device
                 }
-                for (int i = 0; i < M; i++) spsq += hS[i] * hS[i];
-                Bs = hB.data();
-                Ss = hS.data();
             }
         }
         if (lowrank) {
-            hipMemcpyAsync(dB, Bs, (size_t)M * M * sizeof(double), hipMemcpyHostToDevice, e->stream);
-            hipMemcpyAsync(dsp, Ss, (size_t)M * sizeof(double), hipMemcpyHostToDevice, e->stream);
+            if (Bs) hipMemcpyAsync(dB, Bs, (size_t)M * M * sizeof(double), hipMemcpyHostToDevice, e->stream);
+            if (Ss) hipMemcpyAsync(dsp, Ss, (size_t)M * sizeof(double), hipMemcpyHostToDevice, e->stream);
             dim3 g((M + 15) / 16, (M + 15) / 16);
             hipLaunchKernelGGL(k_btb, g, dim3(256), 0, e->stream, dB, M, dS);
             hipLaunchKernelGGL(k_bts, dim3(M), dim3(64), 0, e->stream, dB, dsp, M, dyl);
@@ -1734,134 +1755,347 @@ int psx_run_configs(psx_engine* e, const int16_t* rows, int64_t n_rows, int32_t 
     return 0;
 }
 
-// sss_postcal.cpp:102-380.  The random walk, neighbourhoods, hash map and
-// sampling run on the host exactly as the reference orders them; every
-// iteration's unseen neighbours are one GPU batch.  The host side is kept
-// allocation-free per neighbour: neighbourhoods are flat rows, and the
-// reference's unordered_map<vector<int>, double> (postcal.h:43-56) is an
-// open-addressing table keyed by the packed sorted set.
+// sss_postcal.cpp:102-380 with the iteration's batch work device-resident.
+// The walk is serial: each iteration samples the next configuration from all
+// neighbour scores with the reference's mt19937(12345) and libstdc++
+// discrete_distribution, in the reference's order (sss_postcal.cpp:296-343), so
+// that sampling stays on the host.  Everything else of an iteration runs as
+// three launches and one synchronisation:
+//   k_sss_nbd   one block: the neighbourhood of `cur` (swap ++ minus ++ plus,
+//               sss_postcal.cpp:20-99, 166-186) in the reference's order, each
+//               set looked up in a device open-addressing map (the reference's
+//               unordered_map<vector<int>, double>, postcal.h:43-56, 98), the
+//               unseen ones compacted into the batch in neighbour order (the
+//               unseen current configuration first, :195-202), null sets scored
+//               K + L0 on the spot (:463-499), this rank's slice of the batch
+//   k_eval_sets one wave per batch set of the slice: every pattern's L, the
+//               set's score (max |L| pattern, :624-626), records
+//   k_sss_post  a block per union SNP folds its records in batch order (the
+//               current configuration's members scan the batch; any other SNP
+//               i is only in the swaps (cur \ {c_v}) + {i} and the plus set
+//               cur + {i}, at known neighbour indices), one block folds the set
+//               records and null configurations into the scalars, and the rest
+//               insert the new scores into the map (:280-284) and write every
+//               neighbour's score (the sampling weights) to pinned host memory
+// With several ranks (psx_run_sss_sharded) each evaluates a contiguous slice of
+// the batch; the slices' scores and the ranks' normalisers are all-gathered by
+// the caller's callback, then the insert runs on every rank with all scores.
 namespace {
-// A sorted union set of <= 6 SNPs as two words of three 21-bit fields
-// (index + 1; 0 = no member).  The empty set packs to {0, 0}.
-struct SetKey {
-    uint64_t lo, hi;
-    bool operator==(const SetKey& o) const { return lo == o.lo && hi == o.hi; }
-};
-constexpr int kKeyBits = 21;
+constexpr int kKeyBits = 21;  // a sorted set of <= 6 as two words of three (index + 1) fields
 constexpr int kKeyMaxU = (1 << kKeyBits) - 2;
+constexpr int kNbdThreads = 1024;
 
-inline SetKey pack_set(const int* v, int k) {
-    uint64_t w[2] = {0, 0};
-    for (int j = 0; j < k; j++) w[j / 3] |= (uint64_t)(v[j] + 1) << (kKeyBits * (j % 3));
-    return {w[0], w[1]};
+struct MapEntry {
+    unsigned long long lo, hi;
+    double score;
+    int state, pad;
+};
+
+__host__ __device__ inline unsigned long long mix64(unsigned long long x) {
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ULL;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebULL;
+    return x ^ (x >> 31);
 }
-
-// SetKey -> score with linear probing at load <= 1/2; the empty set lives in
-// a side slot so {0, 0} can mark unused table slots.  Lookup and insert only,
-// which is all the walk asks of its map.
-class SetMap {
-  public:
-    SetMap() { rehash(1 << 16); }
-    bool find(const SetKey& k, double& v) const {
-        if (k.lo == 0 && k.hi == 0) {
-            v = empty_v_;
-            return has_empty_;
-        }
-        for (size_t i = slot(k);; i = (i + 1) & mask_) {
-            if (keys_[i] == k) {
-                v = vals_[i];
-                return true;
-            }
-            if (keys_[i].lo == 0 && keys_[i].hi == 0) return false;
+__device__ inline unsigned long long map_slot(unsigned long long lo, unsigned long long hi, unsigned long long mask) {
+    return mix64(lo ^ mix64(hi + 0x9e3779b97f4a7c15ULL)) & mask;
+}
+__device__ inline bool map_find(const MapEntry* T, unsigned long long mask, unsigned long long lo,
+                                unsigned long long hi, double& v) {
+    for (unsigned long long i = map_slot(lo, hi, mask);; i = (i + 1) & mask) {
+        const MapEntry& e = T[i];
+        if (e.state == 0) return false;
+        if (e.lo == lo && e.hi == hi) {
+            v = e.score;
+            return true;
         }
     }
-    void assign(const SetKey& k, double v) {  // hm[k] = v
-        if (k.lo == 0 && k.hi == 0) {
-            has_empty_ = true;
-            empty_v_ = v;
+}
+// keys inserted by one launch are distinct and no lookup runs beside an insert
+__device__ inline void map_insert(MapEntry* T, unsigned long long mask, unsigned long long lo, unsigned long long hi,
+                                  double v) {
+    for (unsigned long long i = map_slot(lo, hi, mask);; i = (i + 1) & mask)
+        if (atomicCAS(&T[i].state, 0, 1) == 0) {
+            T[i].lo = lo;
+            T[i].hi = hi;
+            T[i].score = v;
             return;
         }
-        if (2 * (n_ + 1) > keys_.size()) rehash(2 * keys_.size());
-        size_t i = slot(k);
-        for (; !(keys_[i].lo == 0 && keys_[i].hi == 0); i = (i + 1) & mask_)
-            if (keys_[i] == k) {
-                vals_[i] = v;
-                return;
-            }
-        keys_[i] = k;
-        vals_[i] = v;
-        n_++;
-    }
-
-  private:
-    static uint64_t mix(uint64_t x) {
-        x ^= x >> 30;
-        x *= 0xbf58476d1ce4e5b9ULL;
-        x ^= x >> 27;
-        x *= 0x94d049bb133111ebULL;
-        return x ^ (x >> 31);
-    }
-    size_t slot(const SetKey& k) const { return mix(k.lo ^ mix(k.hi + 0x9e3779b97f4a7c15ULL)) & mask_; }
-    void rehash(size_t cap) {
-        std::vector<SetKey> ok(cap, SetKey{0, 0});
-        std::vector<double> ov(cap, 0.0);
-        ok.swap(keys_);
-        ov.swap(vals_);
-        mask_ = cap - 1;
-        for (size_t i = 0; i < ok.size(); i++)
-            if (!(ok[i].lo == 0 && ok[i].hi == 0)) {
-                size_t j = slot(ok[i]);
-                while (!(keys_[j].lo == 0 && keys_[j].hi == 0)) j = (j + 1) & mask_;
-                keys_[j] = ok[i];
-                vals_[j] = ov[i];
-            }
-    }
-    std::vector<SetKey> keys_;
-    std::vector<double> vals_;
-    size_t n_ = 0, mask_ = 0;
-    bool has_empty_ = false;
-    double empty_v_ = 0;
-};
-
-// Stage `n` union sets (rows of `stride`, -1 padded, `sz` members each) and
-// the member CSR (union SNP -> record, in record order) into e->hstage in the
-// eval_generic_staged layout; returns the CSR part sizes.
-int stage_sets(psx_engine* e, const int* const* rows, const int* sz, size_t n, int stride, std::vector<int>& cnt,
-               size_t& n_ptr, size_t& n_idx, size_t& n_rows) {
-    int rc;
-    std::fill(cnt.begin(), cnt.end(), 0);
-    n_idx = 0;
-    for (size_t i = 0; i < n; i++)
-        for (int j = 0; j < sz[i]; j++) cnt[rows[i][j]]++;
-    n_rows = 0;
-    for (int u = 0; u < e->U; u++) n_rows += cnt[u] != 0;
-    for (size_t i = 0; i < n; i++) n_idx += sz[i];
-    n_ptr = n_rows + 1;
-    if (e->stage_rec) HIPCHK(hipEventSynchronize(e->stage_ev));
-    if ((rc = ensure_host(e->hstage, e->cap_stage, n * stride + n_ptr + n_idx + n_rows))) return rc;
-    int* hs = e->hstage;
-    int* hptr = hs + n * stride;
-    int* hidx = hptr + n_ptr;
-    int* hrow = hidx + n_idx;
-    int acc = 0, r = 0;
-    hptr[0] = 0;
-    for (int u = 0; u < e->U; u++)
-        if (cnt[u]) {
-            hrow[r++] = u;
-            const int c = cnt[u];
-            cnt[u] = acc;  // now the fill position of u
-            acc += c;
-            hptr[r] = acc;
-        }
-    for (size_t i = 0; i < n; i++) {
-        int* S = hs + i * stride;
-        for (int j = 0; j < stride; j++) S[j] = j < sz[i] ? rows[i][j] : -1;
-        for (int j = 0; j < sz[i]; j++) hidx[cnt[rows[i][j]]++] = (int)(i * stride + j);
-    }
-    return 0;
+}
+__device__ inline void pack_key(const int* row, int n, unsigned long long& lo, unsigned long long& hi) {
+    unsigned long long w[2] = {0, 0};
+#pragma unroll
+    for (int j = 0; j < PSX_KMAX; j++)
+        if (j < n) w[j / 3] |= (unsigned long long)(row[j] + 1) << (kKeyBits * (j % 3));
+    lo = w[0];
+    hi = w[1];
 }
 
-static int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* iterations_out) {
+// one iteration's neighbourhood geometry (sss_postcal.cpp:166-186)
+struct SssIter {
+    int cur[PSX_KMAX];
+    int k, U, stride, num_zero, num_minus, num_plus, n_nbd, rank, world;
+    double null_score;  // K + L0: a null configuration's L (postcal.cpp:797-803)
+};
+
+// neighbour i (0 .. n_nbd) or, for i == -1, the current configuration: its
+// sorted members (-1 padded to `stride`) and size
+__device__ int nbd_row(const SssIter& it, int i, int* row) {
+    const int k = it.k;
+    int x = -1, skip = -1, n;
+    if (i < 0) {
+        n = k;
+    } else if (i < it.num_zero) {  // (cur \ {c_v}) + {x}
+        skip = i % k;
+        x = i / k;
+        n = k;
+    } else if (i < it.num_zero + it.num_minus) {  // cur \ {c_v}
+        skip = i - it.num_zero;
+        n = k - 1;
+    } else {  // cur + {x}
+        x = i - it.num_zero - it.num_minus;
+        n = k + 1;
+    }
+    if (x >= 0)  // the x-th SNP not in cur
+#pragma unroll
+        for (int j = 0; j < PSX_KMAX; j++)
+            if (j < k && it.cur[j] <= x) x++;
+    int m = 0;
+    bool put = x < 0;
+#pragma unroll
+    for (int j = 0; j < PSX_KMAX; j++) {
+        if (j >= k || j == skip) continue;
+        if (!put && x < it.cur[j]) {
+            row[m++] = x;
+            put = true;
+        }
+        row[m++] = it.cur[j];
+    }
+    if (!put) row[m++] = x;
+    for (int j = m; j < it.stride; j++) row[j] = -1;
+    return n;
+}
+
+// sizes written by k_sss_nbd (device ints)
+enum { kBatch = 0, kLo = 1, kHi = 2, kNulls = 3, kUnseen = 4, kNCnt = 8 };
+
+__global__ __launch_bounds__(kNbdThreads) void k_sss_nbd(SssIter it, const MapEntry* __restrict__ T,
+                                                         unsigned long long mask, int* __restrict__ bsets,
+                                                         int* __restrict__ mark, int* __restrict__ cnt,
+                                                         double* __restrict__ lk_host) {
+    __shared__ int wsum[kNbdThreads / 64];
+    __shared__ int run_total;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (t == 0) run_total = 0;
+    int nulls = 0, unseen = 0;
+    __syncthreads();
+    for (int p0 = 0; p0 < it.n_nbd + 1; p0 += kNbdThreads) {
+        const int p = p0 + t, i = p - 1;  // item 0: the current configuration
+        int row[PSX_KMAX];
+        bool in_batch = false;
+        if (p < it.n_nbd + 1) {
+            const int n = nbd_row(it, i, row);
+            unsigned long long lo, hi;
+            pack_key(row, n, lo, hi);
+            double v;
+            const bool seen = map_find(T, mask, lo, hi, v);
+            if (i >= 0) {
+                if (seen) lk_host[i] = v;
+                mark[i] = seen ? -1 : (n == 0 ? -2 : 0);
+                unseen += !seen;
+            }
+            if (!seen) {
+                if (n == 0) nulls++;  // folded as null configurations, score K + L0
+                else in_batch = true;
+            }
+        }
+        // batch position: exclusive prefix in item order
+        const unsigned long long bal = __ballot(in_batch);
+        const int before = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[w] = __popcll(bal);
+        __syncthreads();
+        int off = run_total;
+        for (int q = 0; q < w; q++) off += wsum[q];
+        if (in_batch) {
+            const int bp = off + before;
+            for (int j = 0; j < it.stride; j++) bsets[(size_t)bp * it.stride + j] = row[j];
+            if (i >= 0) mark[i] = bp;
+        }
+        __syncthreads();
+        if (t == 0)
+            for (int q = 0; q < kNbdThreads / 64; q++) run_total += wsum[q];
+        __syncthreads();
+    }
+    // the chunk loop is uniform, so every thread reaches these reductions
+    for (int o = 32; o > 0; o >>= 1) {
+        nulls += __shfl_xor(nulls, o);
+        unseen += __shfl_xor(unseen, o);
+    }
+    __shared__ int sn[kNbdThreads / 64], su[kNbdThreads / 64];
+    if (lane == 0) {
+        sn[w] = nulls;
+        su[w] = unseen;
+    }
+    __syncthreads();
+    if (t == 0) {
+        int a = 0, b = 0;
+        for (int q = 0; q < kNbdThreads / 64; q++) {
+            a += sn[q];
+            b += su[q];
+        }
+        const int nw = run_total;
+        cnt[kBatch] = nw;
+        cnt[kLo] = (int)((long long)nw * it.rank / it.world);
+        cnt[kHi] = (int)((long long)nw * (it.rank + 1) / it.world);
+        cnt[kNulls] = a;
+        cnt[kUnseen] = b;
+    }
+}
+
+// member position of u in a sorted, -1 padded batch row (or -1)
+__device__ inline int member_of(const int* row, int stride, int u) {
+    int j = -1;
+    for (int q = 0; q < stride; q++)
+        if (row[q] == u) j = q;
+    return j;
+}
+
+// blocks [0, U): per-SNP record folds; block U: the scalars; blocks > U: the
+// map inserts and the sampling weights.  mode 0: folds only, 1: folds and
+// inserts, 2: inserts only (after the all-gather of a sharded walk)
+__global__ __launch_bounds__(256) void k_sss_post(SssIter it, const int* __restrict__ bsets,
+                                                  const int* __restrict__ mark, const int* __restrict__ cnt,
+                                                  const Acc5* __restrict__ mrec, const SetRec* __restrict__ srec,
+                                                  const double* __restrict__ bscore, SetRec null1, Acc5* __restrict__ acc,
+                                                  SetRec* __restrict__ sacc, SetRec* __restrict__ sacc_host,
+                                                  MapEntry* __restrict__ T, unsigned long long mask, int mode,
+                                                  double* __restrict__ lk_host) {
+    const int lo = cnt[kLo], hi = cnt[kHi], n = hi - lo;
+    const int b = blockIdx.x, t = threadIdx.x;
+    if (mode == 2 && b <= it.U) return;
+    if (b < it.U) {
+        const int u = b;
+        bool in_cur = false;
+        for (int j = 0; j < it.k; j++) in_cur |= it.cur[j] == u;
+        Acc5 a = psx::acc_zero();
+        if (in_cur) {
+            // in (nearly) every set of the batch: the slice's sets in batch order
+            for (int q = t; q < n; q += 256) {
+                const int j = member_of(bsets + (size_t)(lo + q) * it.stride, it.stride, u);
+                if (j >= 0) psx::fold_acc(a, mrec[(size_t)q * it.stride + j]);
+            }
+            __shared__ Acc5 sh[4];
+            psx::wave_fold_acc(a);
+            if ((t & 63) == 0) sh[t >> 6] = a;
+            __syncthreads();
+            if (t == 0) {
+                Acc5 g = acc[u];
+                for (int q = 0; q < 4; q++) psx::fold_acc(g, sh[q]);
+                acc[u] = g;
+            }
+            return;
+        }
+        if (t != 0) return;
+        // u is the ri-th SNP outside cur: swaps ri * k + v, then the plus set
+        int ri = u;
+        for (int j = 0; j < it.k; j++) ri -= it.cur[j] < u;
+        bool any = false;
+        for (int v = 0; v <= it.k; v++) {
+            int i;
+            if (v < it.k) i = ri * it.k + v;
+            else if (it.num_plus) i = it.num_zero + it.num_minus + ri;
+            else break;
+            const int bp = mark[i];
+            if (bp < lo || bp >= hi) continue;  // seen, null, or another rank's
+            const int j = member_of(bsets + (size_t)bp * it.stride, it.stride, u);
+            psx::fold_acc(a, mrec[(size_t)(bp - lo) * it.stride + j]);
+            any = true;
+        }
+        if (any) {
+            Acc5 g = acc[u];
+            psx::fold_acc(g, a);
+            acc[u] = g;
+        }
+        return;
+    }
+    if (b == it.U) {  // the scalars: the slice's set records, then the null configurations (rank 0)
+        SetRec a = psx::set_zero();
+        for (int q = t; q < n; q += 256) psx::fold_set(a, srec[q]);
+        __shared__ SetRec ss[4];
+        psx::wave_fold_set(a);
+        if ((t & 63) == 0) ss[t >> 6] = a;
+        __syncthreads();
+        if (t == 0) {
+            SetRec g = *sacc;
+            for (int q = 0; q < 4; q++) psx::fold_set(g, ss[q]);
+            const int nn = cnt[kNulls];
+            if (nn > 0 && it.rank == 0) {
+                SetRec x = null1;  // null1 scaled to nn null configurations
+                x.tot *= nn;
+                x.nc0 *= nn;
+                x.nc1 *= nn;
+                x.npat *= nn;
+                psx::fold_set(g, x);
+            }
+            *sacc = g;
+            *sacc_host = g;
+        }
+        return;
+    }
+    if (mode == 0) return;
+    const int i = (b - it.U - 1) * 256 + t;
+    if (i >= it.n_nbd) return;
+    const int mk = mark[i];
+    if (mk == -1) return;  // seen: its weight was written by k_sss_nbd
+    const double v = mk == -2 ? it.null_score : bscore[mk];
+    int row[PSX_KMAX];
+    const int nr = nbd_row(it, i, row);
+    unsigned long long klo, khi;
+    pack_key(row, nr, klo, khi);
+    map_insert(T, mask, klo, khi, v);
+    lk_host[i] = v;
+}
+
+// the map at twice the capacity: re-insert every entry
+__global__ void k_map_rehash(const MapEntry* __restrict__ old, size_t n, MapEntry* __restrict__ T,
+                             unsigned long long mask) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && old[i].state) map_insert(T, mask, old[i].lo, old[i].hi, old[i].score);
+}
+
+// scores of the slice, batch-indexed, into the gather buffer (world > 1)
+__global__ void k_copy_scores(const double* __restrict__ s, const int* __restrict__ cnt, double* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < cnt[kHi] - cnt[kLo]) out[i] = s[i];
+}
+
+struct SssDev {
+    MapEntry* T = nullptr;
+    size_t cap = 0, used = 0;
+    int* bsets = nullptr;
+    int* mark = nullptr;
+    int* cnt = nullptr;
+    double* bscore = nullptr;
+    size_t cap_n = 0;
+    double* lk = nullptr;     // pinned host: every neighbour's score
+    SetRec* shost = nullptr;  // pinned host: the scalars after the iteration
+    int* hcnt = nullptr;      // pinned host: the sizes
+    double* hscore = nullptr; // pinned host: gathered batch scores (world > 1)
+    ~SssDev() {
+        hipFree(T);
+        hipFree(bsets);
+        hipFree(mark);
+        hipFree(cnt);
+        hipFree(bscore);
+        if (lk) hipHostFree(lk);
+        if (shost) hipHostFree(shost);
+        if (hcnt) hipHostFree(hcnt);
+        if (hscore) hipHostFree(hscore);
+    }
+};
+
+int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* iterations_out) {
     HIPCHK(hipSetDevice(e->dev));
     const int rank = allgather ? e->rank : 0, world = allgather ? e->world : 1;
     int rc;
@@ -1870,167 +2104,168 @@ static int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t
     const int U = e->U, C = e->maxc;
     if (C > PSX_KMAX) return fail(PSX_ERANGE, "SSS max_causal > 6");
     if (U > kKeyMaxU) return fail(PSX_ERANGE, "SSS: more union SNPs than the set key holds");
-    SetMap hm;
+    const int stride = std::max(C, 1);
+    // the largest neighbourhood: k = C (swaps C (U - C), minus C) or k = C - 1 (plus)
+    const size_t nmax = (size_t)C * U + C + U + 1;
+    SssDev D;
+    size_t cap = 1 << 16;
+    while (cap < 4 * nmax) cap <<= 1;
+    HIPCHK(hipMalloc(&D.T, cap * sizeof(MapEntry)));
+    HIPCHK(hipMemsetAsync(D.T, 0, cap * sizeof(MapEntry), e->stream));
+    D.cap = cap;
+    HIPCHK(hipMalloc(&D.bsets, nmax * stride * sizeof(int)));
+    HIPCHK(hipMalloc(&D.mark, nmax * sizeof(int)));
+    HIPCHK(hipMalloc(&D.cnt, kNCnt * sizeof(int)));
+    HIPCHK(hipMalloc(&D.bscore, nmax * sizeof(double)));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.lk), nmax * sizeof(double)));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.shost), sizeof(SetRec)));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hcnt), kNCnt * sizeof(int)));
+    if (world > 1) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hscore), nmax * sizeof(double)));
+    int ret;
+    if ((ret = ensure(e->dsrec, e->cap_srec, nmax))) return ret;
+    if ((ret = ensure(e->dmrec, e->cap_mrec, nmax * stride))) return ret;
+    if ((ret = ensure(e->dscore, e->cap_score, nmax))) return ret;
+    const SetRec null1 = null_rec(e, 1.0);
     std::mt19937 gen(12345);
-    int cur[PSX_KMAX], k = 0;  // the current configuration, ascending
+    int cur[PSX_KMAX] = {0, 0, 0, 0, 0, 0}, k = 0;  // the current configuration, ascending
     double old_sum = 0;
     int iter;
-    const int stride = std::max(C, 1);
     double kms = 0;
     auto t0 = std::chrono::steady_clock::now();
-    std::vector<char> in_cur(U, 0);
-    std::vector<int> nb, cnt(U, 0), not_done, bsz;
-    std::vector<const int*> brow;
-    std::vector<int> bpos;
-    std::vector<double> lk, s2, pr;
+    std::vector<double> pr;
     for (iter = 0; iter < 1000; iter++) {
-        // sss_postcal.cpp:166-186 nbd = zero ++ minus ++ plus, as rows of
-        // `stride` (sizes k, k - 1 and k + 1 by group)
-        std::fill(in_cur.begin(), in_cur.end(), 0);
-        for (int j = 0; j < k; j++) in_cur[cur[j]] = 1;
-        int minus[PSX_KMAX][PSX_KMAX];
-        for (int i = 0; i < k; i++)
-            for (int j = 0, m = 0; j < k; j++)
-                if (i != j) minus[i][m++] = cur[j];
-        const int num_zero = (U - k) * k, num_minus = k, num_plus = k < C ? U - k : 0;
-        const int n_nbd = num_zero + num_minus + num_plus;
-        nb.resize((size_t)n_nbd * stride);
-        auto put = [&](int* row, const int* v, int kv, int x) {  // sorted {x} ∪ v
-            int j = 0;
-            for (; j < kv && v[j] < x; j++) row[j] = v[j];
-            row[j] = x;
-            for (; j < kv; j++) row[j + 1] = v[j];
-        };
-        int* w = nb.data();
-        for (int i = 0; i < U; i++)
-            if (!in_cur[i])
-                for (int v = 0; v < k; v++, w += stride) put(w, minus[v], k - 1, i);
-        for (int v = 0; v < k; v++, w += stride)
-            for (int j = 0; j < k - 1; j++) w[j] = minus[v][j];
-        if (num_plus)
-            for (int i = 0; i < U; i++)
-                if (!in_cur[i]) {
-                    put(w, cur, k, i);
-                    w += stride;
-                }
-        auto row_size = [&](int i) { return i < num_zero ? k : i < num_zero + num_minus ? k - 1 : k + 1; };
-        // current configuration (sss_postcal.cpp:195-202): evaluated only if unseen
-        brow.clear();
-        bsz.clear();
-        bpos.clear();
-        double v;
-        if (!hm.find(pack_set(cur, k), v)) {
-            brow.push_back(cur);
-            bsz.push_back(k);
-            bpos.push_back(-1);
+        SssIter it;
+        for (int j = 0; j < PSX_KMAX; j++) it.cur[j] = j < k ? cur[j] : -1;
+        it.k = k;
+        it.U = U;
+        it.stride = stride;
+        it.num_zero = (U - k) * k;
+        it.num_minus = k;
+        it.num_plus = k < C ? U - k : 0;
+        it.n_nbd = it.num_zero + it.num_minus + it.num_plus;
+        it.rank = rank;
+        it.world = world;
+        it.null_score = e->K + e->L0;
+        const int n_nbd = it.n_nbd;
+        // the map stays at load <= 1/2 (every neighbour may be new)
+        if (2 * (D.used + (size_t)n_nbd + 1) > D.cap) {
+            size_t nc = D.cap;
+            while (2 * (D.used + (size_t)n_nbd + 1) > nc) nc <<= 1;
+            MapEntry* nt = nullptr;
+            HIPCHK(hipMalloc(&nt, nc * sizeof(MapEntry)));
+            HIPCHK(hipMemsetAsync(nt, 0, nc * sizeof(MapEntry), e->stream));
+            hipLaunchKernelGGL(k_map_rehash, dim3((unsigned)((D.cap + 255) / 256)), dim3(256), 0, e->stream, D.T,
+                               D.cap, nt, (unsigned long long)(nc - 1));
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipStreamSynchronize(e->stream));
+            hipFree(D.T);
+            D.T = nt;
+            D.cap = nc;
         }
-        lk.assign(n_nbd, 0.0);
-        not_done.clear();
-        for (int i = 0; i < n_nbd; i++) {
-            const int* r = nb.data() + (size_t)i * stride;
-            if (hm.find(pack_set(r, row_size(i)), v)) lk[i] = v;
-            else {
-                not_done.push_back(i);
-                brow.push_back(r);
-                bsz.push_back(row_size(i));
-                bpos.push_back(i);
-            }
-        }
-        // evaluate the batch on the GPU (null sets folded host side); the
-        // non-null sets keep batch order, nulls score K + L0
-        const size_t nb_all = brow.size();
-        double gsum = 0.0;  // the running normaliser over all ranks (world > 1)
-        double nulls = 0;
-        SetRec st;  // this rank's accumulated normaliser after the batch
-        size_t nw = 0;
-        for (size_t i = 0; i < nb_all; i++) {
-            if (bsz[i] == 0) { nulls += 1; continue; }
-            brow[nw] = brow[i];
-            bsz[nw] = bsz[i];
-            bpos[nw] = bpos[i];
-            nw++;
-        }
+        const unsigned long long mask = D.cap - 1;
+        hipLaunchKernelGGL(k_sss_nbd, dim3(1), dim3(kNbdThreads), 0, e->stream, it, D.T, mask, D.bsets, D.mark, D.cnt,
+                           D.lk);
+        HIPCHK(hipEventRecord(e->ev[2], e->stream));
+        hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)(n_nbd + 1)), dim3(64), 0, e->stream, e->dp, D.bsets, stride,
+                           (const int*)nullptr, e->dsrec, e->dmrec, e->dscore, (const int*)(D.cnt + kLo));
+        HIPCHK(hipEventRecord(e->ev[3], e->stream));
+        const unsigned post_blocks = (unsigned)(U + 1 + (world == 1 ? (n_nbd + 255) / 256 : 0));
+        hipLaunchKernelGGL(k_sss_post, dim3(post_blocks), dim3(256), 0, e->stream, it, D.bsets, D.mark, D.cnt, e->dmrec,
+                           e->dsrec, e->dscore, null1, e->dacc, e->dsacc, D.shost, D.T, mask, world == 1 ? 1 : 0,
+                           D.lk);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(D.hcnt, D.cnt, kNCnt * sizeof(int), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
         {
-            // this rank's contiguous slice of the non-null sets (all of it at world 1)
-            const size_t lo = nw * rank / world, hi = nw * (rank + 1) / world;
-            s2.assign(nw, 0.0);
-            if (hi > lo) {
-                size_t n_ptr, n_idx, n_rows;
-                if ((rc = stage_sets(e, brow.data() + lo, bsz.data() + lo, hi - lo, stride, cnt, n_ptr, n_idx,
-                                     n_rows)))
-                    return rc;
-                if ((rc = eval_generic_staged(e, stride, hi - lo, false, n_ptr, n_idx, n_rows, true, s2.data() + lo,
-                                              &kms, false)))
-                    return rc;
-            }
-            if (nulls > 0 && rank == 0 && (rc = fold_null(e, nulls))) return rc;
-            // the normaliser rides back with the scores: one synchronisation
-            HIPCHK(hipMemcpyAsync(e->hstat, e->dsacc, sizeof(SetRec), hipMemcpyDeviceToHost, e->stream));
-            if (hi > lo) {
-                if ((rc = finish_generic(e, hi - lo, s2.data() + lo, &kms))) return rc;
-            } else {
-                HIPCHK(hipStreamSynchronize(e->stream));
-            }
-            std::memcpy(&st, e->hstat, sizeof(SetRec));
-            if (world > 1) {
-                // one all-gather: [slice length, normaliser (m, s), slice scores]
-                const size_t per = (nw + world - 1) / world, wd = 3 + per;
-                std::vector<double> snd(wd, 0.0), rcv(wd * world, 0.0);
-                const SetRec& t = st;
-                snd[0] = (double)(hi - lo);
-                snd[1] = (double)t.m;
-                snd[2] = t.tot;
-                std::copy(s2.begin() + lo, s2.begin() + hi, snd.begin() + 3);
-                if (allgather(ctx, snd.data(), rcv.data(), (int64_t)(wd * sizeof(double))))
-                    return fail(PSX_EEXCHANGE, "SSS all-gather callback failed");
-                double mx = -INFINITY;
-                std::vector<double> part(world, 0.0);
-                for (int r = 0; r < world; r++) {
-                    const double* q = rcv.data() + (size_t)r * wd;
-                    const size_t rlo = nw * r / world, rn = nw * (r + 1) / world - rlo;
-                    if ((size_t)q[0] != rn) return fail(PSX_EEXCHANGE, "SSS all-gather: ranks disagree on the batch");
-                    std::copy(q + 3, q + 3 + rn, s2.begin() + rlo);
-                    part[r] = logval(e, (int32_t)q[1], q[2]);
-                    if (part[r] != 0.0) mx = std::max(mx, part[r]);
-                }
-                double acc = 0.0;  // the ranks' normalisers, combined in rank order
-                for (int r = 0; r < world; r++)
-                    if (part[r] != 0.0) acc += std::exp(part[r] - mx);
-                gsum = acc > 0 ? mx + std::log(acc) : 0.0;
-            }
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+            kms += ms;
         }
-        for (size_t i = 0; i < nw; i++)
-            if (bpos[i] >= 0) lk[bpos[i]] = s2[i];
-        if (nulls > 0)  // a null neighbour (the empty minus set at k = 1)
-            for (int i : not_done)
-                if (row_size(i) == 0) lk[i] = e->K + e->L0;
-        const double sss_sum = world == 1 ? logval(e, st.m, st.tot) : gsum;
-        if (not_done.empty()) break;                                                       // :260-263
-        if (iter >= 100 && (1 - std::exp(old_sum - sss_sum)) <= 0.001) break;             // :265-270
-        for (int i : not_done) hm.assign(pack_set(nb.data() + (size_t)i * stride, row_size(i)), lk[i]);  // :280-284
+        const int nw = D.hcnt[kBatch], unseen = D.hcnt[kUnseen];
+        double sss_sum;
+        if (world == 1) {
+            sss_sum = logval(e, D.shost->m, D.shost->tot);
+        } else {
+            // one all-gather: [slice length, normaliser (m, s), slice scores]; then every
+            // rank inserts all scores (batch order) and writes the sampling weights
+            const int lo = D.hcnt[kLo], hi = D.hcnt[kHi];
+            const size_t per = ((size_t)nw + world - 1) / world, wd = 3 + per;
+            std::vector<double> snd(wd, 0.0), rcv(wd * world, 0.0);
+            if (hi > lo)
+                HIPCHK(hipMemcpy(snd.data() + 3, e->dscore, (size_t)(hi - lo) * sizeof(double), hipMemcpyDeviceToHost));
+            snd[0] = (double)(hi - lo);
+            snd[1] = (double)D.shost->m;
+            snd[2] = D.shost->tot;
+            if (allgather(ctx, snd.data(), rcv.data(), (int64_t)(wd * sizeof(double))))
+                return fail(PSX_EEXCHANGE, "SSS all-gather callback failed");
+            double mx = -INFINITY;
+            std::vector<double> part(world, 0.0);
+            for (int r = 0; r < world; r++) {
+                const double* q = rcv.data() + (size_t)r * wd;
+                const size_t rlo = (size_t)nw * r / world, rn = (size_t)nw * (r + 1) / world - rlo;
+                if ((size_t)q[0] != rn) return fail(PSX_EEXCHANGE, "SSS all-gather: ranks disagree on the batch");
+                std::copy(q + 3, q + 3 + rn, D.hscore + rlo);
+                part[r] = logval(e, (int32_t)q[1], q[2]);
+                if (part[r] != 0.0) mx = std::max(mx, part[r]);
+            }
+            double acc = 0.0;  // the ranks' normalisers, combined in rank order
+            for (int r = 0; r < world; r++)
+                if (part[r] != 0.0) acc += std::exp(part[r] - mx);
+            sss_sum = acc > 0 ? mx + std::log(acc) : 0.0;
+            if (nw > 0) HIPCHK(hipMemcpyAsync(D.bscore, D.hscore, (size_t)nw * sizeof(double), hipMemcpyHostToDevice,
+                                              e->stream));
+            // the insert blocks alone (block indices past U + 1)
+            hipLaunchKernelGGL(k_sss_post, dim3((unsigned)(U + 1 + (n_nbd + 255) / 256)), dim3(256), 0, e->stream, it,
+                               D.bsets, D.mark, D.cnt, e->dmrec, e->dsrec, D.bscore, null1, (Acc5*)nullptr,
+                               (SetRec*)nullptr, (SetRec*)nullptr, D.T, mask, 2, D.lk);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipStreamSynchronize(e->stream));
+        }
+        D.used += (size_t)unseen;
+        if (unseen == 0) break;                                                          // :260-263
+        if (iter >= 100 && (1 - std::exp(old_sum - sss_sum)) <= 0.001) break;            // :265-270
+        const double* lk = D.lk;
         double wz = 0, wm = 0, wp = 0;
         size_t zs = n_nbd, ms = n_nbd, ps = n_nbd;
         auto group = [&](int b, int en, double& wsum, size_t& smp) {
             pr.clear();
-            double mx = *std::max_element(lk.begin() + b, lk.begin() + en);
+            double mx = *std::max_element(lk + b, lk + en);
             for (int ii = b; ii < en; ii++) pr.push_back(std::exp(lk[ii] - mx));
             std::discrete_distribution<size_t> dist(pr.begin(), pr.end());
             smp = dist(gen);
             wsum = std::accumulate(pr.begin(), pr.end(), 0.0);
         };
-        if (num_zero != 0) group(0, num_zero, wz, zs);                                     // :296-306
-        if (num_minus != 0) group(num_zero, num_zero + num_minus, wm, ms);                 // :307-317
-        if (num_plus != 0) group(num_zero + num_minus, n_nbd, wp, ps);                     // :318-328
+        if (it.num_zero != 0) group(0, it.num_zero, wz, zs);                               // :296-306
+        if (it.num_minus != 0) group(it.num_zero, it.num_zero + it.num_minus, wm, ms);     // :307-317
+        if (it.num_plus != 0) group(it.num_zero + it.num_minus, n_nbd, wp, ps);            // :318-328
         std::discrete_distribution<size_t> dist({wz, wm, wp});                             // :330-343
         size_t idx = dist(gen), fin = 0;
         switch (idx) {
             case 0: fin = zs; break;
-            case 1: fin = ms + num_zero; break;
-            case 2: fin = ps + num_zero + num_minus; break;
+            case 1: fin = ms + it.num_zero; break;
+            case 2: fin = ps + it.num_zero + it.num_minus; break;
         }
-        const int nk = row_size((int)fin);
-        std::copy(nb.begin() + fin * stride, nb.begin() + fin * stride + nk, cur);
-        k = nk;
+        // the chosen neighbour becomes the current configuration (host copy of nbd_row)
+        {
+            const int i = (int)fin;
+            int x = -1, skip = -1, n;
+            if (i < it.num_zero) { skip = i % k; x = i / k; n = k; }
+            else if (i < it.num_zero + it.num_minus) { skip = i - it.num_zero; n = k - 1; }
+            else { x = i - it.num_zero - it.num_minus; n = k + 1; }
+            if (x >= 0)
+                for (int j = 0; j < k; j++)
+                    if (cur[j] <= x) x++;
+            int nxt[PSX_KMAX], m = 0;
+            bool put = x < 0;
+            for (int j = 0; j < k; j++) {
+                if (j == skip) continue;
+                if (!put && x < cur[j]) { nxt[m++] = x; put = true; }
+                nxt[m++] = cur[j];
+            }
+            if (!put) nxt[m++] = x;
+            std::copy(nxt, nxt + n, cur);
+            k = n;
+        }
         old_sum = sss_sum;
     }
     auto t1 = std::chrono::steady_clock::now();

@@ -28,6 +28,14 @@ int lu_det_device(double* dA, int n, int* dswp, double* ddiag, hipStream_t st, d
 int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, double* dS, double* dy,
                    LdStudyResult* res, std::string* err);
 
+// The reference's eigen route for a study whose Sigma' is not positive
+// definite (util.cpp:228-263, model.h:213-259), on the GPU (psx_eigen.hip): sig
+// (host, row-major M x M, Sigma' = LD + shift I) and z (host) -> dB = B =
+// |W|^1/2 Q^T (device, column-major) and dsp = S' = |W|^-1/2 Q^T z (device),
+// *spsq = ||S'||^2.  dQ: M x M device scratch.
+int eigen_lowrank_device(const double* sig, const double* z, int M, hipStream_t st, double* dQ, double* dB,
+                         double* dsp, double* spsq, std::string* err);
+
 // this translation unit's device code, loaded ahead of first use (psx_warmup)
 int warm_module_setup();
 

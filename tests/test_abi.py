@@ -156,9 +156,11 @@ def test_host_lu_det_matches_numpy_and_underflows_like_gsl():
 @pytest.mark.parametrize("U", [3, 65, 300, 1000])
 @pytest.mark.parametrize("world", [1, 2, 8])
 def test_k3_units_cover_every_walk_step_once(U, world):
-    """The k = 3 work units of all shards (after the tail refinement cuts the
-    last dispatch round into single-a units and b-walk halves) cover every
-    (a, tile, b-walk step) of the block-pattern decomposition exactly once."""
+    """The k = 3 work units of all shards cover every (a, tile, b-walk step) of
+    the block-pattern decomposition exactly once (a units may split a b-walk:
+    the ranges of one (a, tile) must tile [0, 64)).  The a-chunk sizes depend on
+    the CU count of the current device (or a CPU-only default), the coverage
+    does not."""
     ldg = (U + 63) // 64 * 64
     pad = ldg - U
     seen = {}

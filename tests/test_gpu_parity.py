@@ -591,13 +591,22 @@ def _member_pins(pc_accum, seam, snps, rtol=1e-10):
         np.testing.assert_allclose(got, want, rtol=rtol, atol=0, err_msg=f"SNP {u}")
 
 
+# union SNPs pinned at the headline locus (U = 1000, padded to 1024: the sweep's
+# v = u + 24, so its 64-blocks start at u = 40, 104, ...): both ends; the
+# 64-block edges in u (63 | 64, 127 | 128, 191 | 192) and in the sweep's v
+# space (39 | 40, 103 | 104, 231 | 232); the planted shared causal 250 and the
+# study-0 causal 750 with their neighbours; members of one diagonal tile
+# (499, 500, 501 share v-block 8); the last pair 998, 999
+HEADLINE_PINS = [0, 39, 40, 63, 64, 103, 104, 127, 128, 191, 192, 231, 232, 249, 250, 251, 499, 500, 501, 749, 750,
+                 751, 998, 999]
+
+
 def test_headline_locus_value_pins(gpu):
     """BASELINE configs[3], the bench locus (SYN-v1 M = 1000, c = 3, 4.49e9
     configurations) through the GPU Model setup: post (both studies), shared,
-    sharedLL and notSharedLL of five SNPs — the planted shared causal (250),
-    the study-0 causal (750), both ends and the middle — each against an exact
-    sum over its 13.5M assignments by the oracle (about 2 s per SNP on 16
-    host threads)."""
+    sharedLL and notSharedLL of 24 SNPs (HEADLINE_PINS) each against an exact
+    sum over its 13.5M assignments by the oracle (oracle.member_sums on every
+    host core of the affinity set)."""
     M = 1000
     ld, z, _, _, u2l = synth.syn_v1(M)
     mi = E.model_inputs(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
@@ -606,7 +615,7 @@ def test_headline_locus_value_pins(gpu):
     a = pc.accum()
     assert a.n_configs == 4_491_007_501
     seam = O.cholesky_seam(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
-    _member_pins(a, seam, [250, 750, 0, 499, 999])
+    _member_pins(a, seam, HEADLINE_PINS)
     pc.close()
 
 

@@ -161,6 +161,49 @@ def test_indefinite_sigma_takes_eigen_route(gpu):
     assert_parity(got, O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-9)
 
 
+def _indefinite(M, seed):
+    """A symmetric Sigma with two negative eigenvalues and det > 0 (the PSD loop
+    of util.cpp:195-226 stops at a = 0, so the eigen route must take |W|)."""
+    rng = np.random.default_rng(seed)
+    q, _ = np.linalg.qr(rng.standard_normal((M, M)))
+    w = np.linspace(0.05, 4.0, M)
+    w[:2] = [-0.3, -0.5]
+    sig = (q * w) @ q.T
+    return (sig + sig.T) / 2, rng
+
+
+def test_indefinite_sigma_gpu_eigen_route_m500(gpu):
+    """The eigen route on the GPU (rocSOLVER dsyevd, psx_eigen.hip) at M = 500:
+    PIPs and LL columns of the host route's seam (the restated model.h:213-259
+    eigen route) through the oracle."""
+    M = 500
+    sig, rng = _indefinite(M, 11)
+    assert E.lu_det(sig) > 0
+    ld = [sig, 0.5 ** np.abs(np.arange(M)[:, None] - np.arange(M)[None, :])]
+    z = [rng.standard_normal(M) * 2, rng.standard_normal(M) * 2]
+    z[0][M // 3] += 6.0
+    u2l = np.stack([np.arange(M), np.arange(M)]).astype(np.int32)
+    seam, mi = _both(ld, z, u2l, (6000, 7000), max_causal=2, sharing_param=0.4)
+    pc, got = _run(mi)
+    assert pc.setup_info["eigen_route"] == [1, 0]
+    assert_parity(got, O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-9)
+
+
+def test_indefinite_sigma_m1000_sets_up_under_a_second(gpu):
+    """An indefinite M = 1000 LD through the GPU eigen route: the whole Model
+    setup + PostCal construction (psx_create_from_ld) in < 1 s."""
+    M = 1000
+    sig, rng = _indefinite(M, 12)
+    ld = [sig, 0.5 ** np.abs(np.arange(M)[:, None] - np.arange(M)[None, :])]
+    z = [rng.standard_normal(M), rng.standard_normal(M)]
+    u2l = np.stack([np.arange(M), np.arange(M)]).astype(np.int32)
+    mi = E.model_inputs(ld, z, u2l, (6000, 7000), max_causal=2, sharing_param=0.4)
+    E.PostCal(mi).close()  # first create of the process: runtime / library start-up
+    pc = E.PostCal(mi)
+    assert pc.setup_info["eigen_route"] == [1, 0]
+    assert pc.setup_info["setup_ms"] < 1000.0, pc.setup_info
+
+
 def test_cli_host_setup_route_still_reproduces_goldens(gpu, tmp_path):
     """PSX_HOST_SETUP=1 keeps the reference's eigen route in the drop-in CLI."""
     d = tmp_path / "example"
