@@ -51,6 +51,8 @@ struct CfgWork {
     void* sort_tmp = nullptr;
     size_t cap_sort = 0;
     unsigned long long* hstatus = nullptr;  // pinned host copy of status
+    char* hpin = nullptr;                   // pinned staging of the upload: two chunks
+    hipEvent_t dma[2] = {nullptr, nullptr};  // the chunks' copies out of hpin
 };
 
 struct CfgResult {

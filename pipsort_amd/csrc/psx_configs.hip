@@ -29,6 +29,16 @@
 // pre-pass it replaces (same per-SNP fold order, same arithmetic).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <sched.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <thread>
+#include <vector>
 
 #include "psx_configs.h"
 #include "psx_sweep.h"
@@ -42,10 +52,10 @@ constexpr int kRowsPerBlock = 256;
 constexpr int kLdsHistMax = 16384;  // union SNPs whose per-block counts fit in LDS (64 KB)
 
 // the one forced assignment of an evaluated row (the weights k_eval_rows gives
-// every member record of the row); Ck < 0: the assignment adds nothing
+// every member record of the row); valid == 0: the assignment adds nothing
 struct CfgRow {
     double w, wll;
-    int G, Ck;
+    int G, Ck, valid, pad;
 };
 
 // postcal.cpp:441-590 for one row, as the host pass restated it: returns k
@@ -257,7 +267,7 @@ __global__ __launch_bounds__(kRowsPerBlock) void k_cfg_eval(const int16_t* __res
         }
     const int Ck = P.Ck[k];
     SetRec rr = set_zero();
-    CfgRow row{0.0, 0.0, 0, -1};
+    CfgRow row{0.0, 0.0, 0, 0, 0, 0};
     const bool valid = ((c0 | c1) == (1 << k) - 1) && !(c0 & ~S0) && !(c1 & ~S1);
     if (valid) {
         double mu[2], f[2];
@@ -286,7 +296,7 @@ __global__ __launch_bounds__(kRowsPerBlock) void k_cfg_eval(const int16_t* __res
         rr.nc1 = c1 == 0 ? mup * P.pit[k][0] : 0.0;
         rr.score = f[0] + f[1] + P.prior[k][nsh];
         rr.npat = 1.0;
-        row = CfgRow{w, wll, G, Ck};
+        row = CfgRow{w, wll, G, Ck, 1, 0};
     }
     srec[si] = rr;
     rrec[si] = row;
@@ -304,7 +314,7 @@ __device__ __forceinline__ Acc5 cfg_record(const CfgRow* __restrict__ rrec, cons
     const int set = q / PSX_KMAX, j = q - set * PSX_KMAX;
     const CfgRow row = rrec[set];
     Acc5 a = acc_zero();
-    if (row.Ck < 0) return a;
+    if (!row.valid) return a;
     const int m = masks[set];
     const int x = ((m >> j) & 1) | (((m >> (8 + j)) & 1) << 1);
     a.mP = row.G + row.Ck;
@@ -349,6 +359,58 @@ __global__ __launch_bounds__(256) void k_cfg_merge(const CfgRow* __restrict__ rr
     }
 }
 
+// Host rows -> device.  The caller's rows are pageable (an mmapped -b file, a
+// numpy array), which the runtime would stage chunk by chunk on one thread;
+// here T host threads copy each 8 MB chunk into one of two pinned buffers while
+// the DMA engine moves the previous chunk: the upload runs at the slower of the
+// parallel host copy and the PCIe transfer instead of their sum.
+constexpr size_t kStageChunk = 8u << 20;
+int upload_rows(CfgWork& W, const void* src, size_t bytes, void* dst, hipStream_t st) {
+    if (bytes <= 2 * kStageChunk)
+        return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st) == hipSuccess ? 0 : -1;
+    if (!W.hpin && hipHostMalloc(reinterpret_cast<void**>(&W.hpin), 2 * kStageChunk) != hipSuccess) return -1;
+    for (int b = 0; b < 2; b++)
+        if (!W.dma[b] && hipEventCreateWithFlags(&W.dma[b], hipEventDisableTiming) != hipSuccess) return -1;
+    const size_t nch = (bytes + kStageChunk - 1) / kStageChunk;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    const int cores = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 4;
+    const int T = std::max(1, std::min(cores, 8));
+    std::unique_ptr<std::atomic<int>[]> done(new std::atomic<int>[nch]);
+    for (size_t c = 0; c < nch; c++) done[c].store(0);
+    std::atomic<size_t> writable{2};  // chunks below this may be copied into their pinned buffer
+    auto work = [&](int t) {
+        for (size_t c = 0; c < nch; c++) {
+            while (writable.load(std::memory_order_acquire) <= c) std::this_thread::yield();
+            const size_t len = std::min(kStageChunk, bytes - c * kStageChunk);
+            const size_t a = len * t / T, e = len * (t + 1) / T;
+            std::memcpy(W.hpin + (c & 1) * kStageChunk + a, (const char*)src + c * kStageChunk + a, e - a);
+            done[c].fetch_add(1, std::memory_order_release);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; t++) th.emplace_back(work, t);
+    int rc = 0;
+    std::thread main_copy(work, 0);
+    for (size_t c = 0; c < nch; c++) {
+        while (done[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
+        const size_t len = std::min(kStageChunk, bytes - c * kStageChunk);
+        const int b = (int)(c & 1);
+        if (rc == 0 && (hipMemcpyAsync((char*)dst + c * kStageChunk, W.hpin + b * kStageChunk, len,
+                                       hipMemcpyHostToDevice, st) != hipSuccess ||
+                        hipEventRecord(W.dma[b], st) != hipSuccess))
+            rc = -1;
+        // chunk c + 2 reuses this buffer once its copy has left it
+        if (c + 2 < nch) {
+            if (rc == 0 && hipEventSynchronize(W.dma[b]) != hipSuccess) rc = -1;
+            writable.store(c + 3, std::memory_order_release);
+        }
+    }
+    main_copy.join();
+    for (auto& x : th) x.join();
+    return rc;
+}
+
 template <typename T>
 bool grow(T*& p, size_t& cap, size_t n) {
     if (n <= cap) return true;
@@ -382,7 +444,7 @@ int configs_pass(CfgWork& W, const int16_t* rows, int64_t n_rows, int n_groups, 
         return bad("out of device memory");
     if (!W.hstatus && hipHostMalloc(&W.hstatus, 4 * sizeof(unsigned long long)) != hipSuccess)
         return bad("out of pinned host memory");
-    if (hipMemcpyAsync(W.rows, rows, nel * sizeof(int16_t), hipMemcpyHostToDevice, st) != hipSuccess ||
+    if (upload_rows(W, rows, nel * sizeof(int16_t), W.rows, st) ||
         hipMemsetAsync(W.status, 0xff, sizeof(unsigned long long), st) != hipSuccess ||
         hipMemsetAsync(W.status + 1, 0, 3 * sizeof(unsigned long long), st) != hipSuccess ||
         hipMemsetAsync(W.ptr, 0, ((size_t)C.U + 1) * sizeof(int), st) != hipSuccess)
@@ -475,6 +537,9 @@ void configs_free(CfgWork& W) {
     hipFree(W.vals);
     hipFree(W.sort_tmp);
     if (W.hstatus) hipHostFree(W.hstatus);
+    for (int b = 0; b < 2; b++)
+        if (W.dma[b]) hipEventDestroy(W.dma[b]);
+    if (W.hpin) hipHostFree(W.hpin);
     W = CfgWork{};
 }
 

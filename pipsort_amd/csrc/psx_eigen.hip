@@ -9,11 +9,13 @@
 //
 // B and S' are then PostCal's own inputs (postcal.h:118): the engine forms
 // Sigma~ = B^T B and y = B^T S' from them exactly as for psx_create.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
-#include <rocblas/rocblas.h>
+#include <rocblas/rocblas.h>  // types only: the libraries are opened on first use
 #include <rocsolver/rocsolver.h>
 
 #include <cmath>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -45,6 +47,34 @@ __global__ __launch_bounds__(64) void k_eig_lowrank(const double* __restrict__ Q
     if (threadIdx.x == 0) sp[r] = acc / so;
 }
 
+// rocSOLVER (and the rocBLAS it depends on) opened on the first eigen route of
+// the process, not linked: loading rocBLAS costs every process ~10 ms at start,
+// and the route only runs for a study whose Sigma' is not positive definite
+struct Solver {
+    rocblas_status (*create)(rocblas_handle*) = nullptr;
+    rocblas_status (*set_stream)(rocblas_handle, hipStream_t) = nullptr;
+    rocblas_status (*destroy)(rocblas_handle) = nullptr;
+    rocblas_status (*dsyevd)(rocblas_handle, const rocblas_evect, const rocblas_fill, const rocblas_int, double*,
+                             const rocblas_int, double*, double*, rocblas_int*) = nullptr;
+    bool ok = false;
+};
+
+const Solver& solver() {
+    static Solver S;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librocsolver.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librocsolver.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        S.create = reinterpret_cast<decltype(S.create)>(dlsym(h, "rocblas_create_handle"));
+        S.set_stream = reinterpret_cast<decltype(S.set_stream)>(dlsym(h, "rocblas_set_stream"));
+        S.destroy = reinterpret_cast<decltype(S.destroy)>(dlsym(h, "rocblas_destroy_handle"));
+        S.dsyevd = reinterpret_cast<decltype(S.dsyevd)>(dlsym(h, "rocsolver_dsyevd"));
+        S.ok = S.create && S.set_stream && S.destroy && S.dsyevd;
+    });
+    return S;
+}
+
 }  // namespace
 
 int eigen_lowrank_device(const double* sig, const double* z, int M, hipStream_t st, double* dQ, double* dB,
@@ -53,12 +83,14 @@ int eigen_lowrank_device(const double* sig, const double* z, int M, hipStream_t 
         *err = m;
         return -1;
     };
+    const Solver& L = solver();
+    if (!L.ok) return bad("rocSOLVER not found (librocsolver.so.0)");
     double* dw = nullptr;
     double* dz = nullptr;
     rocblas_int* dinfo = nullptr;
     rocblas_handle h = nullptr;
     auto done = [&]() {
-        if (h) rocblas_destroy_handle(h);
+        if (h) L.destroy(h);
         hipFree(dw);
         hipFree(dz);
         hipFree(dinfo);
@@ -75,11 +107,11 @@ int eigen_lowrank_device(const double* sig, const double* z, int M, hipStream_t 
         done();
         return bad("eigen route upload");
     }
-    if (rocblas_create_handle(&h) != rocblas_status_success || rocblas_set_stream(h, st) != rocblas_status_success) {
+    if (L.create(&h) != rocblas_status_success || L.set_stream(h, st) != rocblas_status_success) {
         done();
         return bad("rocblas handle");
     }
-    if (rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_upper, M, dQ, M, dw, dw + M, dinfo) !=
+    if (L.dsyevd(h, rocblas_evect_original, rocblas_fill_upper, M, dQ, M, dw, dw + M, dinfo) !=
         rocblas_status_success) {
         done();
         return bad("rocsolver_dsyevd");

@@ -136,13 +136,11 @@ __global__ void k_to_union(const double* __restrict__ S, int M, const int* __res
 // the per-lane arrays stay in VGPRs (no scratch); members outside a lane's
 // subset enter its LDL^T as zero rows, which leaves the in-subset arithmetic
 // (and its rounding) exactly that of psx::ldlt_terms.
-// span (optional, device [lo, hi)): block b evaluates set lo + b of `sets`, the
-// blocks past hi - lo exit (a batch whose size the device decided); outputs
-// stay indexed by b
-__global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restrict__ sets, int stride,
-                                                  const int* __restrict__ forced, SetRec* __restrict__ srec,
-                                                  Acc5* __restrict__ mrec, double* __restrict__ score,
-                                                  const int* __restrict__ span = nullptr) {
+// One union set S (stride entries, -1 padded) by the calling wave: its set
+// record (*so), its member records (mo[0 .. k), if mo) and its SSS score (*sc,
+// if sc); fpair = (C0 mask, C1 mask) restricts the set to one pattern.
+__device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride, const int* __restrict__ fpair,
+                         SetRec* __restrict__ so, Acc5* __restrict__ mo, double* __restrict__ sc) {
     constexpr int KM = PSX_KMAX;
     __shared__ double s_g[2][KM][KM];
     __shared__ double s_ad[2][KM], s_y[2][KM];
@@ -150,14 +148,7 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
     __shared__ double s_f[2][64];
     __shared__ int s_n[2][64];
     __shared__ int s_mem[KM];
-    const int set = blockIdx.x;
     const int lane = threadIdx.x;
-    int base = 0;
-    if (span) {
-        base = span[0];
-        if (set >= span[1] - base) return;
-    }
-    const int* S = sets + (size_t)(base + set) * stride;
     const int v = lane < stride && lane < KM ? S[lane] : -1;
     const unsigned long long bal = __ballot(v >= 0);
     const int k = __popcll(bal);
@@ -240,9 +231,9 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
     int npat = 1;
     for (int j = 0; j < k; j++) npat *= 3;
     int fc0 = -1, fc1 = -1;
-    if (forced) {
-        fc0 = forced[2 * set];
-        fc1 = forced[2 * set + 1];
+    if (fpair) {
+        fc0 = fpair[0];
+        fc1 = fpair[1];
     }
     double pit[KM + 1], pri[KM + 1];
 #pragma unroll
@@ -322,10 +313,10 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
         rr.nc1 = nc1;
         rr.score = smin;
         rr.npat = npatv;
-        srec[set] = rr;
-        if (score) score[set] = smin;
+        *so = rr;
+        if (sc) *sc = smin;
     }
-    if (lane < k && mrec) {
+    if (lane < k && mo) {
         Acc5 a;
         a.mP = GS;
         a.mS = Gll;
@@ -339,8 +330,26 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
         a.shared = vsh;
         a.sll = vsl;
         a.nsll = vns;
-        mrec[(size_t)set * stride + lane] = a;
+        mo[lane] = a;
     }
+}
+
+
+// span (optional, device [lo, hi)): block b evaluates set lo + b of `sets`, the
+// blocks past hi - lo exit (a batch whose size the device decided); outputs
+// stay indexed by b
+__global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restrict__ sets, int stride,
+                                                  const int* __restrict__ forced, SetRec* __restrict__ srec,
+                                                  Acc5* __restrict__ mrec, double* __restrict__ score,
+                                                  const int* __restrict__ span = nullptr) {
+    const int set = blockIdx.x;
+    int base = 0;
+    if (span) {
+        base = span[0];
+        if (set >= span[1] - base) return;
+    }
+    eval_set(P, sets + (size_t)(base + set) * stride, stride, forced ? forced + 2 * set : nullptr, srec + set,
+             mrec ? mrec + (size_t)set * stride : nullptr, score ? score + set : nullptr);
 }
 
 // Configs rows (psx_run_configs, postcal.cpp:400-714): every row is one union
@@ -1488,11 +1497,12 @@ int psx_warmup(int device) {
     hipError_t le = hipGetLastError();
     hipError_t se = hipDeviceSynchronize();
     hipFree(d);
-    // and the other translation units' device code (each its own code object),
-    // which Model setup and the first pass would otherwise load on first use
+    // and the device code of the Model setup and the exhaustive sweep (each
+    // translation unit its own code object), which the first create / pass would
+    // otherwise load on first use; the configs-file code object (hipcub's radix
+    // sort, the largest) loads on its first use only
     if (le == hipSuccess && se == hipSuccess &&
-        (psx::warm_module_setup() || psx::warm_module_sweep() || psx::warm_module_sweep3() ||
-         psx::warm_module_configs()))
+        (psx::warm_module_setup() || psx::warm_module_sweep() || psx::warm_module_sweep3()))
         return fail(PSX_EHIP, "warm-up: device code of a translation unit did not load");
     if (le != hipSuccess || se != hipSuccess)
         return fail(PSX_EHIP, std::string("warm-up: ") + hipGetErrorString(le != hipSuccess ? le : se));
@@ -1759,31 +1769,29 @@ int psx_run_configs(psx_engine* e, const int16_t* rows, int64_t n_rows, int32_t 
 // The walk is serial: each iteration samples the next configuration from all
 // neighbour scores with the reference's mt19937(12345) and libstdc++
 // discrete_distribution, in the reference's order (sss_postcal.cpp:296-343), so
-// that sampling stays on the host.  Everything else of an iteration runs as
-// three launches and one synchronisation:
-//   k_sss_nbd   one block: the neighbourhood of `cur` (swap ++ minus ++ plus,
-//               sss_postcal.cpp:20-99, 166-186) in the reference's order, each
-//               set looked up in a device open-addressing map (the reference's
-//               unordered_map<vector<int>, double>, postcal.h:43-56, 98), the
-//               unseen ones compacted into the batch in neighbour order (the
-//               unseen current configuration first, :195-202), null sets scored
-//               K + L0 on the spot (:463-499), this rank's slice of the batch
-//   k_eval_sets one wave per batch set of the slice: every pattern's L, the
-//               set's score (max |L| pattern, :624-626), records
-//   k_sss_post  a block per union SNP folds its records in batch order (the
-//               current configuration's members scan the batch; any other SNP
+// that sampling stays on the host.  Everything else of an iteration is two
+// launches and one synchronisation:
+//   k_sss_eval  one wave per item: the current configuration (item 0) and the
+//               neighbourhood swap ++ minus ++ plus (sss_postcal.cpp:20-99,
+//               166-186) in the reference's order; each wave builds its set,
+//               looks it up in a device open-addressing map (the reference's
+//               unordered_map<vector<int>, double>, postcal.h:43-56, 98), and
+//               evaluates it if unseen (every pattern's L, the set's score =
+//               its max |L| pattern, :624-626, its records); null sets score
+//               K + L0 (:463-499)
+//   k_sss_post  a block per union SNP folds its records in item order (the
+//               current configuration's members scan the items; any other SNP
 //               i is only in the swaps (cur \ {c_v}) + {i} and the plus set
-//               cur + {i}, at known neighbour indices), one block folds the set
+//               cur + {i}, at known item indices), one block folds the set
 //               records and null configurations into the scalars, and the rest
 //               insert the new scores into the map (:280-284) and write every
 //               neighbour's score (the sampling weights) to pinned host memory
 // With several ranks (psx_run_sss_sharded) each evaluates a contiguous slice of
-// the batch; the slices' scores and the ranks' normalisers are all-gathered by
+// the items; the slices' scores and the ranks' normalisers are all-gathered by
 // the caller's callback, then the insert runs on every rank with all scores.
 namespace {
 constexpr int kKeyBits = 21;  // a sorted set of <= 6 as two words of three (index + 1) fields
 constexpr int kKeyMaxU = (1 << kKeyBits) - 2;
-constexpr int kNbdThreads = 1024;
 
 struct MapEntry {
     unsigned long long lo, hi;
@@ -1877,80 +1885,46 @@ __device__ int nbd_row(const SssIter& it, int i, int* row) {
     return n;
 }
 
-// sizes written by k_sss_nbd (device ints)
-enum { kBatch = 0, kLo = 1, kHi = 2, kNulls = 3, kUnseen = 4, kNCnt = 8 };
+// iteration counters (device ints, copied to pinned host memory by k_sss_post)
+enum { kUnseen = 0, kNulls = 1, kCurPos = 2, kNCnt = 4 };
 
-__global__ __launch_bounds__(kNbdThreads) void k_sss_nbd(SssIter it, const MapEntry* __restrict__ T,
-                                                         unsigned long long mask, int* __restrict__ bsets,
-                                                         int* __restrict__ mark, int* __restrict__ cnt,
-                                                         double* __restrict__ lk_host) {
-    __shared__ int wsum[kNbdThreads / 64];
-    __shared__ int run_total;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    if (t == 0) run_total = 0;
-    int nulls = 0, unseen = 0;
-    __syncthreads();
-    for (int p0 = 0; p0 < it.n_nbd + 1; p0 += kNbdThreads) {
-        const int p = p0 + t, i = p - 1;  // item 0: the current configuration
-        int row[PSX_KMAX];
-        bool in_batch = false;
-        if (p < it.n_nbd + 1) {
-            const int n = nbd_row(it, i, row);
-            unsigned long long lo, hi;
-            pack_key(row, n, lo, hi);
-            double v;
-            const bool seen = map_find(T, mask, lo, hi, v);
-            if (i >= 0) {
-                if (seen) lk_host[i] = v;
-                mark[i] = seen ? -1 : (n == 0 ? -2 : 0);
-                unseen += !seen;
-            }
-            if (!seen) {
-                if (n == 0) nulls++;  // folded as null configurations, score K + L0
-                else in_batch = true;
-            }
-        }
-        // batch position: exclusive prefix in item order
-        const unsigned long long bal = __ballot(in_batch);
-        const int before = __popcll(bal & ((1ull << lane) - 1ull));
-        if (lane == 0) wsum[w] = __popcll(bal);
-        __syncthreads();
-        int off = run_total;
-        for (int q = 0; q < w; q++) off += wsum[q];
-        if (in_batch) {
-            const int bp = off + before;
-            for (int j = 0; j < it.stride; j++) bsets[(size_t)bp * it.stride + j] = row[j];
-            if (i >= 0) mark[i] = bp;
-        }
-        __syncthreads();
-        if (t == 0)
-            for (int q = 0; q < kNbdThreads / 64; q++) run_total += wsum[q];
-        __syncthreads();
-    }
-    // the chunk loop is uniform, so every thread reaches these reductions
-    for (int o = 32; o > 0; o >>= 1) {
-        nulls += __shfl_xor(nulls, o);
-        unseen += __shfl_xor(unseen, o);
-    }
-    __shared__ int sn[kNbdThreads / 64], su[kNbdThreads / 64];
+// item p of the iteration: the current configuration (p = 0, always evaluated
+// when unseen: sss_postcal.cpp:195-202) or neighbour i = p - 1.  mark[i]: -1
+// seen (its score is the map's), -2 an unseen null set, p an unseen set
+__global__ __launch_bounds__(64) void k_sss_eval(DevProb P, SssIter it, const MapEntry* __restrict__ T,
+                                                 unsigned long long mask, int lo, int hi, int* __restrict__ rows,
+                                                 int* __restrict__ mark, int* __restrict__ cnt,
+                                                 double* __restrict__ lk_host, SetRec* __restrict__ srec,
+                                                 Acc5* __restrict__ mrec, double* __restrict__ score) {
+    __shared__ int srow[PSX_KMAX];
+    const int p = blockIdx.x, i = p - 1, lane = threadIdx.x;
+    int row[PSX_KMAX];
+    const int n = nbd_row(it, i, row);
+    int seen = 0;
+    double v = 0.0;
     if (lane == 0) {
-        sn[w] = nulls;
-        su[w] = unseen;
-    }
-    __syncthreads();
-    if (t == 0) {
-        int a = 0, b = 0;
-        for (int q = 0; q < kNbdThreads / 64; q++) {
-            a += sn[q];
-            b += su[q];
+        unsigned long long klo, khi;
+        pack_key(row, n, klo, khi);
+        seen = map_find(T, mask, klo, khi, v) ? 1 : 0;
+        if (i >= 0) {
+            if (seen) lk_host[i] = v;
+            mark[i] = seen ? -1 : (n == 0 ? -2 : p);
+            if (!seen) atomicAdd(&cnt[kUnseen], 1);
+        } else {
+            cnt[kCurPos] = (seen || n == 0) ? -1 : 0;  // a null current configuration is counted, not evaluated
         }
-        const int nw = run_total;
-        cnt[kBatch] = nw;
-        cnt[kLo] = (int)((long long)nw * it.rank / it.world);
-        cnt[kHi] = (int)((long long)nw * (it.rank + 1) / it.world);
-        cnt[kNulls] = a;
-        cnt[kUnseen] = b;
+        if (!seen && n == 0) atomicAdd(&cnt[kNulls], 1);
     }
+    seen = __shfl(seen, 0);
+    if (seen || n == 0 || p < lo || p >= hi) return;
+#pragma unroll
+    for (int j = 0; j < PSX_KMAX; j++)
+        if (j < it.stride && lane == j) {
+            srow[j] = row[j];
+            rows[(size_t)p * it.stride + j] = row[j];
+        }
+    __syncthreads();
+    eval_set(P, srow, it.stride, nullptr, srec + p, mrec + (size_t)p * it.stride, score + p);
 }
 
 // member position of u in a sorted, -1 padded batch row (or -1)
@@ -1961,17 +1935,23 @@ __device__ inline int member_of(const int* row, int stride, int u) {
     return j;
 }
 
+// item p evaluated by this rank (its records exist)
+__device__ inline bool evaluated(const int* __restrict__ mark, const int* __restrict__ cnt, int p, int lo, int hi) {
+    if (p < lo || p >= hi) return false;
+    return p == 0 ? cnt[kCurPos] == 0 : mark[p - 1] == p;
+}
+
 // blocks [0, U): per-SNP record folds; block U: the scalars; blocks > U: the
 // map inserts and the sampling weights.  mode 0: folds only, 1: folds and
 // inserts, 2: inserts only (after the all-gather of a sharded walk)
-__global__ __launch_bounds__(256) void k_sss_post(SssIter it, const int* __restrict__ bsets,
+__global__ __launch_bounds__(256) void k_sss_post(SssIter it, int lo, int hi, const int* __restrict__ rows,
                                                   const int* __restrict__ mark, const int* __restrict__ cnt,
                                                   const Acc5* __restrict__ mrec, const SetRec* __restrict__ srec,
-                                                  const double* __restrict__ bscore, SetRec null1, Acc5* __restrict__ acc,
-                                                  SetRec* __restrict__ sacc, SetRec* __restrict__ sacc_host,
+                                                  const double* __restrict__ score, SetRec null1,
+                                                  Acc5* __restrict__ acc, SetRec* __restrict__ sacc,
+                                                  SetRec* __restrict__ sacc_host, int* __restrict__ cnt_host,
                                                   MapEntry* __restrict__ T, unsigned long long mask, int mode,
                                                   double* __restrict__ lk_host) {
-    const int lo = cnt[kLo], hi = cnt[kHi], n = hi - lo;
     const int b = blockIdx.x, t = threadIdx.x;
     if (mode == 2 && b <= it.U) return;
     if (b < it.U) {
@@ -1980,11 +1960,12 @@ __global__ __launch_bounds__(256) void k_sss_post(SssIter it, const int* __restr
         for (int j = 0; j < it.k; j++) in_cur |= it.cur[j] == u;
         Acc5 a = psx::acc_zero();
         if (in_cur) {
-            // in (nearly) every set of the batch: the slice's sets in batch order
-            for (int q = t; q < n; q += 256) {
-                const int j = member_of(bsets + (size_t)(lo + q) * it.stride, it.stride, u);
-                if (j >= 0) psx::fold_acc(a, mrec[(size_t)q * it.stride + j]);
-            }
+            // in (nearly) every item: the slice's evaluated items in item order
+            for (int p = lo + t; p < hi; p += 256)
+                if (evaluated(mark, cnt, p, lo, hi)) {
+                    const int j = member_of(rows + (size_t)p * it.stride, it.stride, u);
+                    if (j >= 0) psx::fold_acc(a, mrec[(size_t)p * it.stride + j]);
+                }
             __shared__ Acc5 sh[4];
             psx::wave_fold_acc(a);
             if ((t & 63) == 0) sh[t >> 6] = a;
@@ -1997,7 +1978,7 @@ __global__ __launch_bounds__(256) void k_sss_post(SssIter it, const int* __restr
             return;
         }
         if (t != 0) return;
-        // u is the ri-th SNP outside cur: swaps ri * k + v, then the plus set
+        // u is the ri-th SNP outside cur: neighbours ri * k + v, then its plus set
         int ri = u;
         for (int j = 0; j < it.k; j++) ri -= it.cur[j] < u;
         bool any = false;
@@ -2006,10 +1987,10 @@ __global__ __launch_bounds__(256) void k_sss_post(SssIter it, const int* __restr
             if (v < it.k) i = ri * it.k + v;
             else if (it.num_plus) i = it.num_zero + it.num_minus + ri;
             else break;
-            const int bp = mark[i];
-            if (bp < lo || bp >= hi) continue;  // seen, null, or another rank's
-            const int j = member_of(bsets + (size_t)bp * it.stride, it.stride, u);
-            psx::fold_acc(a, mrec[(size_t)(bp - lo) * it.stride + j]);
+            const int p = i + 1;
+            if (!evaluated(mark, cnt, p, lo, hi)) continue;  // seen, null, or another rank's
+            const int j = member_of(rows + (size_t)p * it.stride, it.stride, u);
+            psx::fold_acc(a, mrec[(size_t)p * it.stride + j]);
             any = true;
         }
         if (any) {
@@ -2021,7 +2002,8 @@ __global__ __launch_bounds__(256) void k_sss_post(SssIter it, const int* __restr
     }
     if (b == it.U) {  // the scalars: the slice's set records, then the null configurations (rank 0)
         SetRec a = psx::set_zero();
-        for (int q = t; q < n; q += 256) psx::fold_set(a, srec[q]);
+        for (int p = lo + t; p < hi; p += 256)
+            if (evaluated(mark, cnt, p, lo, hi)) psx::fold_set(a, srec[p]);
         __shared__ SetRec ss[4];
         psx::wave_fold_set(a);
         if ((t & 63) == 0) ss[t >> 6] = a;
@@ -2040,6 +2022,7 @@ __global__ __launch_bounds__(256) void k_sss_post(SssIter it, const int* __restr
             }
             *sacc = g;
             *sacc_host = g;
+            for (int q = 0; q < kNCnt; q++) cnt_host[q] = cnt[q];
         }
         return;
     }
@@ -2047,8 +2030,8 @@ __global__ __launch_bounds__(256) void k_sss_post(SssIter it, const int* __restr
     const int i = (b - it.U - 1) * 256 + t;
     if (i >= it.n_nbd) return;
     const int mk = mark[i];
-    if (mk == -1) return;  // seen: its weight was written by k_sss_nbd
-    const double v = mk == -2 ? it.null_score : bscore[mk];
+    if (mk == -1) return;  // seen: its weight was written by k_sss_eval
+    const double v = mk == -2 ? it.null_score : score[mk];
     int row[PSX_KMAX];
     const int nr = nbd_row(it, i, row);
     unsigned long long klo, khi;
@@ -2064,30 +2047,23 @@ __global__ void k_map_rehash(const MapEntry* __restrict__ old, size_t n, MapEntr
     if (i < n && old[i].state) map_insert(T, mask, old[i].lo, old[i].hi, old[i].score);
 }
 
-// scores of the slice, batch-indexed, into the gather buffer (world > 1)
-__global__ void k_copy_scores(const double* __restrict__ s, const int* __restrict__ cnt, double* __restrict__ out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < cnt[kHi] - cnt[kLo]) out[i] = s[i];
-}
-
 struct SssDev {
     MapEntry* T = nullptr;
     size_t cap = 0, used = 0;
-    int* bsets = nullptr;
-    int* mark = nullptr;
+    int* rows = nullptr;      // per item: its set (evaluated items)
+    int* mark = nullptr;      // per neighbour: -1 seen, -2 unseen null, else its item
     int* cnt = nullptr;
-    double* bscore = nullptr;
-    size_t cap_n = 0;
+    double* full = nullptr;   // per item: every rank's scores (world > 1)
     double* lk = nullptr;     // pinned host: every neighbour's score
     SetRec* shost = nullptr;  // pinned host: the scalars after the iteration
-    int* hcnt = nullptr;      // pinned host: the sizes
-    double* hscore = nullptr; // pinned host: gathered batch scores (world > 1)
+    int* hcnt = nullptr;      // pinned host: the counters
+    double* hscore = nullptr; // pinned host: gathered item scores (world > 1)
     ~SssDev() {
         hipFree(T);
-        hipFree(bsets);
+        hipFree(rows);
         hipFree(mark);
         hipFree(cnt);
-        hipFree(bscore);
+        hipFree(full);
         if (lk) hipHostFree(lk);
         if (shost) hipHostFree(shost);
         if (hcnt) hipHostFree(hcnt);
@@ -2105,26 +2081,28 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
     if (C > PSX_KMAX) return fail(PSX_ERANGE, "SSS max_causal > 6");
     if (U > kKeyMaxU) return fail(PSX_ERANGE, "SSS: more union SNPs than the set key holds");
     const int stride = std::max(C, 1);
-    // the largest neighbourhood: k = C (swaps C (U - C), minus C) or k = C - 1 (plus)
-    const size_t nmax = (size_t)C * U + C + U + 1;
+    // the most items of an iteration: the current configuration + the largest
+    // neighbourhood (k = C: swaps C (U - C), minus C; k < C: + U - k plus sets)
+    const size_t nmax = (size_t)C * U + C + U + 2;
     SssDev D;
     size_t cap = 1 << 16;
     while (cap < 4 * nmax) cap <<= 1;
     HIPCHK(hipMalloc(&D.T, cap * sizeof(MapEntry)));
     HIPCHK(hipMemsetAsync(D.T, 0, cap * sizeof(MapEntry), e->stream));
     D.cap = cap;
-    HIPCHK(hipMalloc(&D.bsets, nmax * stride * sizeof(int)));
+    HIPCHK(hipMalloc(&D.rows, nmax * stride * sizeof(int)));
     HIPCHK(hipMalloc(&D.mark, nmax * sizeof(int)));
     HIPCHK(hipMalloc(&D.cnt, kNCnt * sizeof(int)));
-    HIPCHK(hipMalloc(&D.bscore, nmax * sizeof(double)));
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.lk), nmax * sizeof(double)));
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.shost), sizeof(SetRec)));
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hcnt), kNCnt * sizeof(int)));
-    if (world > 1) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hscore), nmax * sizeof(double)));
-    int ret;
-    if ((ret = ensure(e->dsrec, e->cap_srec, nmax))) return ret;
-    if ((ret = ensure(e->dmrec, e->cap_mrec, nmax * stride))) return ret;
-    if ((ret = ensure(e->dscore, e->cap_score, nmax))) return ret;
+    if (world > 1) {
+        HIPCHK(hipMalloc(&D.full, nmax * sizeof(double)));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hscore), nmax * sizeof(double)));
+    }
+    if ((rc = ensure(e->dsrec, e->cap_srec, nmax))) return rc;
+    if ((rc = ensure(e->dmrec, e->cap_mrec, nmax * stride))) return rc;
+    if ((rc = ensure(e->dscore, e->cap_score, nmax))) return rc;
     const SetRec null1 = null_rec(e, 1.0);
     std::mt19937 gen(12345);
     int cur[PSX_KMAX] = {0, 0, 0, 0, 0, 0}, k = 0;  // the current configuration, ascending
@@ -2146,7 +2124,9 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
         it.rank = rank;
         it.world = world;
         it.null_score = e->K + e->L0;
-        const int n_nbd = it.n_nbd;
+        const int n_nbd = it.n_nbd, n_items = n_nbd + 1;
+        // this rank's contiguous slice of the items
+        const int lo = (int)((int64_t)n_items * rank / world), hi = (int)((int64_t)n_items * (rank + 1) / world);
         // the map stays at load <= 1/2 (every neighbour may be new)
         if (2 * (D.used + (size_t)n_nbd + 1) > D.cap) {
             size_t nc = D.cap;
@@ -2163,61 +2143,56 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
             D.cap = nc;
         }
         const unsigned long long mask = D.cap - 1;
-        hipLaunchKernelGGL(k_sss_nbd, dim3(1), dim3(kNbdThreads), 0, e->stream, it, D.T, mask, D.bsets, D.mark, D.cnt,
-                           D.lk);
+        HIPCHK(hipMemsetAsync(D.cnt, 0, kNCnt * sizeof(int), e->stream));
         HIPCHK(hipEventRecord(e->ev[2], e->stream));
-        hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)(n_nbd + 1)), dim3(64), 0, e->stream, e->dp, D.bsets, stride,
-                           (const int*)nullptr, e->dsrec, e->dmrec, e->dscore, (const int*)(D.cnt + kLo));
+        hipLaunchKernelGGL(k_sss_eval, dim3((unsigned)n_items), dim3(64), 0, e->stream, e->dp, it, D.T, mask, lo, hi,
+                           D.rows, D.mark, D.cnt, D.lk, e->dsrec, e->dmrec, e->dscore);
         HIPCHK(hipEventRecord(e->ev[3], e->stream));
         const unsigned post_blocks = (unsigned)(U + 1 + (world == 1 ? (n_nbd + 255) / 256 : 0));
-        hipLaunchKernelGGL(k_sss_post, dim3(post_blocks), dim3(256), 0, e->stream, it, D.bsets, D.mark, D.cnt, e->dmrec,
-                           e->dsrec, e->dscore, null1, e->dacc, e->dsacc, D.shost, D.T, mask, world == 1 ? 1 : 0,
-                           D.lk);
+        hipLaunchKernelGGL(k_sss_post, dim3(post_blocks), dim3(256), 0, e->stream, it, lo, hi, D.rows, D.mark, D.cnt,
+                           e->dmrec, e->dsrec, e->dscore, null1, e->dacc, e->dsacc, D.shost, D.hcnt, D.T, mask,
+                           world == 1 ? 1 : 0, D.lk);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(D.hcnt, D.cnt, kNCnt * sizeof(int), hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
         {
             float ms = 0;
             HIPCHK(hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
             kms += ms;
         }
-        const int nw = D.hcnt[kBatch], unseen = D.hcnt[kUnseen];
+        const int unseen = D.hcnt[kUnseen];
         double sss_sum;
         if (world == 1) {
             sss_sum = logval(e, D.shost->m, D.shost->tot);
         } else {
-            // one all-gather: [slice length, normaliser (m, s), slice scores]; then every
-            // rank inserts all scores (batch order) and writes the sampling weights
-            const int lo = D.hcnt[kLo], hi = D.hcnt[kHi];
-            const size_t per = ((size_t)nw + world - 1) / world, wd = 3 + per;
+            // one all-gather: [normaliser (m, s), the slice's item scores]; then
+            // every rank inserts all scores and writes the sampling weights
+            const size_t per = ((size_t)n_items + world - 1) / world, wd = 2 + per;
             std::vector<double> snd(wd, 0.0), rcv(wd * world, 0.0);
             if (hi > lo)
-                HIPCHK(hipMemcpy(snd.data() + 3, e->dscore, (size_t)(hi - lo) * sizeof(double), hipMemcpyDeviceToHost));
-            snd[0] = (double)(hi - lo);
-            snd[1] = (double)D.shost->m;
-            snd[2] = D.shost->tot;
+                HIPCHK(hipMemcpy(snd.data() + 2, e->dscore + lo, (size_t)(hi - lo) * sizeof(double),
+                                 hipMemcpyDeviceToHost));
+            snd[0] = (double)D.shost->m;
+            snd[1] = D.shost->tot;
             if (allgather(ctx, snd.data(), rcv.data(), (int64_t)(wd * sizeof(double))))
                 return fail(PSX_EEXCHANGE, "SSS all-gather callback failed");
             double mx = -INFINITY;
             std::vector<double> part(world, 0.0);
             for (int r = 0; r < world; r++) {
                 const double* q = rcv.data() + (size_t)r * wd;
-                const size_t rlo = (size_t)nw * r / world, rn = (size_t)nw * (r + 1) / world - rlo;
-                if ((size_t)q[0] != rn) return fail(PSX_EEXCHANGE, "SSS all-gather: ranks disagree on the batch");
-                std::copy(q + 3, q + 3 + rn, D.hscore + rlo);
-                part[r] = logval(e, (int32_t)q[1], q[2]);
+                const size_t rlo = (size_t)n_items * r / world, rn = (size_t)n_items * (r + 1) / world - rlo;
+                std::copy(q + 2, q + 2 + rn, D.hscore + rlo);
+                part[r] = logval(e, (int32_t)q[0], q[1]);
                 if (part[r] != 0.0) mx = std::max(mx, part[r]);
             }
             double acc = 0.0;  // the ranks' normalisers, combined in rank order
             for (int r = 0; r < world; r++)
                 if (part[r] != 0.0) acc += std::exp(part[r] - mx);
             sss_sum = acc > 0 ? mx + std::log(acc) : 0.0;
-            if (nw > 0) HIPCHK(hipMemcpyAsync(D.bscore, D.hscore, (size_t)nw * sizeof(double), hipMemcpyHostToDevice,
-                                              e->stream));
-            // the insert blocks alone (block indices past U + 1)
+            HIPCHK(hipMemcpyAsync(D.full, D.hscore, (size_t)n_items * sizeof(double), hipMemcpyHostToDevice, e->stream));
+            // the insert blocks alone (block indices past U)
             hipLaunchKernelGGL(k_sss_post, dim3((unsigned)(U + 1 + (n_nbd + 255) / 256)), dim3(256), 0, e->stream, it,
-                               D.bsets, D.mark, D.cnt, e->dmrec, e->dsrec, D.bscore, null1, (Acc5*)nullptr,
-                               (SetRec*)nullptr, (SetRec*)nullptr, D.T, mask, 2, D.lk);
+                               lo, hi, D.rows, D.mark, D.cnt, e->dmrec, e->dsrec, D.full, null1, (Acc5*)nullptr,
+                               (SetRec*)nullptr, (SetRec*)nullptr, (int*)nullptr, D.T, mask, 2, D.lk);
             HIPCHK(hipGetLastError());
             HIPCHK(hipStreamSynchronize(e->stream));
         }
