@@ -40,7 +40,8 @@ struct CfgWork {
     size_t cap_blk = 0;            // ints
     int* ptr = nullptr;            // per union SNP: record counts, then the CSR row pointer (U + 1)
     size_t cap_ptr = 0;
-    unsigned long long* status = nullptr;  // [0] first failing row << 3 | code, [1] nulls, [2] sets, [3] records
+    unsigned long long* status = nullptr;  // [0] first failing row << 3 | code, [1] nulls, [2] sets, [3] records,
+                                           // [4] most records of one union SNP
     SetRec* srec = nullptr;        // per evaluated row: scalars
     void* rrec = nullptr;          // per evaluated row: weights of its one assignment
     int* masks = nullptr;          // per evaluated row: c0 | c1 << 8
@@ -50,6 +51,8 @@ struct CfgWork {
     size_t cap_rec = 0;
     void* sort_tmp = nullptr;
     size_t cap_sort = 0;
+    void* parts = nullptr;         // two-level folds: per (union SNP, slice) Acc5, then per block SetRec
+    size_t cap_parts = 0;          // bytes
     unsigned long long* hstatus = nullptr;  // pinned host copy of status
     char* hpin = nullptr;                   // pinned staging of the upload: two chunks
     hipEvent_t dma[2] = {nullptr, nullptr};  // the chunks' copies out of hpin

@@ -21,12 +21,20 @@
 //                at offsets fixed by row order
 //   radix sort   (hipcub, stable) member records by union SNP: the CSR's record
 //                order within an SNP is row order, as the host pass built it
-//   k_cfg_merge  a block per union SNP folds its records in that order; the
-//                records themselves are rebuilt from the row's weights and
-//                its assignment masks (no 56-byte record per member in HBM)
+//   k_cfg_merge  per union SNP, its records in that order, folded in two levels:
+//                S contiguous slices of the SNP's run by one block each, then
+//                the S partials in slice order (a file's records concentrate on
+//                the few SNPs its groups name: one block per SNP left the GPU
+//                idle for ~3 ms on 29M records, r03e); the records themselves
+//                are rebuilt from the row's weights and its assignment masks
+//                (no 56-byte record per member in HBM)
+//   k_cfg_sets   the set records folded the same way: contiguous chunks, then
+//                the chunk partials in order (the one-block fold took 6 ms on
+//                4.8M rows)
 //
-// plus the existing set-record fold.  Results are bit-identical to the host
-// pre-pass it replaces (same per-SNP fold order, same arithmetic).
+// Every fold order is fixed by the row order and the launch shapes, so the
+// results are deterministic (and within rounding of the host pre-pass this
+// replaced).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <sched.h>
@@ -227,6 +235,9 @@ __device__ long block_scan_inplace(int* a, int n) {
 
 __global__ __launch_bounds__(1024) void k_cfg_scan(int* __restrict__ blk, int nblk, int* __restrict__ ptr, int U,
                                                    unsigned long long* __restrict__ status) {
+    unsigned long long mx = 0;  // the most records of one union SNP (sizes the member fold's slices)
+    for (int u = threadIdx.x; u < U; u += 1024) mx = max(mx, (unsigned long long)ptr[u]);
+    if (mx) atomicMax(&status[4], mx);
     const long sets = block_scan_inplace(blk, nblk);
     const long recs = block_scan_inplace(blk + nblk, nblk);
     const long recs2 = block_scan_inplace(ptr, U);
@@ -329,15 +340,19 @@ __device__ __forceinline__ Acc5 cfg_record(const CfgRow* __restrict__ rrec, cons
 
 // per union SNP u, its records in CSR order (row order), folded as
 // k_merge_members (psx_sweep.hip) folds gathered records: 256 threads, eight
-// loads in flight per thread, then the wave / block trees, then into acc[u]
+// loads in flight per thread, then the wave / block trees.  Level 1: block
+// (u, s) folds slice s of S of u's run into parts[u * S + s]; level 2 (one
+// thread per SNP) folds the S partials in slice order into acc[u].
 constexpr int kMergeR = 8;
+constexpr int kSliceRecs = 8192;  // records per level-1 slice (S = ceil(most / kSliceRecs))
+constexpr int kMaxSlices = 256;
 __global__ __launch_bounds__(256) void k_cfg_merge(const CfgRow* __restrict__ rrec, const int* __restrict__ masks,
-                                                   const int* __restrict__ ptr, const int* __restrict__ idx,
-                                                   Acc5* __restrict__ acc) {
+                                                   const int* __restrict__ ptr, const int* __restrict__ idx, int S,
+                                                   Acc5* __restrict__ parts) {
     __shared__ Acc5 sh[4];
-    const int u = blockIdx.x;
-    const int b = ptr[u], e = ptr[u + 1];
-    if (b == e) return;
+    const int u = blockIdx.x, sl = blockIdx.y;
+    const long b0 = ptr[u], len = ptr[u + 1] - b0;
+    const int b = (int)(b0 + len * sl / S), e = (int)(b0 + len * (sl + 1) / S);
     Acc5 a = acc_zero();
     for (int i0 = b + (int)threadIdx.x; i0 < e; i0 += 256 * kMergeR) {
         int ix[kMergeR];
@@ -353,9 +368,43 @@ __global__ __launch_bounds__(256) void k_cfg_merge(const CfgRow* __restrict__ rr
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = a;
     __syncthreads();
     if (threadIdx.x == 0) {
-        Acc5 g = acc[u];
+        Acc5 g = acc_zero();
         for (int w = 0; w < 4; w++) fold_acc(g, sh[w]);
-        acc[u] = g;
+        parts[(size_t)u * S + sl] = g;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_cfg_merge2(const Acc5* __restrict__ parts, int S, int U,
+                                                   Acc5* __restrict__ acc) {
+    const int u = blockIdx.x * 64 + threadIdx.x;
+    if (u >= U) return;
+    Acc5 g = acc[u];
+    for (int sl = 0; sl < S; sl++) fold_acc(g, parts[(size_t)u * S + sl]);
+    acc[u] = g;
+}
+
+// the set records: block b folds chunk b (contiguous, row order) into parts[b]
+constexpr int kSetChunk = 4096;
+constexpr int kMaxSetChunks = 2048;
+__global__ __launch_bounds__(256) void k_cfg_sets(const SetRec* __restrict__ rec, long n, long chunk,
+                                                  SetRec* __restrict__ parts) {
+    __shared__ SetRec sh[4];
+    const long b = (long)blockIdx.x * chunk, e = min(n, b + chunk);
+    SetRec a = set_zero();
+    for (long i0 = b + threadIdx.x; i0 < e; i0 += 256 * kMergeR) {
+        SetRec v[kMergeR];
+#pragma unroll
+        for (int q = 0; q < kMergeR; q++) v[q] = i0 + 256 * q < e ? rec[i0 + 256 * q] : set_zero();
+#pragma unroll
+        for (int q = 0; q < kMergeR; q++) fold_set(a, v[q]);
+    }
+    wave_fold_set(a);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        SetRec g = set_zero();
+        for (int w = 0; w < 4; w++) fold_set(g, sh[w]);
+        parts[blockIdx.x] = g;
     }
 }
 
@@ -440,13 +489,13 @@ int configs_pass(CfgWork& W, const int16_t* rows, int64_t n_rows, int n_groups, 
     if (!grow(W.rows, W.cap_rows, nel) || !grow(W.blk, W.cap_blk, 2 * (size_t)nblk) ||
         !grow(W.ptr, W.cap_ptr, (size_t)C.U + 1))
         return bad("out of device memory (configs rows)");
-    if (!W.status && hipMalloc(&W.status, 4 * sizeof(unsigned long long)) != hipSuccess)
+    if (!W.status && hipMalloc(&W.status, 5 * sizeof(unsigned long long)) != hipSuccess)
         return bad("out of device memory");
-    if (!W.hstatus && hipHostMalloc(&W.hstatus, 4 * sizeof(unsigned long long)) != hipSuccess)
+    if (!W.hstatus && hipHostMalloc(&W.hstatus, 5 * sizeof(unsigned long long)) != hipSuccess)
         return bad("out of pinned host memory");
     if (upload_rows(W, rows, nel * sizeof(int16_t), W.rows, st) ||
         hipMemsetAsync(W.status, 0xff, sizeof(unsigned long long), st) != hipSuccess ||
-        hipMemsetAsync(W.status + 1, 0, 3 * sizeof(unsigned long long), st) != hipSuccess ||
+        hipMemsetAsync(W.status + 1, 0, 4 * sizeof(unsigned long long), st) != hipSuccess ||
         hipMemsetAsync(W.ptr, 0, ((size_t)C.U + 1) * sizeof(int), st) != hipSuccess)
         return bad("configs upload");
     const int lds = C.U <= kLdsHistMax ? 1 : 0;
@@ -454,7 +503,7 @@ int configs_pass(CfgWork& W, const int16_t* rows, int64_t n_rows, int n_groups, 
                        W.rows, (long)n_rows, n_groups, C, (long)r0, (long)r1, W.status, W.blk, (int)nblk, W.ptr, lds);
     hipLaunchKernelGGL(k_cfg_scan, dim3(1), dim3(1024), 0, st, W.blk, (int)nblk, W.ptr, C.U, W.status);
     if (hipGetLastError() != hipSuccess) return bad("configs count launch");
-    if (hipMemcpyAsync(W.hstatus, W.status, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st) != hipSuccess ||
+    if (hipMemcpyAsync(W.hstatus, W.status, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return bad("configs status");
     const unsigned long long f = W.hstatus[0];
@@ -468,6 +517,19 @@ int configs_pass(CfgWork& W, const int16_t* rows, int64_t n_rows, int n_groups, 
     out->nrec = (int64_t)W.hstatus[3];
     const size_t ns = (size_t)out->nsets, nr = (size_t)out->nrec;
     if (ns == 0) return 0;
+    // level-1 shapes of the two folds and their partials buffer
+    const int S = (int)std::min<unsigned long long>(kMaxSlices, std::max<unsigned long long>(1, (W.hstatus[4] + kSliceRecs - 1) / kSliceRecs));
+    long chunk = kSetChunk;
+    while ((long)((ns + chunk - 1) / chunk) > kMaxSetChunks) chunk *= 2;
+    const int nchunk = (int)((ns + chunk - 1) / chunk);
+    const size_t need = std::max((size_t)C.U * S * sizeof(Acc5), (size_t)nchunk * sizeof(SetRec));
+    if (need > W.cap_parts) {
+        hipFree(W.parts);
+        W.parts = nullptr;
+        W.cap_parts = 0;
+        if (hipMalloc(&W.parts, need) != hipSuccess) return bad("out of device memory (configs folds)");
+        W.cap_parts = need;
+    }
     if (ns > W.cap_sets) {
         hipFree(W.srec);
         hipFree(W.rrec);
@@ -518,10 +580,15 @@ int configs_pass(CfgWork& W, const int16_t* rows, int64_t n_rows, int n_groups, 
     if (hipcub::DeviceRadixSort::SortPairs(W.sort_tmp, tmp2, W.keys, keys_out, W.vals, vals_out, (int)nr, 0, end_bit,
                                            st) != hipSuccess)
         return bad("configs sort");
-    hipLaunchKernelGGL(k_cfg_merge, dim3((unsigned)C.U), dim3(256), 0, st, (const CfgRow*)W.rrec, W.masks, W.ptr,
-                       vals_out, acc);
+    hipLaunchKernelGGL(k_cfg_merge, dim3((unsigned)C.U, (unsigned)S), dim3(256), 0, st, (const CfgRow*)W.rrec,
+                       W.masks, W.ptr, vals_out, S, (Acc5*)W.parts);
+    hipLaunchKernelGGL(k_cfg_merge2, dim3((unsigned)((C.U + 63) / 64)), dim3(64), 0, st, (const Acc5*)W.parts, S, C.U,
+                       acc);
     if (hipGetLastError() != hipSuccess) return bad("configs merge launch");
-    if (launch_merge_sets(W.srec, (long)ns, set_zero(), sacc, st)) return bad("configs set merge");
+    // the set records (the partials buffer is free again: same stream)
+    hipLaunchKernelGGL(k_cfg_sets, dim3((unsigned)nchunk), dim3(256), 0, st, W.srec, (long)ns, chunk, (SetRec*)W.parts);
+    if (hipGetLastError() != hipSuccess) return bad("configs set fold launch");
+    if (launch_merge_sets((const SetRec*)W.parts, (long)nchunk, set_zero(), sacc, st)) return bad("configs set merge");
     return 0;
 }
 
@@ -536,6 +603,7 @@ void configs_free(CfgWork& W) {
     hipFree(W.keys);
     hipFree(W.vals);
     hipFree(W.sort_tmp);
+    hipFree(W.parts);
     if (W.hstatus) hipHostFree(W.hstatus);
     for (int b = 0; b < 2; b++)
         if (W.dma[b]) hipEventDestroy(W.dma[b]);

@@ -4,6 +4,7 @@
 // sss_postcal.cpp:102-685) with HIP kernels.  See DESIGN.md for the data layout
 // and the kernel inventory; psx_math.h for the accumulator representation.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <chrono>
@@ -18,6 +19,8 @@
 #include <tuple>
 #include <vector>
 #include <thread>
+#include <atomic>
+#include <sched.h>
 
 #include "../../include/pipsort_engine.h"
 #include "../../include/pipsort_model.h"
@@ -179,7 +182,7 @@ __device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride
     if (lane < nsub) {
 #pragma unroll
         for (int s = 0; s < 2; s++) {
-            double L[KM][KM], D[KM], w[KM];
+            double L[KM][KM], D[KM], Rd[KM], w[KM];
             double q = 0.0, Pd = 1.0;
 #pragma unroll
             for (int i = 0; i < KM; i++) {
@@ -191,7 +194,7 @@ __device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride
 #pragma unroll
                     for (int m = 0; m < j; m++) acc -= L[i][m] * L[j][m] * D[m];
                     // L[j][*] = 0 and D[j] = 1 for j outside the subset
-                    L[i][j] = in && ((lane >> j) & 1) ? acc / D[j] : 0.0;
+                    L[i][j] = in && ((lane >> j) & 1) ? acc * Rd[j] : 0.0;
                 }
                 if (in) {
                     di = s_ad[s][i];
@@ -201,7 +204,12 @@ __device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride
                         di -= L[i][m] * L[i][m] * D[m];
                         wi -= L[i][m] * w[m];
                     }
-                    q += wi * wi / di;
+                }
+                // one division per pivot (ldlt_terms' rounding): the L entries
+                // below it and the quadratic form multiply by its reciprocal
+                Rd[i] = 1.0 / di;
+                if (in) {
+                    q += wi * wi * Rd[i];
                     Pd *= P.dval[s] * di;
                 }
                 D[i] = di;
@@ -1789,6 +1797,8 @@ int psx_run_configs(psx_engine* e, const int16_t* rows, int64_t n_rows, int32_t 
 // With several ranks (psx_run_sss_sharded) each evaluates a contiguous slice of
 // the items; the slices' scores and the ranks' normalisers are all-gathered by
 // the caller's callback, then the insert runs on every rank with all scores.
+extern "C" __device__ __attribute__((const)) int __ockl_wfred_add_i32(int);
+
 namespace {
 constexpr int kKeyBits = 21;  // a sorted set of <= 6 as two words of three (index + 1) fields
 constexpr int kKeyMaxU = (1 << kKeyBits) - 2;
@@ -1809,15 +1819,25 @@ __host__ __device__ inline unsigned long long mix64(unsigned long long x) {
 __device__ inline unsigned long long map_slot(unsigned long long lo, unsigned long long hi, unsigned long long mask) {
     return mix64(lo ^ mix64(hi + 0x9e3779b97f4a7c15ULL)) & mask;
 }
-__device__ inline bool map_find(const MapEntry* T, unsigned long long mask, unsigned long long lo,
-                                unsigned long long hi, double& v) {
-    for (unsigned long long i = map_slot(lo, hi, mask);; i = (i + 1) & mask) {
-        const MapEntry& e = T[i];
-        if (e.state == 0) return false;
-        if (e.lo == lo && e.hi == hi) {
-            v = e.score;
+// Lookup of a key (linear probing) by a whole wave: 64 consecutive probe slots
+// per round trip (the table stays at load <= 1/2, so the first window nearly
+// always holds an empty slot); the key's slot is the first in probe order that
+// is empty or matches, as a serial probe would find it.  Result in every lane.
+__device__ inline bool map_find_wave(const MapEntry* T, unsigned long long mask, unsigned long long lo,
+                                     unsigned long long hi, double& v) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long base = map_slot(lo, hi, mask);
+    for (unsigned long long off = 0;; off += 64) {
+        const MapEntry& e = T[(base + off + lane) & mask];
+        const bool empty = e.state == 0;
+        const bool match = !empty && e.lo == lo && e.hi == hi;
+        const unsigned long long me = __ballot(empty), mm = __ballot(match);
+        const unsigned long long before = me ? (me & (0ull - me)) - 1ull : ~0ull;  // lanes below the first empty
+        if (mm & before) {
+            v = __shfl(e.score, __ffsll((long long)(mm & before)) - 1);
             return true;
         }
+        if (me) return false;
     }
 }
 // keys inserted by one launch are distinct and no lookup runs beside an insert
@@ -1885,8 +1905,12 @@ __device__ int nbd_row(const SssIter& it, int i, int* row) {
     return n;
 }
 
-// iteration counters (device ints, copied to pinned host memory by k_sss_post)
-enum { kUnseen = 0, kNulls = 1, kCurPos = 2, kNCnt = 4 };
+// iteration counters: k_sss_eval's block 0 writes the current configuration's
+// two (kCurPos: 0 if it is evaluated, else -1; kCurNull: 1 if it is an unseen
+// null configuration), k_sss_post's scalar block counts the unseen neighbours
+// and null configurations from mark[] (no contended atomics in the eval) and
+// copies all four to pinned host memory
+enum { kUnseen = 0, kNulls = 1, kCurPos = 2, kCurNull = 3, kNCnt = 4 };
 
 // item p of the iteration: the current configuration (p = 0, always evaluated
 // when unseen: sss_postcal.cpp:195-202) or neighbour i = p - 1.  mark[i]: -1
@@ -1895,27 +1919,30 @@ __global__ __launch_bounds__(64) void k_sss_eval(DevProb P, SssIter it, const Ma
                                                  unsigned long long mask, int lo, int hi, int* __restrict__ rows,
                                                  int* __restrict__ mark, int* __restrict__ cnt,
                                                  double* __restrict__ lk_host, SetRec* __restrict__ srec,
-                                                 Acc5* __restrict__ mrec, double* __restrict__ score) {
+                                                 Acc5* __restrict__ mrec, double* __restrict__ score,
+                                                 int* __restrict__ mark_host) {
     __shared__ int srow[PSX_KMAX];
     const int p = blockIdx.x, i = p - 1, lane = threadIdx.x;
     int row[PSX_KMAX];
     const int n = nbd_row(it, i, row);
-    int seen = 0;
     double v = 0.0;
+    unsigned long long klo, khi;
+    pack_key(row, n, klo, khi);
+    const int seen = map_find_wave(T, mask, klo, khi, v) ? 1 : 0;
     if (lane == 0) {
-        unsigned long long klo, khi;
-        pack_key(row, n, klo, khi);
-        seen = map_find(T, mask, klo, khi, v) ? 1 : 0;
         if (i >= 0) {
+            const int mk = seen ? -1 : (n == 0 ? -2 : p);
+            mark[i] = mk;
             if (seen) lk_host[i] = v;
-            mark[i] = seen ? -1 : (n == 0 ? -2 : p);
-            if (!seen) atomicAdd(&cnt[kUnseen], 1);
+            if (mark_host) {  // one rank: every item's weight and mark go to the host from here
+                mark_host[i] = mk;
+                if (mk == -2) lk_host[i] = it.null_score;
+            }
         } else {
             cnt[kCurPos] = (seen || n == 0) ? -1 : 0;  // a null current configuration is counted, not evaluated
+            cnt[kCurNull] = (!seen && n == 0) ? 1 : 0;
         }
-        if (!seen && n == 0) atomicAdd(&cnt[kNulls], 1);
     }
-    seen = __shfl(seen, 0);
     if (seen || n == 0 || p < lo || p >= hi) return;
 #pragma unroll
     for (int j = 0; j < PSX_KMAX; j++)
@@ -1925,6 +1952,7 @@ __global__ __launch_bounds__(64) void k_sss_eval(DevProb P, SssIter it, const Ma
         }
     __syncthreads();
     eval_set(P, srow, it.stride, nullptr, srec + p, mrec + (size_t)p * it.stride, score + p);
+    if (mark_host && lane == 0 && i >= 0) lk_host[i] = score[p];  // the lane that wrote it
 }
 
 // member position of u in a sorted, -1 padded batch row (or -1)
@@ -2002,16 +2030,30 @@ __global__ __launch_bounds__(256) void k_sss_post(SssIter it, int lo, int hi, co
     }
     if (b == it.U) {  // the scalars: the slice's set records, then the null configurations (rank 0)
         SetRec a = psx::set_zero();
+        int nu = 0, nz = 0;  // unseen neighbours, unseen null neighbours
         for (int p = lo + t; p < hi; p += 256)
             if (evaluated(mark, cnt, p, lo, hi)) psx::fold_set(a, srec[p]);
+        for (int i = t; i < it.n_nbd; i += 256) {
+            const int mk = mark[i];
+            nu += mk != -1;
+            nz += mk == -2;
+        }
         __shared__ SetRec ss[4];
+        __shared__ int sc[2][4];
         psx::wave_fold_set(a);
-        if ((t & 63) == 0) ss[t >> 6] = a;
+        nu = __ockl_wfred_add_i32(nu);  // DPP wave sums
+        nz = __ockl_wfred_add_i32(nz);
+        if ((t & 63) == 0) {
+            ss[t >> 6] = a;
+            sc[0][t >> 6] = nu;
+            sc[1][t >> 6] = nz;
+        }
         __syncthreads();
         if (t == 0) {
             SetRec g = *sacc;
             for (int q = 0; q < 4; q++) psx::fold_set(g, ss[q]);
-            const int nn = cnt[kNulls];
+            const int unseen = sc[0][0] + sc[0][1] + sc[0][2] + sc[0][3];
+            const int nn = sc[1][0] + sc[1][1] + sc[1][2] + sc[1][3] + cnt[kCurNull];
             if (nn > 0 && it.rank == 0) {
                 SetRec x = null1;  // null1 scaled to nn null configurations
                 x.tot *= nn;
@@ -2022,7 +2064,10 @@ __global__ __launch_bounds__(256) void k_sss_post(SssIter it, int lo, int hi, co
             }
             *sacc = g;
             *sacc_host = g;
-            for (int q = 0; q < kNCnt; q++) cnt_host[q] = cnt[q];
+            cnt_host[kUnseen] = unseen;
+            cnt_host[kNulls] = nn;
+            cnt_host[kCurPos] = cnt[kCurPos];
+            cnt_host[kCurNull] = cnt[kCurNull];
         }
         return;
     }
@@ -2047,6 +2092,72 @@ __global__ void k_map_rehash(const MapEntry* __restrict__ old, size_t n, MapEntr
     if (i < n && old[i].state) map_insert(T, mask, old[i].lo, old[i].hi, old[i].score);
 }
 
+// The walk's sampling weights exp(lk - max) (sss_postcal.cpp:296-328) on a few
+// host threads that spin between iterations: each std::exp is independent, so
+// slicing the loop leaves every weight bit-identical to the serial loop (the
+// sums and the discrete_distribution stay serial, in the reference's order).
+// ~10 us of the ~50 us iteration at 1,000 neighbours on one core.
+class ExpPool {
+  public:
+    explicit ExpPool(int n) : n_(n) {
+        for (int w = 1; w < n_; w++) th_.emplace_back([this, w] { loop(w); });
+    }
+    ~ExpPool() {
+        quit_.store(true, std::memory_order_release);
+        for (auto& t : th_) t.join();
+    }
+    // out[i] = exp(in[i] - mx), i < len
+    void run(const double* in, double mx, double* out, int len) {
+        if (n_ == 1 || len < 512) {
+            for (int i = 0; i < len; i++) out[i] = std::exp(in[i] - mx);
+            return;
+        }
+        in_ = in;
+        mx_ = mx;
+        out_ = out;
+        len_ = len;
+        done_.store(0, std::memory_order_relaxed);
+        gen_.fetch_add(1, std::memory_order_release);
+        slice(0);
+        while (done_.load(std::memory_order_acquire) < n_ - 1) __builtin_ia32_pause();
+    }
+
+  private:
+    void slice(int w) {
+        const int b = (int)((int64_t)len_ * w / n_), e = (int)((int64_t)len_ * (w + 1) / n_);
+        for (int i = b; i < e; i++) out_[i] = std::exp(in_[i] - mx_);
+    }
+    void loop(int w) {
+        unsigned seen = 0;
+        for (;;) {
+            unsigned g;
+            while ((g = gen_.load(std::memory_order_acquire)) == seen) {
+                if (quit_.load(std::memory_order_acquire)) return;
+                __builtin_ia32_pause();
+            }
+            seen = g;
+            slice(w);
+            done_.fetch_add(1, std::memory_order_release);
+        }
+    }
+    int n_;
+    std::vector<std::thread> th_;
+    std::atomic<unsigned> gen_{0};
+    std::atomic<int> done_{0};
+    std::atomic<bool> quit_{false};
+    const double* in_ = nullptr;
+    double* out_ = nullptr;
+    double mx_ = 0.0;
+    int len_ = 0;
+};
+
+int sampling_threads() {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    const int cores = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
+    return std::max(1, std::min(4, cores / 2));
+}
+
 struct SssDev {
     MapEntry* T = nullptr;
     size_t cap = 0, used = 0;
@@ -2057,6 +2168,7 @@ struct SssDev {
     double* lk = nullptr;     // pinned host: every neighbour's score
     SetRec* shost = nullptr;  // pinned host: the scalars after the iteration
     int* hcnt = nullptr;      // pinned host: the counters
+    int* hmark = nullptr;     // pinned host: per neighbour, its mark (one rank)
     double* hscore = nullptr; // pinned host: gathered item scores (world > 1)
     ~SssDev() {
         hipFree(T);
@@ -2067,6 +2179,7 @@ struct SssDev {
         if (lk) hipHostFree(lk);
         if (shost) hipHostFree(shost);
         if (hcnt) hipHostFree(hcnt);
+        if (hmark) hipHostFree(hmark);
         if (hscore) hipHostFree(hscore);
     }
 };
@@ -2096,6 +2209,7 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.lk), nmax * sizeof(double)));
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.shost), sizeof(SetRec)));
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hcnt), kNCnt * sizeof(int)));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hmark), nmax * sizeof(int)));
     if (world > 1) {
         HIPCHK(hipMalloc(&D.full, nmax * sizeof(double)));
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hscore), nmax * sizeof(double)));
@@ -2105,12 +2219,22 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
     if ((rc = ensure(e->dscore, e->cap_score, nmax))) return rc;
     const SetRec null1 = null_rec(e, 1.0);
     std::mt19937 gen(12345);
+    ExpPool pool(world == 1 ? sampling_threads() : 1);  // sharded walks: one rank per thread already
     int cur[PSX_KMAX] = {0, 0, 0, 0, 0, 0}, k = 0;  // the current configuration, ascending
     double old_sum = 0;
     int iter;
     double kms = 0;
     auto t0 = std::chrono::steady_clock::now();
     std::vector<double> pr;
+    // diagnostics (PSX_SSS_PROFILE): host time per phase of the walk, on stderr
+    static const bool prof = std::getenv("PSX_SSS_PROFILE") != nullptr;
+    double ph[4] = {0, 0, 0, 0};  // launch, wait for the eval, sampling, wait for the post
+    auto tick = [&](int i, std::chrono::steady_clock::time_point& t) {
+        if (!prof) return;
+        const auto n = std::chrono::steady_clock::now();
+        ph[i] += std::chrono::duration<double, std::micro>(n - t).count();
+        t = n;
+    };
     for (iter = 0; iter < 1000; iter++) {
         SssIter it;
         for (int j = 0; j < PSX_KMAX; j++) it.cur[j] = j < k ? cur[j] : -1;
@@ -2143,27 +2267,33 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
             D.cap = nc;
         }
         const unsigned long long mask = D.cap - 1;
-        HIPCHK(hipMemsetAsync(D.cnt, 0, kNCnt * sizeof(int), e->stream));
+        auto tp = std::chrono::steady_clock::now();
+        // plain event records around the eval (the stop event is what the host
+        // waits on): hipExtLaunchKernelGGL's in-packet events cost the host ~12 us
+        // more per launch here (profiles/r03i_sss_host_phases.txt)
         HIPCHK(hipEventRecord(e->ev[2], e->stream));
         hipLaunchKernelGGL(k_sss_eval, dim3((unsigned)n_items), dim3(64), 0, e->stream, e->dp, it, D.T, mask, lo, hi,
-                           D.rows, D.mark, D.cnt, D.lk, e->dsrec, e->dmrec, e->dscore);
+                           D.rows, D.mark, D.cnt, D.lk, e->dsrec, e->dmrec, e->dscore, world == 1 ? D.hmark : nullptr);
         HIPCHK(hipEventRecord(e->ev[3], e->stream));
         const unsigned post_blocks = (unsigned)(U + 1 + (world == 1 ? (n_nbd + 255) / 256 : 0));
         hipLaunchKernelGGL(k_sss_post, dim3(post_blocks), dim3(256), 0, e->stream, it, lo, hi, D.rows, D.mark, D.cnt,
                            e->dmrec, e->dsrec, e->dscore, null1, e->dacc, e->dsacc, D.shost, D.hcnt, D.T, mask,
                            world == 1 ? 1 : 0, D.lk);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipStreamSynchronize(e->stream));
-        {
-            float ms = 0;
-            HIPCHK(hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
-            kms += ms;
-        }
-        const int unseen = D.hcnt[kUnseen];
-        double sss_sum;
+        int unseen = 0;
+        double sss_sum = 0.0;
         if (world == 1) {
-            sss_sum = logval(e, D.shost->m, D.shost->tot);
+            // One rank: the eval wrote every neighbour's weight and mark to pinned
+            // host memory, so the host samples the next configuration while the
+            // GPU folds the records and inserts the new scores (k_sss_post); it
+            // waits for the post only where the stop test needs the normaliser.
+            tick(0, tp);
+            HIPCHK(hipEventSynchronize(e->ev[3]));
+            tick(1, tp);
+            for (int i = 0; i < n_nbd; i++) unseen += D.hmark[i] != -1;
         } else {
+            HIPCHK(hipStreamSynchronize(e->stream));
+            unseen = D.hcnt[kUnseen];
             // one all-gather: [normaliser (m, s), the slice's item scores]; then
             // every rank inserts all scores and writes the sampling weights
             const size_t per = ((size_t)n_items + world - 1) / world, wd = 2 + per;
@@ -2196,16 +2326,22 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
             HIPCHK(hipGetLastError());
             HIPCHK(hipStreamSynchronize(e->stream));
         }
+        {
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+            kms += ms;
+        }
         D.used += (size_t)unseen;
         if (unseen == 0) break;                                                          // :260-263
-        if (iter >= 100 && (1 - std::exp(old_sum - sss_sum)) <= 0.001) break;            // :265-270
+        // (one rank: the sampling below runs first and is dropped when the stop
+        // test of sss_postcal.cpp:265-270 ends the walk — it only advances gen)
         const double* lk = D.lk;
         double wz = 0, wm = 0, wp = 0;
         size_t zs = n_nbd, ms = n_nbd, ps = n_nbd;
         auto group = [&](int b, int en, double& wsum, size_t& smp) {
-            pr.clear();
+            pr.resize((size_t)(en - b));
             double mx = *std::max_element(lk + b, lk + en);
-            for (int ii = b; ii < en; ii++) pr.push_back(std::exp(lk[ii] - mx));
+            pool.run(lk + b, mx, pr.data(), en - b);
             std::discrete_distribution<size_t> dist(pr.begin(), pr.end());
             smp = dist(gen);
             wsum = std::accumulate(pr.begin(), pr.end(), 0.0);
@@ -2241,9 +2377,21 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
             std::copy(nxt, nxt + n, cur);
             k = n;
         }
+        tick(2, tp);
+        if (world == 1 && iter >= 99) {  // the normaliser of this iteration (k_sss_post)
+            HIPCHK(hipStreamSynchronize(e->stream));
+            tick(3, tp);
+            sss_sum = logval(e, D.shost->m, D.shost->tot);
+        }
+        if (iter >= 100 && (1 - std::exp(old_sum - sss_sum)) <= 0.001) break;            // :265-270
         old_sum = sss_sum;
     }
+    HIPCHK(hipStreamSynchronize(e->stream));  // the last iteration's post (one rank: not waited for in the loop)
     auto t1 = std::chrono::steady_clock::now();
+    if (prof)
+        fprintf(stderr, "[psx sss] %d iterations, host us per iteration: launch %.1f, wait eval %.1f, sampling %.1f, "
+                "wait post %.1f\n", iter, ph[0] / std::max(iter, 1), ph[1] / std::max(iter, 1),
+                ph[2] / std::max(iter, 1), ph[3] / std::max(iter, 1));
     if (iterations_out) *iterations_out = iter;
     e->timing.sweep_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     e->timing.kernel_ms = kms;

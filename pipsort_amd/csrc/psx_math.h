@@ -118,7 +118,7 @@ __host__ __device__ inline void split_exp(double h, double rP, int& n, double& m
 __host__ __device__ inline void ldlt_terms(const double* G, int ldg, const double* Ad, const double* y,
                                            double dval, const int* idx, int t, double& q, double& P) {
     double L[PSX_KMAX][PSX_KMAX];
-    double D[PSX_KMAX], w[PSX_KMAX];
+    double D[PSX_KMAX], Rd[PSX_KMAX], w[PSX_KMAX];
     q = 0.0;
     P = 1.0;
     for (int i = 0; i < t; i++) {
@@ -126,7 +126,7 @@ __host__ __device__ inline void ldlt_terms(const double* G, int ldg, const doubl
         for (int j = 0; j < i; j++) {
             double acc = Gi[idx[j]];
             for (int k = 0; k < j; k++) acc -= L[i][k] * L[j][k] * D[k];
-            L[i][j] = acc / D[j];
+            L[i][j] = acc * Rd[j];  // one division per pivot (below)
         }
         double di = Ad[idx[i]];
         double wi = y[idx[i]];
@@ -135,8 +135,9 @@ __host__ __device__ inline void ldlt_terms(const double* G, int ldg, const doubl
             wi -= L[i][k] * w[k];
         }
         D[i] = di;
+        Rd[i] = 1.0 / di;
         w[i] = wi;
-        q += wi * wi / di;
+        q += wi * wi * Rd[i];
         P *= dval * di;
     }
 }

@@ -3,8 +3,9 @@
 #ifndef PSX_SWEEP_H
 #define PSX_SWEEP_H
 
-// waves per SIMD the k = 3 sweep is compiled for (VGPR budget 512 / waves);
-// the unit planner sizes its a-chunks for the same number of wave slots
+// waves per SIMD the k = 3 sweep is compiled for (VGPR budget 512 / waves, LDS
+// 160 KiB / (4 x waves) per one-wave block); the unit planner sizes its a-chunks
+// for the same number of wave slots
 #ifndef PSX_K3_WAVES
 #define PSX_K3_WAVES 2
 #endif

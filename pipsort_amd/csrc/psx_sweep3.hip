@@ -149,13 +149,18 @@ __device__ __forceinline__ void split3a(double h, double rP, int& N, double& q) 
 
 // split3a with the rounding offset by an integer R (cmag = kMagic - 256 R):
 // N = round(256 (h - R)), so the caller's exponent is N >> 8 = n - R directly;
-// the fraction's exponential by the walk's cubic (kC*)
-__device__ __forceinline__ void split3r(double h, double rP, double cmag, int& N, double& q) {
-    const double xr = fma(h, 256.0, cmag);
+// the fraction's exponential by the walk's cubic (kC*).  k256 = 256 and kc3 = kC3
+// in SGPRs, kc2 = kC2 in a VGPR: opaque values the caller holds for the walk, so
+// the compiler emits one VOP3 v_fma_f64 instead of copying the addend (a
+// loop-carried VGPR, or a constant it cannot put on the constant bus beside
+// another) for the two-address v_fmac_f64 with a literal: a v_mov_b64 per use
+__device__ __forceinline__ void split3r(double h, double rP, double cmag, double k256, double kc3, double kc2,
+                                        int& N, double& q) {
+    const double xr = fma(h, k256, cmag);
     N = __double2loint(xr);
     const double kf = xr - cmag;
-    const double f = fma(h, 256.0, -kf);
-    double p = fma(kC3, f, kC2);
+    const double f = fma(h, k256, -kf);
+    double p = fma(f, kc3, kc2);
     p = fma(p, f, kC1);
     p = fma(p, f, kC0);
     q = p * rP;
@@ -286,18 +291,23 @@ __global__ void k_build_bc3(Sweep3Args A, double2* __restrict__ mu01, int2* __re
 //
 // Pivot factors: P_T^{-1/2} = prod_i r_i rsd over the LDL^T pivots of T.  The
 // step computes r2x = 2 / sqrt(D), so the staged factors carry rsd / 2.
-// LDS of a k = 3 unit: b-block terms (per unit) and (a, b) terms (per a),
-// indexed [study][b slot], the exp2 table and the rotating b-slot accumulators
+// LDS budget: 3 one-wave blocks per SIMD (12 per CU, VGPRs <= 168) need <= 13,312
+// bytes per block (160 KiB / 12, in 512-byte allocation granules).  Only what other
+// lanes read lives in LDS — the exp2 table, the per-a (a, b) terms of the rotating
+// b slot and the slot accumulators; everything a lane reads only for itself (its b
+// slot's and c's constants, its record positions, the next a's Sigma~ row entries)
+// is held in registers, which the compiler parks in scratch across the b-walk.
+//
+// LDS of a k = 3 unit, ROBUST variant: (a, b) terms (per a), indexed [study][b
+// slot], the exp2 table and the rotating b-slot accumulators
 struct Sweep3Smem {
     double tab[256];
-    double bH[2][64], bR[2][64];
-    double abG[2][64], abD[2][64], abI[2][64], abW[2][64], abH[2][64], abR[2][64], abMu[2][64], abMuB[2][64];
+    double abG[2][64], abI[2][64], abW[2][64], abH[2][64], abR[2][64], abMu[2][64], abMuB[2][64];
     int abN[2][64];
-    double bW[64];
+    float bW[64];
     double sP0[64], sP1[64], sSh[64], sSl[64], sNs[64];
     int sM[64];
-    double g1ab[2][64], g1ac[2][64];  // the first a's Sigma~ row entries
-    int sPos[3][64];                   // record positions: c, b slot, a
+    int aPos[kMaxChunkA3];  // a record positions
 };
 // LDS of the fast k = 3 variant: the per-b terms of both studies side by side
 // (one 16-byte read per term and step; lane t reads slot (t + j) & 63, so the
@@ -305,24 +315,21 @@ struct Sweep3Smem {
 // factor sF = 2^(Gm - sM) (Gm: the wave's largest a shift)
 struct Sweep3FastSmem {
     double tab[256];
-    double2 bAd[64], bY[64], bMuB[64];  // b-slot constants of the unit (both studies): A_bb, y_b, {b} weight
-    int2 bNB[64];
     double2 aAd[kMaxChunkA3], aY[kMaxChunkA3];  // the unit's a: A_aa, y_a (both studies), presence
     unsigned aP[kMaxChunkA3];
+    int aPos[kMaxChunkA3];  // a record positions
     double2 abG[64], abI[64], abIW[64], abH[64], abR[64], abMu[64], abMuB[64];
     int2 abN[64];
     double sF[64];
-    double bW[64];
+    float bW[64];  // membership weight of the slot's b (0, 1 or 3)
     double sW0[64], sW1[64], sW2[64], sSl[64], sNs[64];
-    int sM[64];
-    double g1ab[2][64], g1ac[2][64];  // this a's Sigma~ row entries
-    int sPos[3][64];                   // record positions: c, b slot, a
 };
 union SweepSmem {  // a block runs either a k = 3 unit or a level-2 unit
     Sweep3Smem s3;
     Sweep3FastSmem f3;
     SweepUnitSmem u2;
 };
+static_assert(sizeof(SweepSmem) <= 13312, "k_sweep3 LDS above the 3-blocks-per-SIMD budget");
 
 // One k = 3 unit, ROBUST variant: every step's subset weights are taken
 // relative to the set's own top exponent (n_abc per study) and the lane / slot
@@ -333,10 +340,7 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
                                                 Acc5* __restrict__ rec, SetRec* __restrict__ srec, int rec_stride,
                                                 int* __restrict__ flag, const int* __restrict__ pos, SweepSmem& sm) {
     double (&tab)[256] = sm.s3.tab;
-    double (&bH)[2][64] = sm.s3.bH;
-    double (&bR)[2][64] = sm.s3.bR;
     double (&abG)[2][64] = sm.s3.abG;
-    double (&abD)[2][64] = sm.s3.abD;
     double (&abI)[2][64] = sm.s3.abI;
     double (&abW)[2][64] = sm.s3.abW;
     double (&abH)[2][64] = sm.s3.abH;
@@ -344,16 +348,13 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
     double (&abMu)[2][64] = sm.s3.abMu;
     double (&abMuB)[2][64] = sm.s3.abMuB;
     int (&abN)[2][64] = sm.s3.abN;
-    double (&bW)[64] = sm.s3.bW;
+    float (&bW)[64] = sm.s3.bW;
     double (&sP0)[64] = sm.s3.sP0;
     double (&sP1)[64] = sm.s3.sP1;
     double (&sSh)[64] = sm.s3.sSh;
     double (&sSl)[64] = sm.s3.sSl;
     double (&sNs)[64] = sm.s3.sNs;
     int (&sM)[64] = sm.s3.sM;
-    double (&g1ab)[2][64] = sm.s3.g1ab;
-    double (&g1ac)[2][64] = sm.s3.g1ac;
-    int (&sPos)[3][64] = sm.s3.sPos;
 
     const int t = threadIdx.x;
     const int4 un = units[unit];
@@ -376,13 +377,14 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
     const int vbl = 64 * K + t, ubl = vbl - pad;
     const bool okb = vbl >= pad;
     const unsigned pbl = okb ? A.pres[ubl] : 0u;
+    double bH[2], bR[2];  // this lane's b slot: {b} quadratic form and pivot factor
 #pragma unroll
     for (int s = 0; s < 2; s++) {
         const BTerms b = b_terms<ALLPRES>(A, s, vbl);
-        bH[s][t] = b.H;
-        bR[s][t] = b.R;
+        bH[s] = b.H;
+        bR[s] = b.R;
     }
-    bW[t] = memb_weight(pbl);
+    bW[t] = (float)memb_weight(pbl);
     sM[t] = EMPTY;
     sP0[t] = sP1[t] = sSh[t] = sSl[t] = sNs[t] = 0.0;
 
@@ -415,19 +417,15 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
     const int2* bnn = A.bcn + (size_t)tile * 4096 + t;
 
     // record positions (CSR map) of this unit's c / b-slot / a records, and the
-    // first a's Sigma~ row entries, loaded with the unit prologue into LDS: no
-    // dependent global-load round trip later at the first a or at the record
-    // writes, and no registers held across the walk
-    {
-        const size_t rbase = (size_t)unit * rec_stride;
-        sPos[0][t] = pos[rbase + t];
-        sPos[1][t] = pos[rbase + 64 + t];
-        sPos[2][t] = (t < a1 - a0) ? pos[rbase + 128 + t] : -1;
+    // first a's Sigma~ row entries, loaded with the unit prologue
+    const size_t rbase = (size_t)unit * rec_stride;
+    const int posC = pos[rbase + t], posB = pos[rbase + 64 + t];
+    if (t < a1 - a0) sm.s3.aPos[t] = pos[rbase + 128 + t];
+    double g1ab[2], g1ac[2];
 #pragma unroll
-        for (int s = 0; s < 2; s++) {
-            g1ab[s][t] = okb ? A.G[s][(size_t)(a0 - pad) * ldg + ubl] : 0.0;
-            g1ac[s][t] = okc ? A.G[s][(size_t)(a0 - pad) * ldg + uc] : 0.0;
-        }
+    for (int s = 0; s < 2; s++) {
+        g1ab[s] = okb ? A.G[s][(size_t)(a0 - pad) * ldg + ubl] : 0.0;
+        g1ac[s] = okc ? A.G[s][(size_t)(a0 - pad) * ldg + uc] : 0.0;
     }
 
     for (int ai = 0; ai < a1 - a0; ai++) {
@@ -452,7 +450,7 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
             split3(ha, rPa, tab, nA, muA);
             {
                 // {a, b} and {b} for this lane's b, into LDS
-                const double Gab = ai ? (okb ? A.G[s][(size_t)ua * ldg + ubl] : 0.0) : g1ab[s][t];
+                const double Gab = ai ? (okb ? A.G[s][(size_t)ua * ldg + ubl] : 0.0) : g1ab[s];
                 const double Abb = okb ? A.Ad[s][ubl] : 1.0;
                 const double yb = okb ? A.ys[s][ubl] : 0.0;
                 const double l = Gab * iAaa;
@@ -466,9 +464,8 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
                 int nAB, nB;
                 double muAB, muB;
                 split3(hab, rPab, tab, nAB, muAB);
-                split3(bH[s][t], bR[s][t] * (2.0 / A.rsd[s]), tab, nB, muB);
+                split3(bH[s], bR[s] * (2.0 / A.rsd[s]), tab, nB, muB);
                 abG[s][t] = Gab;
-                abD[s][t] = Dab;
                 abI[s][t] = rab * rab;
                 abW[s][t] = 0.5 * wab;
                 abH[s][t] = hab;
@@ -478,7 +475,7 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
                 abN[s][t] = nAB;
             }
             // {a, c}: lane-owned
-            const double Gac = ai ? (okc ? A.G[s][(size_t)ua * ldg + uc] : 0.0) : g1ac[s][t];
+            const double Gac = ai ? (okc ? A.G[s][(size_t)ua * ldg + uc] : 0.0) : g1ac[s];
             l1[s] = Gac * iAaa;
             D1[s] = fma(-l1[s], Gac, Acc[s]);
             const double w1 = fma(-l1[s], ya, yc[s]);
@@ -527,10 +524,11 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
                     // {b, c}: precomputed (k_build_bc3, a-independent)
                     const int n2 = s ? ncur.y : ncur.x;
                     const double mu2 = s ? mcur1 : mcur0;
-                    // {a, b, c}: extend the (a, b) factor by the c row
-                    const double lcb = fma(-l1[s], abG[s][bs], Gbc) * abI[s][bs];
-                    const double u3 = lcb * abD[s][bs];
-                    const double D3 = fma(-u3, lcb, D1[s]);
+                    // {a, b, c}: extend the (a, b) factor by the c row (x = the
+                    // unnormalised L entry; D_ab I_ab = 1 folds the pivot away)
+                    const double x = fma(-l1[s], abG[s][bs], Gbc);
+                    const double lcb = x * abI[s][bs];
+                    const double D3 = fma(-x, lcb, D1[s]);
                     const double w3 = fma(-lcb, abW[s][bs], w1h[s]);
                     const double r3 = rsq2x(D3);
                     const double t3 = w3 * r3;
@@ -649,7 +647,7 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
         }
         Acc5 ra = lacc_rec(accA, A.Ck, A.pit0);
         wave_fold_acc(ra);
-        const int qa = sPos[2][ai];
+        const int qa = sm.s3.aPos[ai];
         if (t == 0 && qa >= 0) store_rec(rec + qa, ra);
     }
     __syncthreads();
@@ -664,8 +662,8 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
         Acc5 rc = lacc_rec(accC, A.Ck, A.pit0);
         const Acc5 rb = lacc_rec(sl, A.Ck, A.pit0);
         if (diag) fold_acc(rc, rb);  // one SNP: c = b slot t (the plan keys one record)
-        if (sPos[0][t] >= 0) store_rec(rec + sPos[0][t], rc);
-        if (!diag && sPos[1][t] >= 0) store_rec(rec + sPos[1][t], rb);
+        if (posC >= 0) store_rec(rec + posC, rc);
+        if (!diag && posB >= 0) store_rec(rec + posB, rb);
     }
     SetRec sr;
     sr.tot = totC * A.pit0;
@@ -708,17 +706,13 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                                                  bool& redo) {
     Sweep3FastSmem& F = sm.f3;
     double (&tab)[256] = F.tab;
-    double (&bW)[64] = F.bW;
+    float (&bW)[64] = F.bW;
     double (&sW0)[64] = F.sW0;  // b slots: W0, W1, W2 (own rho deferred), sharedLL, notSharedLL
     double (&sW1)[64] = F.sW1;
     double (&sW2)[64] = F.sW2;
     double (&sSl)[64] = F.sSl;
     double (&sNs)[64] = F.sNs;
     double (&sF)[64] = F.sF;
-    int (&sM)[64] = F.sM;
-    double (&g1ab)[2][64] = F.g1ab;
-    double (&g1ac)[2][64] = F.g1ac;
-    int (&sPos)[3][64] = F.sPos;
 
     const int t = threadIdx.x;
     const unsigned long long t_start = A.trace ? wall_clock64() : 0ull;
@@ -731,8 +725,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     const int tile = C * (C + 1) / 2 + K;
     const double rho = A.rho;
 
-    // ---- unit prologue: every global load of the unit's constants is issued
-    // here, once (the a prologues below then read LDS only) -------------------------
+    // ---- unit prologue: the unit's constants are loaded once, into LDS where other
+    // lanes read them and into registers where a lane reads only its own ---------------
     for (int i = t; i < 256; i += 64) tab[i] = A.tab[i];
     const int vbl = 64 * K + t, ubl = vbl - pad;
     const bool okb = vbl >= pad;
@@ -749,9 +743,10 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         F.aAd[t] = make_double2(A.Ad[0][u], A.Ad[1][u]);
         F.aY[t] = make_double2(A.ys[0][u], A.ys[1][u]);
         F.aP[t] = A.pres[u];
+        F.aPos[t] = pos[(size_t)unit * rec_stride + 128 + t];
     }
-    bW[t] = memb_weight(pbl);
-    sM[t] = EMPTY;
+    bW[t] = (float)memb_weight(pbl);
+    int sMt = EMPTY;  // shift of b slot t (lane-owned outside the walk)
     sW0[t] = sW1[t] = sW2[t] = sSl[t] = sNs[t] = 0.0;
 
     const int vc = 64 * C + t, uc = vc - pad;
@@ -777,34 +772,27 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     const double2* g01 = A.g01 + (size_t)tile * 4096 + t;
     const double2* m01 = A.mu01 + (size_t)tile * 4096 + t;
     const int2* bnn = A.bcn + (size_t)tile * 4096 + t;
-    {
-        const size_t rbase = (size_t)unit * rec_stride;
-        sPos[0][t] = pos[rbase + t];
-        sPos[1][t] = pos[rbase + 64 + t];
-        sPos[2][t] = (t < a1 - a0) ? pos[rbase + 128 + t] : -1;
+    // record positions (CSR map) of this unit's c / b-slot records; this a's
+    // Sigma~ row entries (g1ab: this lane's b slot, g1ac: its c)
+    const size_t rbase = (size_t)unit * rec_stride;
+    const int posC = pos[rbase + t], posB = pos[rbase + 64 + t];
+    double g1ab[2], g1ac[2];
 #pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const double* row = A.G[s] + (size_t)(a0 - pad) * ldg;
-            const double gb = row[ib], gc = row[ic];
-            g1ab[s][t] = okb ? gb : 0.0;
-            g1ac[s][t] = okc ? gc : 0.0;
-        }
+    for (int s = 0; s < 2; s++) {
+        const double* row = A.G[s] + (size_t)(a0 - pad) * ldg;
+        const double gb = row[ib], gc = row[ic];
+        g1ab[s] = okb ? gb : 0.0;
+        g1ac[s] = okc ? gc : 0.0;
     }
     __syncthreads();  // exp2 table staged
-    {
-        // the {b} weight of every slot: unit-constant (the a prologues rescale it)
-        int nB[2];
-        double muB[2];
+    // the {b} weight of this lane's slot: unit-constant (the a prologues rescale it)
+    int nBb[2];
+    double muBb[2];
 #pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const double chib = (okb && (ALLPRES || ((pbl >> s) & 1u))) ? 1.0 : 0.0;
-            const double r = rsqrt_nr(Abb[s]);
-            split3(yb[s] * yb[s] * r * r, r * A.rsd[s] * chib, tab, nB[s], muB[s]);
-        }
-        F.bAd[t] = make_double2(Abb[0], Abb[1]);
-        F.bY[t] = make_double2(yb[0], yb[1]);
-        F.bMuB[t] = make_double2(muB[0], muB[1]);
-        F.bNB[t] = make_int2(nB[0], nB[1]);
+    for (int s = 0; s < 2; s++) {
+        const double chib = (okb && (ALLPRES || ((pbl >> s) & 1u))) ? 1.0 : 0.0;
+        const double r = rsqrt_nr(Abb[s]);
+        split3(yb[s] * yb[s] * r * r, r * A.rsd[s] * chib, tab, nBb[s], muBb[s]);
     }
 
     unsigned long long t_ph[4] = {0ull, 0ull, 0ull, 0ull};  // diagnostics: phases of the first a
@@ -814,8 +802,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         double l1[2], D1[2], w1h[2], Ep[2][4];  // Ep: {}, {a}, {c}, {a,c} relative to 2^R
         int R[2];
         // global loads of this a, all consumed late (no wait in the prologue): the
-        // walk's first tile row, and the next a's Sigma~ row entries, staged into
-        // LDS (this lane's own entries) once this a's prologue is done
+        // walk's first tile row, and the next a's Sigma~ row entries
         double2 gnx = g01[j0 * 64], mnx = m01[j0 * 64];
         int2 nnx = bnn[j0 * 64];
         const bool nxt = ai + 1 < a1 - a0;
@@ -829,8 +816,6 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         __syncthreads();  // previous a's (a, b) terms and slots fully consumed
         const unsigned pa = F.aP[ai];
         const double2 aAd = F.aAd[ai], aY = F.aY[ai];
-        const double2 bAd = F.bAd[t], bY = F.bY[t], bMuB = F.bMuB[t];
-        const int2 bNB = F.bNB[t];
         double pG[2], pI[2], pIW[2], pH[2], pR[2], pMu[2], pMuB[2];
         int pN[2];
 #pragma unroll
@@ -845,19 +830,19 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             double muA;
             split3(ha, rPa, tab, nA, muA);
             {
-                const double Gab = g1ab[s][t];
+                const double Gab = g1ab[s];
                 const double l = Gab * iAaa;
-                const double Dab = fma(-l, Gab, s ? bAd.y : bAd.x);
+                const double Dab = fma(-l, Gab, Abb[s]);
                 const double rab = rsqrt_nr(Dab);
-                const double wab = fma(-l, ya, s ? bY.y : bY.x);
+                const double wab = fma(-l, ya, yb[s]);
                 const double hab = fma(wab * wab, rab * rab, ha);
                 const bool chib = okb && (ALLPRES || ((pbl >> s) & 1u));
                 const double rPab = chib ? rPa * rab * A.rsd[s] : 0.0;
                 int nAB;
                 double muAB;
                 split3(hab, rPab, tab, nAB, muAB);
-                const int nB = s ? bNB.y : bNB.x;
-                const double muB = s ? bMuB.y : bMuB.x;
+                const int nB = nBb[s];
+                const double muB = muBb[s];
                 pG[s] = Gab;
                 pI[s] = rab * rab;
                 pIW[s] = rab * rab * (0.5 * wab);  // I_ab w_ab / 2 (the pivot itself is not needed)
@@ -867,7 +852,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 pMuB[s] = ldexp(muB, nB - nAB);
                 pN[s] = nAB;
             }
-            const double Gac = g1ac[s][t];
+            const double Gac = g1ac[s];
             l1[s] = Gac * iAaa;
             D1[s] = fma(-l1[s], Gac, Acc[s]);
             const double w1 = fma(-l1[s], ya, yc[s]);
@@ -937,19 +922,21 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             m0 = M0;
             m1 = M1;
         }
-        const double fC = ldexp(1.0, G - mC), f0 = ldexp(1.0, R[1] - m0), f1 = ldexp(1.0, R[0] - m1);
         // round-to-nearest magic offset by R: N = round(256 (h3 - R)), so n3 - R = N >> 8
         const double cmag[2] = {kMagic - 256.0 * R[0], kMagic - 256.0 * R[1]};
+        // the walk's split constants as opaque registers (split3r)
+        double k256 = 256.0, kc3 = kC3, kc2 = kC2;
+        asm volatile("" : "+s"(k256), "+s"(kc3), "+v"(kc2));
         double gF;
         {
             const int Gm = __ockl_wfred_max_i32(G);  // DPP wave reduction, no LDS round trips
-            const int Ms = max(sM[t], Gm), d = sM[t] - Ms;
+            const int Ms = max(sMt, Gm), d = sMt - Ms;
             sW0[t] = ldexp(sW0[t], d);
             sW1[t] = ldexp(sW1[t], d);
             sW2[t] = ldexp(sW2[t], d);
             sSl[t] = ldexp(sSl[t], d);
             sNs[t] = ldexp(sNs[t], d);
-            sM[t] = Ms;
+            sMt = Ms;
             // a lane's contribution to slot b is scaled by 2^(G - sM[b]) = sF[b] * gF
             // (powers of two: the product is exact down to the underflow either form has)
             sF[t] = ldexp(1.0, Gm - Ms);
@@ -959,8 +946,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         if (nxt) {
 #pragma unroll
             for (int s = 0; s < 2; s++) {
-                g1ab[s][t] = okb ? nGab[s] : 0.0;
-                g1ac[s][t] = okc ? nGac[s] : 0.0;
+                g1ab[s] = okb ? nGab[s] : 0.0;
+                g1ac[s] = okc ? nGac[s] : 0.0;
             }
         }
         if (A.trace && ai == 0) t_ph[1] = wall_clock64();
@@ -989,7 +976,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 const double h3 = fma(t3, t3, s ? aH.y : aH.x);
                 double rP3 = (s ? aR.y : aR.x) * r3;
                 if (!ALLPRES && !((pcm >> s) & 1u)) rP3 = 0.0;  // c absent from study s
-                split3r(h3, rP3, cmag[s], N[s], q[s]);
+                split3r(h3, rP3, cmag[s], k256, kc3, kc2, N[s], q[s]);
             }
         };
         auto finish = [&](int j, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
@@ -1160,6 +1147,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         const double NC = ((Cu[0][0] + Cu[1][0]) + Cu[2][0]) + ((Cu[0][1] + Cu[1][1]) + Cu[2][1]);
         // a notSharedLL sum far below the shift loses precision: exact rerun
         if (nact > 0) tiny |= (NA < kTinyNs) | (NC < kTinyNs);
+        const double fC = ldexp(1.0, G - mC), f0 = ldexp(1.0, R[1] - m0), f1 = ldexp(1.0, R[0] - m1);
         cW0 = fma(WC[0], fC, cW0);
         cW1 = fma(WC[1], fC, cW1);
         cW2 = fma(WC[2], fC, cW2);
@@ -1184,7 +1172,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             const double W2 = __ockl_wfred_add_f64(ldexp(WA[2], dg));
             const double Sl = __ockl_wfred_add_f64(ldexp(LA2, dg));
             const double Ns = __ockl_wfred_add_f64(ldexp(NA, dg));
-            const int qa = sPos[2][ai];
+            const int qa = F.aPos[ai];
             if (t == 0 && qa >= 0) store_rec(rec + qa, wrec(Gw, W0, W1, W2, Sl, Ns, rho, A.Ck, A.pit0));
         }
         if (A.trace && ai == 0) t_ph[3] = wall_clock64();
@@ -1194,10 +1182,10 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         // a diagonal tile's lane t and b slot t are one SNP: one record (the plan
         // keys no b records there), folded here instead of in the merge
         Acc5 rc = wrec(mC, cW0, cW1, cW2, cSl, cNs, rho, A.Ck, A.pit0);
-        const Acc5 rb = wrec(sM[t], sW0[t], sW1[t], sW2[t], sSl[t], sNs[t], rho, A.Ck, A.pit0);
+        const Acc5 rb = wrec(sMt, sW0[t], sW1[t], sW2[t], sSl[t], sNs[t], rho, A.Ck, A.pit0);
         if (diag) fold_acc(rc, rb);
-        if (sPos[0][t] >= 0) store_rec(rec + sPos[0][t], rc);
-        if (!diag && sPos[1][t] >= 0) store_rec(rec + sPos[1][t], rb);
+        if (posC >= 0) store_rec(rec + posC, rc);
+        if (!diag && posB >= 0) store_rec(rec + posB, rb);
     }
     SetRec sr;
     sr.tot = ((cW0 + cW1) + rho * cW2) * A.pit0;  // every assignment of the lane's sets
@@ -1229,7 +1217,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
 // The k = 3 sweep: one block per unit (fast variant, redone robustly in the same
 // block when flagged); level-2 units ride in the same launch, after them.
 template <bool ALLPRES>
-__global__ __launch_bounds__(64, PSX_K3_WAVES) void k_sweep3(Sweep3Args A, const int4* __restrict__ units,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PSX_K3_WAVES, PSX_K3_WAVES))) void k_sweep3(Sweep3Args A, const int4* __restrict__ units,
                                                   Acc5* __restrict__ rec, SetRec* __restrict__ srec, int rec_stride,
                                                   int* __restrict__ flag, const int* __restrict__ pos, int nk3,
                                                   TileArgs A2, const int4* __restrict__ units2,
