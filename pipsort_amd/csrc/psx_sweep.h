@@ -93,6 +93,8 @@ struct Sweep3Args {
     const double2* g01;        // skewT of both studies interleaved (one 16-byte load per step)
     const double2* mu01;       // {b, c} subset weights mu per [tile][step][lane], both studies (a-independent)
     const int2* bcn;           // their base-2 exponents, both studies
+    const double2* bcsm;       // per [tile][lane]: sum over the tile's 64 b of the {b, c} weights, both
+    const int2* bcsn;          //   studies, as 2^bcsn * bcsm (the off-diagonal walk's closed-form sums)
     const double* muS[2];      // singleton weights {c}, by u
     const int* nS[2];
     const unsigned char* pres; // bit s: SNP present in study s, by u
@@ -116,6 +118,8 @@ int launch_build_skewT(const double* G, int ldg, int pad, double* skew, hipStrea
 // step), computed once per locus with the sweep kernel's own arithmetic
 constexpr int kTileRowPad = 4;  // zero rows after the last tile of mu01 / bcn / g01
 int launch_build_bc3(const Sweep3Args& A, int ntile, double2* mu01, int2* n, hipStream_t st);
+// per tile and lane c: the sum over the tile's 64 b of the {b, c} weights
+int launch_bc3_rowsum(int ntile, const double2* mu01, const int2* n, double2* sm, int2* sn, hipStream_t st);
 // out[i] = (a[i], b[i])
 int launch_interleave2(const double* a, const double* b, size_t n, double2* out, hipStream_t st);
 
@@ -126,6 +130,8 @@ struct SweepPlanCache {
     double2* d_g01 = nullptr;                // skewT of both studies interleaved (k = 3 fast kernel)
     double2* d_mu01 = nullptr;               // {b, c} weights per skewT entry, both studies
     int2* d_bcn = nullptr;
+    double2* d_bcsm = nullptr;               // row sums of the {b, c} weights per tile and lane
+    int2* d_bcsn = nullptr;
     double* d_muS[2] = {nullptr, nullptr};   // singleton subset weights
     int* d_nS[2] = {nullptr, nullptr};
     double* d_ys[2] = {nullptr, nullptr};    // scaled y (k = 3 fast kernel)

@@ -291,12 +291,13 @@ __global__ void k_build_bc3(Sweep3Args A, double2* __restrict__ mu01, int2* __re
 //
 // Pivot factors: P_T^{-1/2} = prod_i r_i rsd over the LDL^T pivots of T.  The
 // step computes r2x = 2 / sqrt(D), so the staged factors carry rsd / 2.
-// LDS budget: 3 one-wave blocks per SIMD (12 per CU, VGPRs <= 168) need <= 13,312
-// bytes per block (160 KiB / 12, in 512-byte allocation granules).  Only what other
-// lanes read lives in LDS — the exp2 table, the per-a (a, b) terms of the rotating
-// b slot and the slot accumulators; everything a lane reads only for itself (its b
-// slot's and c's constants, its record positions, the next a's Sigma~ row entries)
-// is held in registers, which the compiler parks in scratch across the b-walk.
+// LDS: what other lanes read — the exp2 table, the per-a (a, b) terms of the
+// rotating b slot, the slot accumulators; what a lane reads only for itself (its b
+// slot's and c's constants, record positions, the next a's Sigma~ row entries)
+// is held in registers.  (Three waves per SIMD, <= 13,312 bytes per block and 168
+// VGPRs, were measured 17 % slower: the walk state left no registers for the
+// per-a state, which the compiler parked in scratch behind dependent waits,
+// profiles/r03d_k3_three_waves_rejected.txt.)
 //
 // LDS of a k = 3 unit, ROBUST variant: (a, b) terms (per a), indexed [study][b
 // slot], the exp2 table and the rotating b-slot accumulators
@@ -323,13 +324,19 @@ struct Sweep3FastSmem {
     double sF[64];
     float bW[64];  // membership weight of the slot's b (0, 1 or 3)
     double sW0[64], sW1[64], sW2[64], sSl[64], sNs[64];
+    // off-diagonal units (closed-form sums, sweep3_unit_fast): this lane's c terms
+    double2 bcsm[64];           // the {b, c} weights of this lane's c summed over the block, both studies
+    int2 bcsn[64];
+    double pbS[2];              // sum of the block's {b} weights, both studies: 2^pbM * pbS
+    int pbM[2];
 };
 union SweepSmem {  // a block runs either a k = 3 unit or a level-2 unit
     Sweep3Smem s3;
     Sweep3FastSmem f3;
     SweepUnitSmem u2;
 };
-static_assert(sizeof(SweepSmem) <= 13312, "k_sweep3 LDS above the 3-blocks-per-SIMD budget");
+// PSX_K3_WAVES one-wave blocks per SIMD: 160 KiB / (4 x waves) per block, in 512-byte granules
+static_assert(sizeof(SweepSmem) <= (163840 / (4 * PSX_K3_WAVES)) / 512 * 512, "k_sweep3 LDS above its occupancy budget");
 
 // One k = 3 unit, ROBUST variant: every step's subset weights are taken
 // relative to the set's own top exponent (n_abc per study) and the lane / slot
@@ -794,6 +801,26 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         const double r = rsqrt_nr(Abb[s]);
         split3(yb[s] * yb[s] * r * r, r * A.rsd[s] * chib, tab, nBb[s], muBb[s]);
     }
+    // Off-diagonal units walk every b of block K on every lane (a < 64K <= b <
+    // 64C <= c, all lanes active, steps 0 .. 63), so the parts of the per-step fold
+    // that factor into (b-only or a,b-only) x (a,c-only) terms have closed forms
+    // (sep): the walk sums V_s of the {b}, {a, b} and {b, c} weights, and the b
+    // slot's one-study dot products over {b} and {a, b} (see below).
+    const bool sep = !diag && j0 == 0 && j1 == 64;
+    if (sep) {
+        F.bcsm[t] = A.bcsm[(size_t)tile * 64 + t];
+        F.bcsn[t] = A.bcsn[(size_t)tile * 64 + t];
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            int m = nBb[s];
+            double x = muBb[s];
+            wave_pair_dpp(m, x);
+            if (t == 0) {
+                F.pbS[s] = x;
+                F.pbM[s] = m;
+            }
+        }
+    }
 
     unsigned long long t_ph[4] = {0ull, 0ull, 0ull, 0ull};  // diagnostics: phases of the first a
     if (A.trace) t_ph[0] = wall_clock64();
@@ -942,6 +969,25 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             sF[t] = ldexp(1.0, Gm - Ms);
             gF = ldexp(1.0, G - Gm);
         }
+        if (sep) {
+            // b in one study, subsets {} and {a} of {a, c} with b: over the walk
+            // slot b receives from every lane c once
+            //   v_0[A](b, c) uW_1[A](c) 2^(G(c) - sM[b]) = E_0[A + b] 2^(-sM[b]) uW_1[A](c) 2^(R_1(c)),
+            // A in {{}, {a}}, i.e. E_0[A + b] 2^(-sM[b]) times a wave sum over c
+            // (likewise study 1); the walk then only takes their {b, c} and {a, b, c}
+            // terms.  Lane t adds slot t's share.
+            double QW[2][2];
+            int Qm[2];
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                Qm[s] = __ockl_wfred_max_i32(R[s]);
+#pragma unroll
+                for (int i = 0; i < 2; i++) QW[s][i] = __ockl_wfred_add_f64(ldexp(uW[s][i], R[s] - Qm[s]));
+            }
+            // E_s[A + b] of this lane's slot: {b} = pMuB 2^pN, {a, b} = pMu 2^pN
+            sW0[t] += fma(pMuB[0], QW[1][0], pMu[0] * QW[1][1]) * ldexp(1.0, pN[0] + Qm[1] - sMt);
+            sW1[t] += fma(pMuB[1], QW[0][0], pMu[1] * QW[0][1]) * ldexp(1.0, pN[1] + Qm[0] - sMt);
+        }
         __syncthreads();  // (a, b) terms and slot shifts visible
         if (nxt) {
 #pragma unroll
@@ -979,7 +1025,12 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 split3r(h3, rP3, cmag[s], k256, kc3, kc2, N[s], q[s]);
             }
         };
-        auto finish = [&](int j, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
+        // SEP (off-diagonal units): the {} / {a} parts of the prior-weighted one-study
+        // dot products and the walk sums V_s[0 .. 2] have closed forms (a prologue,
+        // after the walk).  notSharedLL (NB) stays whole: its per-set precision check
+        // (kTinyNs) needs the whole value.
+        auto finish = [&](auto SEP, int j, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
+            constexpr bool sepc = decltype(SEP)::value;
             const int bs = (t + j) & 63;
             const double2 aMuB = F.abMuB[bs], aMu = F.abMu[bs];
             const int2 aN = F.abN[bs];
@@ -1003,9 +1054,12 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             auto dot4 = [](const double (&u)[4], const double (&x)[4], double acc0) {
                 return fma(u[3], x[3], fma(u[2], x[2], fma(u[1], x[1], fma(u[0], x[0], acc0))));
             };
+            auto dot2 = [](const double (&u)[4], const double (&x)[4], double acc0) {  // the {b, c} and {a, b, c} terms
+                return fma(u[3], x[3], fma(u[2], x[2], acc0));
+            };
             // ---- member b (this step's slot): b in study 0 only / study 1 only ----
-            const double WB0 = dot4(v[0], uW[1], 0.0);
-            const double WB1 = dot4(v[1], uW[0], 0.0);
+            const double WB0 = sepc ? dot2(v[0], uW[1], 0.0) : dot4(v[0], uW[1], 0.0);
+            const double WB1 = sepc ? dot2(v[1], uW[0], 0.0) : dot4(v[1], uW[0], 0.0);
             const double NB = dot4(v[0], uL[1], dot4(v[1], uL[0], 0.0));
             // ---- b in both studies: the 9 assignments of (a, c); their sums for a and c ----
 #pragma unroll
@@ -1023,7 +1077,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             const double WB2 = fma(rho, fma(rho, z22, Z1), Z0);
             const double LB2 = (Z0 + Z1) + z22;
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
+            for (int i = sepc ? 3 : 0; i < 4; i++) {
                 V0[i] += v[0][i];
                 V1[i] += v[1][i];
             }
@@ -1048,7 +1102,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             je = j0 + ((j1 - j0) & ~1);
         else if ((va < 64 * K || va >= 64 * K + 64) && 64 * K >= pad)
             je = j0 + ((min(j1, 32) - j0) & ~1);
-        if (je > j0) {
+        auto walk = [&](auto SEP) {
             // unrolled by two: the chained state alternates between (NA, qA) and (NB, qB).
             // Loads run up to three rows ahead unclamped (the buffers carry
             // kTileRowPad rows past the last tile; what lies past je is not used),
@@ -1068,7 +1122,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 int2 n_nxt = nb[o + 64];
                 double2 g_after = gb[o + 128];
                 chain(j + 1, g_next, NB, qB);
-                finish(j, NA, qA, m_cur, n_cur);
+                finish(SEP, j, NA, qA, m_cur, n_cur);
                 // b-slot ownership rotates across lanes every step: the workgroup is
                 // one wave and LDS executes a wave's instructions in issue order
                 __builtin_amdgcn_wave_barrier();
@@ -1084,12 +1138,18 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 pin_vgpr(n_nxt);
                 pin_vgpr(g_after);
                 chain(j + 2, g_after, NA, qA);  // (the last pair's is not used)
-                finish(j + 1, NB, qB, m_nxt, n_nxt);
+                finish(SEP, j + 1, NB, qB, m_nxt, n_nxt);
                 __builtin_amdgcn_wave_barrier();
                 pin_vgpr(m_cur);
                 pin_vgpr(n_cur);
                 pin_vgpr(g_next);
             }
+        };
+        if (je > j0) {
+            if (sep)
+                walk(std::true_type{});
+            else
+                walk(std::false_type{});
             if (je < j1) {
                 gnx = g01[je * 64];
                 mnx = m01[je * 64];
@@ -1116,13 +1176,32 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 int N[2];
                 double q[2];
                 chain(j, gcur, N, q);
-                finish(j, N, q, mcur, ncur);
+                finish(std::false_type{}, j, N, q, mcur, ncur);
                 nact++;
             }
             __builtin_amdgcn_wave_barrier();
         }
         nact += je - j0;
         if (ALLPRES) npat += 27.0 * nact;
+        if (sep) {
+            // the walk sums of the {b}, {a, b} and {b, c} weights relative to 2^R_s:
+            // the block's {b} sum (unit prologue), this a's {a, b} sum over the slots
+            // (wave sum of the slot owners' LDS terms) and the tile row's {b, c} sum
+            const double2 bsm = F.bcsm[t];
+            const int2 bsn = F.bcsn[t];
+            const double2 muab = F.abMu[t];
+            const int2 nab = F.abN[t];
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                int m = s ? nab.y : nab.x;
+                double x = s ? muab.y : muab.x;
+                wave_pair_dpp(m, x);
+                double* Vs = s ? V1 : V0;
+                Vs[0] = ldexp(F.pbS[s], F.pbM[s] - R[s]);
+                Vs[1] = ldexp(x, m - R[s]);
+                Vs[2] = ldexp(s ? bsm.y : bsm.x, (s ? bsn.y : bsn.x) - R[s]);
+            }
+        }
         // ---- members a and c: fold the walk's sums.  Per assignment (xa, xc) of the
         // pair, L = (b in study 0 only) + (b in study 1 only), then b in both from ZS
         double Cw[3][3], Cu[3][3];  // prior-weighted (b's rho, not a's or c's) / plain
@@ -1259,6 +1338,35 @@ int launch_build_skewT(const double* G, int ldg, int pad, double* skew, hipStrea
 int launch_build_bc3(const Sweep3Args& A, int ntile, double2* mu01, int2* n, hipStream_t st) {
     // a non-ALLPRES build is exact for every locus (chi factors of present SNPs are 1)
     hipLaunchKernelGGL((k_build_bc3<false>), dim3(ntile, 64), dim3(64), 0, st, A, mu01, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// per tile and lane t (c = 64C + t): sum over the 64 steps j (every b of block K)
+// of the {b, c} weights 2^bcn * mu01, both studies, at the largest exponent of
+// the lane's nonzero terms (in step order)
+__global__ __launch_bounds__(64) void k_bc3_rowsum(const double2* __restrict__ mu01, const int2* __restrict__ n,
+                                                   double2* __restrict__ sm, int2* __restrict__ sn) {
+    const size_t base = (size_t)blockIdx.x * 4096 + threadIdx.x;
+    int M0 = EMPTY, M1 = EMPTY;
+    for (int j = 0; j < 64; j++) {
+        const double2 m = mu01[base + 64 * j];
+        const int2 e = n[base + 64 * j];
+        if (m.x != 0.0) M0 = max(M0, e.x);
+        if (m.y != 0.0) M1 = max(M1, e.y);
+    }
+    double S0 = 0.0, S1 = 0.0;
+    for (int j = 0; j < 64; j++) {
+        const double2 m = mu01[base + 64 * j];
+        const int2 e = n[base + 64 * j];
+        if (m.x != 0.0) S0 += ldexp(m.x, e.x - M0);
+        if (m.y != 0.0) S1 += ldexp(m.y, e.y - M1);
+    }
+    sm[(size_t)blockIdx.x * 64 + threadIdx.x] = make_double2(S0, S1);
+    sn[(size_t)blockIdx.x * 64 + threadIdx.x] = make_int2(M0, M1);
+}
+
+int launch_bc3_rowsum(int ntile, const double2* mu01, const int2* n, double2* sm, int2* sn, hipStream_t st) {
+    hipLaunchKernelGGL(k_bc3_rowsum, dim3(ntile), dim3(64), 0, st, mu01, n, sm, sn);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
