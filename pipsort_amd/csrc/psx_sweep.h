@@ -95,6 +95,8 @@ struct Sweep3Args {
     const int2* bcn;           // their base-2 exponents, both studies
     const double2* bcsm;       // per [tile][lane]: sum over the tile's 64 b of the {b, c} weights, both
     const int2* bcsn;          //   studies, as 2^bcsn * bcsm (the off-diagonal walk's closed-form sums)
+    const double2* bccm;       // per [tile][b slot]: sum over the tile's 64 c of the {b, c} weights
+    const int2* bccn;
     const double* muS[2];      // singleton weights {c}, by u
     const int* nS[2];
     const unsigned char* pres; // bit s: SNP present in study s, by u
@@ -120,6 +122,8 @@ constexpr int kTileRowPad = 4;  // zero rows after the last tile of mu01 / bcn /
 int launch_build_bc3(const Sweep3Args& A, int ntile, double2* mu01, int2* n, hipStream_t st);
 // per tile and lane c: the sum over the tile's 64 b of the {b, c} weights
 int launch_bc3_rowsum(int ntile, const double2* mu01, const int2* n, double2* sm, int2* sn, hipStream_t st);
+// per tile and b slot: the sum over the tile's 64 c of the {b, c} weights
+int launch_bc3_colsum(int ntile, const double2* mu01, const int2* n, double2* sm, int2* sn, hipStream_t st);
 // out[i] = (a[i], b[i])
 int launch_interleave2(const double* a, const double* b, size_t n, double2* out, hipStream_t st);
 
@@ -132,6 +136,8 @@ struct SweepPlanCache {
     int2* d_bcn = nullptr;
     double2* d_bcsm = nullptr;               // row sums of the {b, c} weights per tile and lane
     int2* d_bcsn = nullptr;
+    double2* d_bccm = nullptr;               // column sums of the {b, c} weights per tile and b slot
+    int2* d_bccn = nullptr;
     double* d_muS[2] = {nullptr, nullptr};   // singleton subset weights
     int* d_nS[2] = {nullptr, nullptr};
     double* d_ys[2] = {nullptr, nullptr};    // scaled y (k = 3 fast kernel)

@@ -547,6 +547,8 @@ static Sweep3Args sweep3_args(const SweepPlanCache& C, const SweepArgs& a, int U
     S3.bcn = C.d_bcn;
     S3.bcsm = C.d_bcsm;
     S3.bcsn = C.d_bcsn;
+    S3.bccm = C.d_bccm;
+    S3.bccn = C.d_bccn;
     S3.g01 = C.d_g01;
     S3.mu01 = C.d_mu01;
     S3.pad = ldg - U;
@@ -572,6 +574,8 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
     hipFree(C.d_bcn); C.d_bcn = nullptr;
     hipFree(C.d_bcsm); C.d_bcsm = nullptr;
     hipFree(C.d_bcsn); C.d_bcsn = nullptr;
+    hipFree(C.d_bccm); C.d_bccm = nullptr;
+    hipFree(C.d_bccn); C.d_bccn = nullptr;
     hipFree(C.d_g01); C.d_g01 = nullptr;
     hipFree(C.d_mu01); C.d_mu01 = nullptr;
     {
@@ -623,6 +627,9 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
         SWCHK(hipMalloc(&C.d_bcsm, sizeof(double2) * (size_t)ntile * 64));
         SWCHK(hipMalloc(&C.d_bcsn, sizeof(int2) * (size_t)ntile * 64));
         if (launch_bc3_rowsum(ntile, C.d_mu01, C.d_bcn, C.d_bcsm, C.d_bcsn, st)) SWCHK(hipGetLastError());
+        SWCHK(hipMalloc(&C.d_bccm, sizeof(double2) * (size_t)ntile * 64));
+        SWCHK(hipMalloc(&C.d_bccn, sizeof(int2) * (size_t)ntile * 64));
+        if (launch_bc3_colsum(ntile, C.d_mu01, C.d_bcn, C.d_bccm, C.d_bccn, st)) SWCHK(hipGetLastError());
         if (launch_interleave2(C.d_skewT[0], C.d_skewT[1], (size_t)ntile * 4096, C.d_g01, st)) SWCHK(hipGetLastError());
     }
     C.skew_ldg = ldg;
@@ -837,6 +844,8 @@ void sweep_free(SweepPlanCache& C) {
     hipFree(C.d_bcn); C.d_bcn = nullptr;
     hipFree(C.d_bcsm); C.d_bcsm = nullptr;
     hipFree(C.d_bcsn); C.d_bcsn = nullptr;
+    hipFree(C.d_bccm); C.d_bccm = nullptr;
+    hipFree(C.d_bccn); C.d_bccn = nullptr;
     hipFree(C.d_g01); C.d_g01 = nullptr;
     hipFree(C.d_mu01); C.d_mu01 = nullptr;
     hipFree(C.d_redo); C.d_redo = nullptr;

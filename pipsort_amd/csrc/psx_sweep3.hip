@@ -327,6 +327,8 @@ struct Sweep3FastSmem {
     // off-diagonal units (closed-form sums, sweep3_unit_fast): this lane's c terms
     double2 bcsm[64];           // the {b, c} weights of this lane's c summed over the block, both studies
     int2 bcsn[64];
+    double2 bccm[64];           // the {b, c} weights of slot b summed over the tile's c, both studies
+    int2 bccn[64];
     double pbS[2];              // sum of the block's {b} weights, both studies: 2^pbM * pbS
     int pbM[2];
 };
@@ -810,6 +812,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     if (sep) {
         F.bcsm[t] = A.bcsm[(size_t)tile * 64 + t];
         F.bcsn[t] = A.bcsn[(size_t)tile * 64 + t];
+        F.bccm[t] = A.bccm[(size_t)tile * 64 + t];
+        F.bccn[t] = A.bccn[(size_t)tile * 64 + t];
 #pragma unroll
         for (int s = 0; s < 2; s++) {
             int m = nBb[s];
@@ -987,6 +991,17 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             // E_s[A + b] of this lane's slot: {b} = pMuB 2^pN, {a, b} = pMu 2^pN
             sW0[t] += fma(pMuB[0], QW[1][0], pMu[0] * QW[1][1]) * ldexp(1.0, pN[0] + Qm[1] - sMt);
             sW1[t] += fma(pMuB[1], QW[0][0], pMu[1] * QW[0][1]) * ldexp(1.0, pN[1] + Qm[0] - sMt);
+            // b in both studies, a and c each in one (different) study, b's partner
+            // subsets {a, b} in one study and {b, c} in the other: per step
+            //   v_0[{b,c}] v_1[{a,b}] 2^(G - sM[b]) = E_0[b, c] E_1[a, b] 2^(-sM[b])
+            // (no lane scale left), summed over c: E_1[a, b] x the tile's column sum
+            // of the {b, c} weights, for both prior-weighted (W2) and plain (sharedLL)
+            // sums (their coefficient in Z0 is 1)
+            const double2 cs = F.bccm[t];
+            const int2 cn = F.bccn[t];
+            const double z0 = fma(pMu[1] * cs.x, ldexp(1.0, pN[1] + cn.x - sMt), pMu[0] * cs.y * ldexp(1.0, pN[0] + cn.y - sMt));
+            sW2[t] += z0;
+            sSl[t] += z0;
         }
         __syncthreads();  // (a, b) terms and slot shifts visible
         if (nxt) {
@@ -1069,8 +1084,10 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                     const int i0 = (xa != 1) | ((xc != 1) << 1), i1 = (xa != 0) | ((xc != 0) << 1);
                     ZS[xa][xc] = fma(v[0][i0], v[1][i1], ZS[xa][xc]);
                 }
-            // Z0: (xa, xc) in {0,1}^2 -> (i0, i1) = (3,0), (1,2), (2,1), (0,3)
-            const double Z0 = fma(v[0][0], v[1][3], fma(v[0][2], v[1][1], fma(v[0][1], v[1][2], v[0][3] * v[1][0])));
+            // Z0: (xa, xc) in {0,1}^2 -> (i0, i1) = (3,0), (1,2), (2,1), (0,3); SEP: the
+            // {b, c} x {a, b} pairs (1,2), (2,1) in closed form (a prologue)
+            const double Z0 = sepc ? fma(v[0][0], v[1][3], v[0][3] * v[1][0])
+                                   : fma(v[0][0], v[1][3], fma(v[0][2], v[1][1], fma(v[0][1], v[1][2], v[0][3] * v[1][0])));
             // Z1: one of a, c in both studies -> (3,1), (1,3), (3,2), (2,3)
             const double Z1 = fma(v[0][2], v[1][3], fma(v[0][3], v[1][2], fma(v[0][1], v[1][3], v[0][3] * v[1][1])));
             const double z22 = v[0][3] * v[1][3];
@@ -1367,6 +1384,37 @@ __global__ __launch_bounds__(64) void k_bc3_rowsum(const double2* __restrict__ m
 
 int launch_bc3_rowsum(int ntile, const double2* mu01, const int2* n, double2* sm, int2* sn, hipStream_t st) {
     hipLaunchKernelGGL(k_bc3_rowsum, dim3(ntile), dim3(64), 0, st, mu01, n, sm, sn);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// per tile and b slot (thread b): the same sum over the 64 c of the tile; slot b
+// sits at step j in lane (b - j) & 63
+__global__ __launch_bounds__(64) void k_bc3_colsum(const double2* __restrict__ mu01, const int2* __restrict__ n,
+                                                   double2* __restrict__ sm, int2* __restrict__ sn) {
+    const size_t base = (size_t)blockIdx.x * 4096;
+    const int b = threadIdx.x;
+    int M0 = EMPTY, M1 = EMPTY;
+    for (int j = 0; j < 64; j++) {
+        const size_t o = base + 64 * j + ((b - j) & 63);
+        const double2 m = mu01[o];
+        const int2 e = n[o];
+        if (m.x != 0.0) M0 = max(M0, e.x);
+        if (m.y != 0.0) M1 = max(M1, e.y);
+    }
+    double S0 = 0.0, S1 = 0.0;
+    for (int j = 0; j < 64; j++) {
+        const size_t o = base + 64 * j + ((b - j) & 63);
+        const double2 m = mu01[o];
+        const int2 e = n[o];
+        if (m.x != 0.0) S0 += ldexp(m.x, e.x - M0);
+        if (m.y != 0.0) S1 += ldexp(m.y, e.y - M1);
+    }
+    sm[(size_t)blockIdx.x * 64 + b] = make_double2(S0, S1);
+    sn[(size_t)blockIdx.x * 64 + b] = make_int2(M0, M1);
+}
+
+int launch_bc3_colsum(int ntile, const double2* mu01, const int2* n, double2* sm, int2* sn, hipStream_t st) {
+    hipLaunchKernelGGL(k_bc3_colsum, dim3(ntile), dim3(64), 0, st, mu01, n, sm, sn);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
