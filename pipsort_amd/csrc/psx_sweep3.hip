@@ -708,7 +708,7 @@ constexpr int kMaxRefGap = 960;  // fast variant: largest n_abc - n_ac (bits, bo
 //      m = [[0, 1], [1, rho]] (prior-weighted) or [[0, 1], [1, 1]] (LL sums)
 // (101 VALU operations instead of 27 products and ~90 partial sums).  Each
 // member's own rho (x = 2) is applied when its record is written.
-template <bool ALLPRES>
+template <bool ALLPRES, bool SEP>
 __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, const int4* __restrict__ units,
                                                  Acc5* __restrict__ rec, SetRec* __restrict__ srec, int rec_stride,
                                                  int* __restrict__ flag, const int* __restrict__ pos, SweepSmem& sm,
@@ -808,7 +808,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     // that factor into (b-only or a,b-only) x (a,c-only) terms have closed forms
     // (sep): the walk sums V_s of the {b}, {a, b} and {b, c} weights, and the b
     // slot's one-study dot products over {b} and {a, b} (see below).
-    const bool sep = !diag && j0 == 0 && j1 == 64;
+    constexpr bool sep = SEP;  // the caller checked !diag && j0 == 0 && j1 == 64
     if (sep) {
         F.bcsm[t] = A.bcsm[(size_t)tile * 64 + t];
         F.bcsn[t] = A.bcsn[(size_t)tile * 64 + t];
@@ -1044,8 +1044,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         // dot products and the walk sums V_s[0 .. 2] have closed forms (a prologue,
         // after the walk).  notSharedLL (NB) stays whole: its per-set precision check
         // (kTinyNs) needs the whole value.
-        auto finish = [&](auto SEP, int j, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
-            constexpr bool sepc = decltype(SEP)::value;
+        auto finish = [&](int j, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
+            constexpr bool sepc = SEP;
             const int bs = (t + j) & 63;
             const double2 aMuB = F.abMuB[bs], aMu = F.abMu[bs];
             const int2 aN = F.abN[bs];
@@ -1119,7 +1119,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             je = j0 + ((j1 - j0) & ~1);
         else if ((va < 64 * K || va >= 64 * K + 64) && 64 * K >= pad)
             je = j0 + ((min(j1, 32) - j0) & ~1);
-        auto walk = [&](auto SEP) {
+        auto walk = [&]() {
             // unrolled by two: the chained state alternates between (NA, qA) and (NB, qB).
             // Loads run up to three rows ahead unclamped (the buffers carry
             // kTileRowPad rows past the last tile; what lies past je is not used),
@@ -1139,7 +1139,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 int2 n_nxt = nb[o + 64];
                 double2 g_after = gb[o + 128];
                 chain(j + 1, g_next, NB, qB);
-                finish(SEP, j, NA, qA, m_cur, n_cur);
+                finish(j, NA, qA, m_cur, n_cur);
                 // b-slot ownership rotates across lanes every step: the workgroup is
                 // one wave and LDS executes a wave's instructions in issue order
                 __builtin_amdgcn_wave_barrier();
@@ -1155,7 +1155,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 pin_vgpr(n_nxt);
                 pin_vgpr(g_after);
                 chain(j + 2, g_after, NA, qA);  // (the last pair's is not used)
-                finish(SEP, j + 1, NB, qB, m_nxt, n_nxt);
+                finish(j + 1, NB, qB, m_nxt, n_nxt);
                 __builtin_amdgcn_wave_barrier();
                 pin_vgpr(m_cur);
                 pin_vgpr(n_cur);
@@ -1163,10 +1163,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             }
         };
         if (je > j0) {
-            if (sep)
-                walk(std::true_type{});
-            else
-                walk(std::false_type{});
+            walk();
             if (je < j1) {
                 gnx = g01[je * 64];
                 mnx = m01[je * 64];
@@ -1193,7 +1190,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 int N[2];
                 double q[2];
                 chain(j, gcur, N, q);
-                finish(std::false_type{}, j, N, q, mcur, ncur);
+                finish(j, N, q, mcur, ncur);  // (never in SEP units: their walk is all pipelined)
                 nact++;
             }
             __builtin_amdgcn_wave_barrier();
@@ -1325,7 +1322,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PSX_K3_WAVES
         return;
     }
     bool redo = false;
-    sweep3_unit_fast<ALLPRES>(A, blockIdx.x, units, rec, srec, rec_stride, flag, pos, sm, redo);
+    // off-diagonal units with the whole b-walk (all of them, as plan_units3c
+    // cuts them) take the closed-form variant; a copy of the unit code each, so
+    // each copy's walk loop gets its own register assignment (one function with
+    // both loops rotated ~14 loop-carried registers per step pair in the other)
+    const int4 un = units[blockIdx.x];
+    if ((un.z & 0xffff) != (un.w & 0xffff) && (un.z >> 16) == 0 && (un.w >> 16) == 64)
+        sweep3_unit_fast<ALLPRES, true>(A, blockIdx.x, units, rec, srec, rec_stride, flag, pos, sm, redo);
+    else
+        sweep3_unit_fast<ALLPRES, false>(A, blockIdx.x, units, rec, srec, rec_stride, flag, pos, sm, redo);
     if (redo) {
         if (threadIdx.x == 0 && A.redo_count) atomicAdd(A.redo_count, 1);
         __syncthreads();
