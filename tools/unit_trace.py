@@ -44,6 +44,9 @@ order = np.argsort(st)
 print("start time by unit index decile (us):",
       [round(float((st[order][int(q * (len(st) - 1))] - t0) / 100.0), 1) for q in np.linspace(0, 1, 11)])
 uid = tr[:, 3] & 0xffffffff
+redo = (tr[:, 3] >> 40) & 1
+print(f"units redone by the robust variant: {int(redo.sum())} (mean duration {dur[redo == 1].mean() if redo.any() else 0:.1f} us); "
+      f"busy unit-us {dur.sum():.0f}")
 diag = (tr[:, 3] >> 32) & 1
 na = tr[:, 3] >> 33
 for dflag in (0, 1):
