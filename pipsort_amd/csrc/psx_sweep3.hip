@@ -1044,18 +1044,29 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         // dot products and the walk sums V_s[0 .. 2] have closed forms (a prologue,
         // after the walk).  notSharedLL (NB) stays whole: its per-set precision check
         // (kTinyNs) needs the whole value.
-        auto finish = [&](int j, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
+        // finish(j)'s LDS operands: its slot's {b} / {a, b} terms and scale, and the
+        // exp2 table entries of the chain's split (read as soon as the chain ends)
+        struct FTt {
+            double2 muB, mu;
+            int2 n;
+            double sF, tb0, tb1;
+        };
+        auto ld_ft = [&](int j, const int (&N)[2]) {
+            const int bs = (t + j) & 63;
+            return FTt{F.abMuB[bs], F.abMu[bs], F.abN[bs], sF[bs], tab[N[0] & 255], tab[N[1] & 255]};
+        };
+        auto finish_ft = [&](int j, const FTt& ft, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
             constexpr bool sepc = SEP;
             const int bs = (t + j) & 63;
-            const double2 aMuB = F.abMuB[bs], aMu = F.abMu[bs];
-            const int2 aN = F.abN[bs];
+            const double2 aMuB = ft.muB, aMu = ft.mu;
+            const int2 aN = ft.n;
             // v[s][A] = E_s[A + b] relative to 2^{R_s}: {b}, {a, b}, {b, c}, {a, b, c}
             double v[2][4];
             int d3s = 0;
 #pragma unroll
             for (int s = 0; s < 2; s++) {
                 const int d3 = N[s] >> 8;  // n3 - R (N is R-relative)
-                const double mu3 = tab[N[s] & 255] * q[s];
+                const double mu3 = (s ? ft.tb1 : ft.tb0) * q[s];
                 const int n2 = s ? ncur.y : ncur.x;
                 const double mu2 = s ? mcur.y : mcur.x;
                 const int dab = (s ? aN.y : aN.x) - R[s];
@@ -1100,7 +1111,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             }
             tiny |= NB < kTinyNs;
             // ---- b slot (LDS, x fS) ----
-            const double fS = sF[bs] * gF;
+            const double fS = ft.sF * gF;
             // LDS float adds: no read round trip; one lane per slot per step, and a
             // wave's LDS instructions execute in issue order (deterministic)
             __hip_atomic_fetch_add(&sW0[bs], WB0 * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1109,6 +1120,9 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             __hip_atomic_fetch_add(&sSl[bs], LB2 * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&sNs[bs], NB * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (!ALLPRES) npat += wac * bW[bs];
+        };
+        auto finish = [&](int j, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
+            finish_ft(j, ld_ft(j, N), N, q, mcur, ncur);
         };
         // Steps on which every lane is active run pipelined: the whole walk of an
         // off-diagonal tile, and steps 1..30 of a diagonal tile whose a lies
@@ -1133,13 +1147,17 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             int NA[2], NB[2];
             double qA[2], qB[2];
             chain(j0, gnx, NA, qA);
+            // each finish's LDS operands are read right after the chain it follows,
+            // one half step pair before the finish runs
+            FTt ftA = ld_ft(j0, NA);
             for (int j = j0; j < je; j += 2) {
                 const int o = j * 64 + t;
                 double2 m_nxt = mb[o + 64];
                 int2 n_nxt = nb[o + 64];
                 double2 g_after = gb[o + 128];
                 chain(j + 1, g_next, NB, qB);
-                finish(j, NA, qA, m_cur, n_cur);
+                finish_ft(j, ftA, NA, qA, m_cur, n_cur);
+                const FTt ftB = ld_ft(j + 1, NB);
                 // b-slot ownership rotates across lanes every step: the workgroup is
                 // one wave and LDS executes a wave's instructions in issue order
                 __builtin_amdgcn_wave_barrier();
@@ -1155,7 +1173,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 pin_vgpr(n_nxt);
                 pin_vgpr(g_after);
                 chain(j + 2, g_after, NA, qA);  // (the last pair's is not used)
-                finish(j + 1, NB, qB, m_nxt, n_nxt);
+                finish_ft(j + 1, ftB, NB, qB, m_nxt, n_nxt);
+                ftA = ld_ft(j + 2, NA);
                 __builtin_amdgcn_wave_barrier();
                 pin_vgpr(m_cur);
                 pin_vgpr(n_cur);
