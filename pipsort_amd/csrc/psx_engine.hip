@@ -19,8 +19,6 @@
 #include <tuple>
 #include <vector>
 #include <thread>
-#include <atomic>
-#include <sched.h>
 
 #include "../../include/pipsort_engine.h"
 #include "../../include/pipsort_model.h"
@@ -2092,72 +2090,6 @@ __global__ void k_map_rehash(const MapEntry* __restrict__ old, size_t n, MapEntr
     if (i < n && old[i].state) map_insert(T, mask, old[i].lo, old[i].hi, old[i].score);
 }
 
-// The walk's sampling weights exp(lk - max) (sss_postcal.cpp:296-328) on a few
-// host threads that spin between iterations: each std::exp is independent, so
-// slicing the loop leaves every weight bit-identical to the serial loop (the
-// sums and the discrete_distribution stay serial, in the reference's order).
-// ~10 us of the ~50 us iteration at 1,000 neighbours on one core.
-class ExpPool {
-  public:
-    explicit ExpPool(int n) : n_(n) {
-        for (int w = 1; w < n_; w++) th_.emplace_back([this, w] { loop(w); });
-    }
-    ~ExpPool() {
-        quit_.store(true, std::memory_order_release);
-        for (auto& t : th_) t.join();
-    }
-    // out[i] = exp(in[i] - mx), i < len
-    void run(const double* in, double mx, double* out, int len) {
-        if (n_ == 1 || len < 512) {
-            for (int i = 0; i < len; i++) out[i] = std::exp(in[i] - mx);
-            return;
-        }
-        in_ = in;
-        mx_ = mx;
-        out_ = out;
-        len_ = len;
-        done_.store(0, std::memory_order_relaxed);
-        gen_.fetch_add(1, std::memory_order_release);
-        slice(0);
-        while (done_.load(std::memory_order_acquire) < n_ - 1) __builtin_ia32_pause();
-    }
-
-  private:
-    void slice(int w) {
-        const int b = (int)((int64_t)len_ * w / n_), e = (int)((int64_t)len_ * (w + 1) / n_);
-        for (int i = b; i < e; i++) out_[i] = std::exp(in_[i] - mx_);
-    }
-    void loop(int w) {
-        unsigned seen = 0;
-        for (;;) {
-            unsigned g;
-            while ((g = gen_.load(std::memory_order_acquire)) == seen) {
-                if (quit_.load(std::memory_order_acquire)) return;
-                __builtin_ia32_pause();
-            }
-            seen = g;
-            slice(w);
-            done_.fetch_add(1, std::memory_order_release);
-        }
-    }
-    int n_;
-    std::vector<std::thread> th_;
-    std::atomic<unsigned> gen_{0};
-    std::atomic<int> done_{0};
-    std::atomic<bool> quit_{false};
-    const double* in_ = nullptr;
-    double* out_ = nullptr;
-    double mx_ = 0.0;
-    int len_ = 0;
-};
-
-int sampling_threads() {
-    cpu_set_t set;
-    CPU_ZERO(&set);
-    const int cores = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
-    return std::max(1, std::min(4, cores / 2));
-}
-
 struct SssDev {
     MapEntry* T = nullptr;
     size_t cap = 0, used = 0;
@@ -2219,7 +2151,6 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
     if ((rc = ensure(e->dscore, e->cap_score, nmax))) return rc;
     const SetRec null1 = null_rec(e, 1.0);
     std::mt19937 gen(12345);
-    ExpPool pool(world == 1 ? sampling_threads() : 1);  // sharded walks: one rank per thread already
     int cur[PSX_KMAX] = {0, 0, 0, 0, 0, 0}, k = 0;  // the current configuration, ascending
     double old_sum = 0;
     int iter;
@@ -2341,7 +2272,9 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
         auto group = [&](int b, int en, double& wsum, size_t& smp) {
             pr.resize((size_t)(en - b));
             double mx = *std::max_element(lk + b, lk + en);
-            pool.run(lk + b, mx, pr.data(), en - b);
+            // (slicing these exps over spinning host threads measured slower: the
+            // serial loop takes ~5 us at 1,000 neighbours, profiles/r03v_sss_threads.txt)
+            for (int ii = b; ii < en; ii++) pr[ii - b] = std::exp(lk[ii] - mx);
             std::discrete_distribution<size_t> dist(pr.begin(), pr.end());
             smp = dist(gen);
             wsum = std::accumulate(pr.begin(), pr.end(), 0.0);
