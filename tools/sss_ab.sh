@@ -1,5 +1,6 @@
 #!/bin/bash
 # SSS walk timing A/B over PSX_SSS_THREADS values (alternating): bash tools/sss_ab.sh "1 4" reps
+# (r03v; the knob and the exp thread pool it sized were removed after this A/B)
 mkdir -p gpurun_out/sss_ab
 for r in $(seq 1 ${2:-3}); do
   for n in $1; do
