@@ -177,14 +177,17 @@ __device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride
     }
     __syncthreads();
     const int nsub = 1 << k;
-    if (lane < nsub) {
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
+    // one (study, subset) per lane: 2^k subsets of both studies (one pass for
+    // k <= 5, two for k = 6) — half the serial chain of a lane doing both studies
+    for (int wk = lane; wk < 2 * nsub; wk += 64) {
+        const int s = wk >> k, sub = wk & (nsub - 1);
+        {
             double L[KM][KM], D[KM], Rd[KM], w[KM];
             double q = 0.0, Pd = 1.0;
+            const double dv = s ? P.dval[1] : P.dval[0];
 #pragma unroll
             for (int i = 0; i < KM; i++) {
-                const bool in = i < k && ((lane >> i) & 1);
+                const bool in = i < k && ((sub >> i) & 1);
                 double di = 1.0, wi = 0.0;
 #pragma unroll
                 for (int j = 0; j < i; j++) {
@@ -192,7 +195,7 @@ __device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride
 #pragma unroll
                     for (int m = 0; m < j; m++) acc -= L[i][m] * L[j][m] * D[m];
                     // L[j][*] = 0 and D[j] = 1 for j outside the subset
-                    L[i][j] = in && ((lane >> j) & 1) ? acc * Rd[j] : 0.0;
+                    L[i][j] = in && ((sub >> j) & 1) ? acc * Rd[j] : 0.0;
                 }
                 if (in) {
                     di = s_ad[s][i];
@@ -208,7 +211,7 @@ __device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride
                 Rd[i] = 1.0 / di;
                 if (in) {
                     q += wi * wi * Rd[i];
-                    Pd *= P.dval[s] * di;
+                    Pd *= dv * di;
                 }
                 D[i] = di;
                 w[i] = wi;
@@ -216,9 +219,9 @@ __device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride
             int n;
             double mu;
             psx::split_exp(0.5 * q * PSX_LOG2E, 1.0 / sqrt(Pd), n, mu);
-            s_mu[s][lane] = mu;
-            s_n[s][lane] = n;
-            s_f[s][lane] = 0.5 * q - 0.5 * log(Pd);
+            s_mu[s][sub] = mu;
+            s_n[s][sub] = n;
+            s_f[s][sub] = 0.5 * q - 0.5 * log(Pd);
         }
     }
     __syncthreads();
@@ -1942,6 +1945,9 @@ __global__ __launch_bounds__(64) void k_sss_eval(DevProb P, SssIter it, const Ma
         }
     }
     if (seen || n == 0 || p < lo || p >= hi) return;
+#ifdef PSX_SSS_ABLATE
+    if (PSX_SSS_ABLATE == 1) return;
+#endif
 #pragma unroll
     for (int j = 0; j < PSX_KMAX; j++)
         if (j < it.stride && lane == j) {
