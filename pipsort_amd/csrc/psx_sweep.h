@@ -13,7 +13,7 @@
 // sized for (a build-time A/B knob, tools/build_variant.sh; the product build
 // uses the default)
 #ifndef PSX_K3_ROUNDS
-#define PSX_K3_ROUNDS 3.5
+#define PSX_K3_ROUNDS 2.0
 #endif
 
 #include <hip/hip_runtime.h>
