@@ -312,8 +312,8 @@ struct Sweep3Smem {
 };
 // LDS of the fast k = 3 variant: the per-b terms of both studies side by side
 // (one 16-byte read per term and step; lane t reads slot (t + j) & 63, so the
-// reads are conflict-free), and the b-slot accumulators with their per-a scale
-// factor sF = 2^(Gm - sM) (Gm: the wave's largest a shift)
+// reads are conflict-free), and the b-slot accumulators (one shift sM for every
+// slot: all slots move up to the wave's largest a shift together)
 struct Sweep3FastSmem {
     double tab[256];
     double2 aAd[kMaxChunkA3], aY[kMaxChunkA3];  // the unit's a: A_aa, y_a (both studies), presence
@@ -321,7 +321,6 @@ struct Sweep3FastSmem {
     int aPos[kMaxChunkA3];  // a record positions
     double2 abG[64], abI[64], abIW[64], abH[64], abR[64], abMu[64], abMuB[64];
     int2 abN[64];
-    double sF[64];
     float bW[64];  // membership weight of the slot's b (0, 1 or 3)
     double sW0[64], sW1[64], sW2[64], sSl[64], sNs[64];
     // off-diagonal units (closed-form sums, sweep3_unit_fast): this lane's c terms
@@ -721,7 +720,6 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     double (&sW2)[64] = F.sW2;
     double (&sSl)[64] = F.sSl;
     double (&sNs)[64] = F.sNs;
-    double (&sF)[64] = F.sF;
 
     const int t = threadIdx.x;
     const unsigned long long t_start = A.trace ? wall_clock64() : 0ull;
@@ -755,7 +753,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         F.aPos[t] = pos[(size_t)unit * rec_stride + 128 + t];
     }
     bW[t] = (float)memb_weight(pbl);
-    int sMt = EMPTY;  // shift of b slot t (lane-owned outside the walk)
+    int sMt = EMPTY;  // shift of the b slots (wave-uniform: every a moves all slots alike)
     sW0[t] = sW1[t] = sW2[t] = sSl[t] = sNs[t] = 0.0;
 
     const int vc = 64 * C + t, uc = vc - pad;
@@ -958,7 +956,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         // the walk's split constants as opaque registers (split3r)
         double k256 = 256.0, kc3 = kC3, kc2 = kC2;
         asm volatile("" : "+s"(k256), "+s"(kc3), "+v"(kc2));
-        double gF;
+        double fS;  // a lane's contribution to the b slots is scaled by 2^(G - sM)
         {
             const int Gm = __ockl_wfred_max_i32(G);  // DPP wave reduction, no LDS round trips
             const int Ms = max(sMt, Gm), d = sMt - Ms;
@@ -968,10 +966,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             sSl[t] = ldexp(sSl[t], d);
             sNs[t] = ldexp(sNs[t], d);
             sMt = Ms;
-            // a lane's contribution to slot b is scaled by 2^(G - sM[b]) = sF[b] * gF
-            // (powers of two: the product is exact down to the underflow either form has)
-            sF[t] = ldexp(1.0, Gm - Ms);
-            gF = ldexp(1.0, G - Gm);
+            fS = ldexp(1.0, G - Ms);
         }
         if (sep) {
             // b in one study, subsets {} and {a} of {a, c} with b: over the walk
@@ -1003,6 +998,12 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             sW2[t] += z0;
             sSl[t] += z0;
         }
+        // the slot scale rides in the prior-weighted vectors (only the b-slot dot
+        // products use them from here on; a power of two, so exact above underflow)
+#pragma unroll
+        for (int s = 0; s < 2; s++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) uW[s][i] *= fS;
         __syncthreads();  // (a, b) terms and slot shifts visible
         if (nxt) {
 #pragma unroll
@@ -1049,11 +1050,11 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         struct FTt {
             double2 muB, mu;
             int2 n;
-            double sF, tb0, tb1;
+            double tb0, tb1;
         };
         auto ld_ft = [&](int j, const int (&N)[2]) {
             const int bs = (t + j) & 63;
-            return FTt{F.abMuB[bs], F.abMu[bs], F.abN[bs], sF[bs], tab[N[0] & 255], tab[N[1] & 255]};
+            return FTt{F.abMuB[bs], F.abMu[bs], F.abN[bs], tab[N[0] & 255], tab[N[1] & 255]};
         };
         auto finish_ft = [&](int j, const FTt& ft, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
             constexpr bool sepc = SEP;
@@ -1110,12 +1111,11 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 V1[i] += v[1][i];
             }
             tiny |= NB < kTinyNs;
-            // ---- b slot (LDS, x fS) ----
-            const double fS = ft.sF * gF;
+            // ---- b slot (LDS, x fS: WB0 / WB1 carry it from uW) ----
             // LDS float adds: no read round trip; one lane per slot per step, and a
             // wave's LDS instructions execute in issue order (deterministic)
-            __hip_atomic_fetch_add(&sW0[bs], WB0 * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&sW1[bs], WB1 * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&sW0[bs], WB0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&sW1[bs], WB1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&sW2[bs], WB2 * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&sSl[bs], LB2 * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&sNs[bs], NB * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
