@@ -124,18 +124,31 @@ def host_cores():
     return n, quota
 
 
+def usable_cores():
+    """Threads the CPU baselines run: min(affinity set, cgroup CPU quota), so
+    `cores` counts CPUs the process can actually run on at once (256 threads on
+    a 16-CPU quota would time 16 CPUs, oversubscribed)."""
+    n, quota = host_cores()
+    return max(1, min(n, int(quota))) if quota is not None else n
+
+
 def cores_note(threads):
     n, quota = host_cores()
-    return (f"{threads} host threads = the {n} CPUs of this process's affinity set"
-            + (f" (cgroup CPU quota {quota:g})" if quota is not None else " (no cgroup CPU quota)"))
+    return (f"{threads} host threads = min(the {n} CPUs of this process's affinity set, "
+            + (f"cgroup CPU quota {quota:g})" if quota is not None else "no cgroup CPU quota)"))
+
+
+def cores_fields(threads):
+    n, quota = host_cores()
+    return {"cores": threads, "affinity_cpus": n, "cgroup_cpu_quota": quota}
 
 
 def cpu_baseline(seam, budget_s=15.0, threads=None):
     """Oracle literal (N x N, postcal.cpp:214-304) per-configuration cost on the
-    host cores (every CPU of the affinity set), on a random sample of this
-    workload's configurations."""
+    host cores (usable_cores()), on a random sample of this workload's
+    configurations."""
     from oracle import oracle as O
-    threads = threads or host_cores()[0]
+    threads = threads or usable_cores()
     U = seam.n_union
     k = int(seam.max_causal)
     rng = np.random.default_rng(0)
@@ -174,7 +187,7 @@ def cpu_baseline(seam, budget_s=15.0, threads=None):
         x.join()
     dt = time.time() - t0
     n = sum(done)
-    return {"value": n / dt, "unit": "configs/s", "cores": threads, "kind": "port",
+    return {"value": n / dt, "unit": "configs/s", **cores_fields(threads), "kind": "port",
             "sample": f"{n} random {k}-SNP configurations of this workload, oracle literal N x N "
                       f"restatement of lowrank_likelihood (postcal.cpp:214-304), {cores_note(threads)}, "
                       f"{dt:.1f} s"}
@@ -210,7 +223,7 @@ def cpu_baseline_example(threads=None):
     L values are checked against the reference's expected_study*_post.txt."""
     from oracle import oracle as O
     import loci
-    threads = threads or host_cores()[0]
+    threads = threads or usable_cores()
     seam = build_seam("example")
     levels = example_patterns(seam)
     O.load()
@@ -269,7 +282,7 @@ def cpu_baseline_example(threads=None):
                .read().splitlines()[1:]]
         got = acc[s * m0: s * m0 + len(exp)]
         ok = ok and bool(np.all(np.abs(got - np.array(exp)) <= 5e-6 * np.maximum(np.abs(exp), 1e-300) + 1e-12))
-    return {"value": n / dt, "unit": "configs/s", "cores": threads, "kind": "port", "wall_s": dt, "configs": n,
+    return {"value": n / dt, "unit": "configs/s", **cores_fields(threads), "kind": "port", "wall_s": dt, "configs": n,
             "pips_match_reference_expected": ok,
             "sample": f"full tests/example c=2 sweep ({n} configurations), oracle literal N x N restatement of "
                       f"lowrank_likelihood (postcal.cpp:214-304), {cores_note(threads)}; PIPs checked against "
@@ -689,15 +702,22 @@ def main():
                          + (f" / {world} (this rank's shard)" if world > 1 else ""))
         else:
             flops = tm["flops"]
-            flops_src = "model: 159 FP64 operations per 3-SNP union set (PMC-calibrated, r02zd build)"
+            flops_src = ("model: 138 FP64 operations per 3-SNP union set (fitted to the PMC count of the last "
+                         "collected build, a lower bound for later ones) - NOT counters of this build")
         achieved = flops / avg_kernel_s / 1e12 if avg_kernel_s > 0 else 0.0
-        roofline = {"bound": "valu_fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": achieved / FP64_PEAK_TFLOPS,
+        # the roofline fraction is reported only from counters of this very build;
+        # without them the model's figure goes to a separately named field
+        have_pmc = bool(pmc and pmc.get("fp64_flop_insts_per_launch"))
+        roofline = {"bound": "valu_fp64", "achieved": achieved if have_pmc else None, "peak": FP64_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS if have_pmc else None,
                     "traffic": (pmc or {}).get("hbm_bytes_per_launch") if world == 1 else None,
                     "kernel": "k_sweep3" if seam.max_causal >= 3 else "k_sweep<2>",
                     "kernel_ms": avg_kernel_s * 1e3,
                     "flops_per_launch": flops, "flops_source": flops_src,
                     "pmc_kernel_src_sha": (pmc or {}).get("kernel_src_sha"), "kernel_src_sha": kernel_src_sha()}
+        if not have_pmc:
+            roofline["model_achieved"] = achieved
+            roofline["model_frac"] = achieved / FP64_PEAK_TFLOPS
         if pmc and pmc.get("valu_insts_per_launch") and avg_kernel_s > 0:
             roofline["valu_issue"] = valu_issue_roof(pmc, avg_kernel_s, world)
         if pmc and world == 1:

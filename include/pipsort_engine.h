@@ -89,6 +89,11 @@ int psx_device_count(int *count);
  * pay for it.  Thread-safe; the drop-in CLI calls it on a second thread while
  * it parses the LD / z files (model.h:86-144), overlapping the two. */
 int psx_warmup(int device);
+/* The same, loading only the device code a run of this shape uses: the k = 3
+ * sweep's only for max_causal >= 3, the configs-file path's only when
+ * configs_file != 0 (psx_warmup(d) = psx_warmup_for(d, 3, 0)).  With PSX_TIMING
+ * set it prints its phases (context, each code object) on stderr. */
+int psx_warmup_for(int device, int32_t max_causal, int32_t configs_file);
 
 /* PostCal::PostCal (postcal.h:118-195).  Copies the problem to device `device`,
  * forms Sigma~_s = B_s^T B_s, y_s = B_s^T S'_s and ||S'||^2 on the GPU. */

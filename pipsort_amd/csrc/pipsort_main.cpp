@@ -411,7 +411,9 @@ int main(int argc, char* argv[]) {
     g_multi = devices.size() > 1;
     // the HIP runtime / contexts come up on a second thread while the inputs
     // are parsed (errors, if any, surface again at psx_create*)
-    std::thread warm([devices] {
+    const int warm_c = sss_flag == 1 ? 0 : totalCausalSNP;  // SSS batches run the generic set kernel
+    const int warm_b = configsFile != "";
+    std::thread warm([devices, warm_c, warm_b] {
         g_ph.rt0 = epoch_ms();
         int nd = 0;
         psx_device_count(&nd);  // the HIP runtime
@@ -420,7 +422,7 @@ int main(int argc, char* argv[]) {
         for (int32_t d : devices)
             if (std::find(seen.begin(), seen.end(), d) == seen.end()) {
                 seen.push_back(d);
-                psx_warmup(d);
+                psx_warmup_for(d, warm_c, warm_b);
             }
         g_ph.warm1 = epoch_ms();
     });

@@ -1495,28 +1495,47 @@ int gpu_ready(int device) {
 }
 }  // namespace
 
-int psx_warmup(int device) {
+int psx_warmup_for(int device, int32_t max_causal, int32_t configs_file) {
+    // PSX_TIMING: the warm-up's phases on stderr (module load costs per
+    // translation unit; each is its own code object, loaded on first use)
+    const bool trace = getenv("PSX_TIMING") != nullptr;
+    auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    double t[7] = {now(), 0, 0, 0, 0, 0, 0};
     int rc;
     if ((rc = gpu_ready(device))) return rc;
     HIPCHK(hipFree(nullptr));  // context
-    // one launch loads the device code
+    t[1] = now();
+    // one launch loads this translation unit's device code
     double* d = nullptr;
     HIPCHK(hipMalloc(&d, 64 * sizeof(double)));
     hipLaunchKernelGGL(k_diag, dim3(1), dim3(64), 0, nullptr, d, 8, d + 8);
     hipError_t le = hipGetLastError();
     hipError_t se = hipDeviceSynchronize();
     hipFree(d);
-    // and the device code of the Model setup and the exhaustive sweep (each
-    // translation unit its own code object), which the first create / pass would
-    // otherwise load on first use; the configs-file code object (hipcub's radix
-    // sort, the largest) loads on its first use only
-    if (le == hipSuccess && se == hipSuccess &&
-        (psx::warm_module_setup() || psx::warm_module_sweep() || psx::warm_module_sweep3()))
-        return fail(PSX_EHIP, "warm-up: device code of a translation unit did not load");
     if (le != hipSuccess || se != hipSuccess)
         return fail(PSX_EHIP, std::string("warm-up: ") + hipGetErrorString(le != hipSuccess ? le : se));
+    t[2] = now();
+    // then the code objects the run will use, which the first create / pass
+    // would otherwise load: the Model setup and the tiled sweep always, the
+    // k = 3 sweep only for c >= 3, the configs-file path (hipcub's radix sort,
+    // the largest) only for a -b run
+    if (psx::warm_module_setup()) return fail(PSX_EHIP, "warm-up: setup device code did not load");
+    t[3] = now();
+    if (psx::warm_module_sweep()) return fail(PSX_EHIP, "warm-up: sweep device code did not load");
+    t[4] = now();
+    if (max_causal >= 3 && psx::warm_module_sweep3()) return fail(PSX_EHIP, "warm-up: k = 3 device code did not load");
+    t[5] = now();
+    if (configs_file && psx::warm_module_configs()) return fail(PSX_EHIP, "warm-up: configs device code did not load");
+    t[6] = now();
+    if (trace)
+        fprintf(stderr,
+                "psx-warm {\"context_ms\": %.3f, \"engine_module_ms\": %.3f, \"setup_module_ms\": %.3f, "
+                "\"sweep_module_ms\": %.3f, \"sweep3_module_ms\": %.3f, \"configs_module_ms\": %.3f}\n",
+                t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4], t[6] - t[5]);
     return 0;
 }
+
+int psx_warmup(int device) { return psx_warmup_for(device, 3, 0); }
 
 int psx_lu_det_gpu(const double* a, int32_t m, int device, double* det) {
     if (!a || m <= 0 || !det) return fail(PSX_EINVAL, "bad argument");
@@ -1611,7 +1630,14 @@ int psx_sync(psx_engine* e, int32_t* exact_needed) {
     HIPCHK(hipMemsetAsync(e->dflag + 1, 0, sizeof(int), e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     if (exact_needed) *exact_needed = sticky;
-    if (e->a_pending == 0 && e->a_count == 0) return 0;  // nothing asynchronous since the last sync
+    if (e->a_pending == 0 && e->a_count == 0) {
+        // nothing asynchronous since the last sync: the count still follows the
+        // accumulators just read (a merge of partial images folds the shards')
+        SetRec st;
+        std::memcpy(&st, e->hstat, sizeof(SetRec));
+        e->timing.configs = (uint64_t)(st.npat + 0.5);
+        return 0;
+    }
     while (e->a_pending > 0)
         if ((rc = consume_async(e))) return rc;
     // timing of the asynchronous passes since the last sync: the dominant

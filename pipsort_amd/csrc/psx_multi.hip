@@ -144,6 +144,7 @@ struct psx_multi {
     int64_t bytes = 0;
     double sweep_ms = 0;
     uint64_t configs = 0;
+    int32_t exact = 0;  // the last exhaustive step took the EXACT rerun
     ShardPool* pool = nullptr;
 };
 
@@ -358,6 +359,7 @@ int psx_multi_run_exhaustive(psx_multi* m) {
             return r;
         });
     if (rc) return rc;
+    m->exact = exact;
     if (exact) return run_and_gather(m, [&](int i) { return psx_run_exhaustive(m->h[i]); });
     shard_times(m);
     total_configs(m, true);
@@ -365,6 +367,7 @@ int psx_multi_run_exhaustive(psx_multi* m) {
 }
 
 int psx_multi_run_configs(psx_multi* m, const int16_t* rows, int64_t n_rows, int32_t n_groups) {
+    m->exact = 0;
     return run_and_gather(m, [&](int i) { return psx_run_configs(m->h[i], rows, n_rows, n_groups); });
 }
 
@@ -374,6 +377,7 @@ int psx_multi_run_sss(psx_multi* m, int32_t* iterations_out) {
     g.n = n;
     std::vector<GatherCtx> ctx(n);
     std::vector<int32_t> it(n, 0);
+    m->exact = 0;
     for (int i = 0; i < n; i++) ctx[i] = GatherCtx{&g, i};
     int rc = run_and_gather(m, [&](int i) {
         const int r = psx_run_sss_sharded(m->h[i], gather_fn, &ctx[i], &it[i]);
@@ -398,6 +402,12 @@ int psx_multi_get_timing(psx_multi* m, psx_timing* t) {
     }
     t->sweep_ms = m->sweep_ms;  // the slowest shard's pass
     t->configs = m->configs;
+    // any shard's flag: handle 0's own may be clear while another shard reran
+    t->exact_rerun = m->exact;
+    for (psx_engine* e : m->h) {
+        psx_timing u;
+        if (psx_get_timing(e, &u) == 0 && u.exact_rerun) t->exact_rerun = 1;
+    }
     return 0;
 }
 

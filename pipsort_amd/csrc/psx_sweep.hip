@@ -454,12 +454,13 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     P.n_units = (int)mine.size();
     P.union_sets = (uint64_t)sets;
     P.alg_bytes = bytes;
-    // FP64 operations per union set (FMA = 2), calibrated from the PMC FP64
-    // counts of the k = 3 fast kernel (profiles/r02zd_pmc.json: 64 x
-    // SQ_INSTS_VALU_FLOPS_FP64 / sets = 159 with the deferred fold; 281 before it);
-    // k = 2 by the round-1 ratio of VALU work per set.  Used only when bench.py
-    // has no PMC file of the same kernel build.
-    P.flops = sets * (k == 3 ? 159.0 : 110.0);
+    // FP64 operations per union set (FMA = 2), fitted to the PMC FP64 counts of
+    // the k = 3 fast kernel (64 x SQ_INSTS_VALU_FLOPS_FP64 / sets: 281 before the
+    // deferred fold, 159 after it (r02zd), 141.8 in r03zb, ~139 since the uniform
+    // slot shift): kept at or below the last count, so a bench line without PMC
+    // counters of its own build cannot overstate the FP64 rate; k = 2 by the
+    // round-1 ratio of VALU work per set.  bench.py reports it only as a model.
+    P.flops = sets * (k == 3 ? 138.0 : 110.0);
     const int pad = variant ? ldg - U : 0;  // record keys of variant 1 are in v space
     // device buffers
     std::vector<int4> hu(P.n_units);
@@ -561,16 +562,11 @@ static Sweep3Args sweep3_args(const SweepPlanCache& C, const SweepArgs& a, int U
     return S3;
 }
 
-static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hipStream_t st) {
-    if (C.d_skew[0] && C.skew_ldg == ldg && C.skew_src[0] == a.G0 && C.skew_src[1] == a.G1) return 0;
+static void free_k3(SweepPlanCache& C) {
     for (int s = 0; s < 2; s++) {
-        hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
         hipFree(C.d_skewT[s]); C.d_skewT[s] = nullptr;
-        hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
-        hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
         hipFree(C.d_ys[s]); C.d_ys[s] = nullptr;
     }
-    hipFree(C.d_tab); C.d_tab = nullptr;
     hipFree(C.d_bcn); C.d_bcn = nullptr;
     hipFree(C.d_bcsm); C.d_bcsm = nullptr;
     hipFree(C.d_bcsn); C.d_bcsn = nullptr;
@@ -578,6 +574,19 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
     hipFree(C.d_bccn); C.d_bccn = nullptr;
     hipFree(C.d_g01); C.d_g01 = nullptr;
     hipFree(C.d_mu01); C.d_mu01 = nullptr;
+}
+
+// the layouts every tiled level reads (skewed Sigma~ tiles, singleton weights,
+// the exp2 table), built once per locus
+static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hipStream_t st) {
+    if (C.d_skew[0] && C.skew_ldg == ldg && C.skew_src[0] == a.G0 && C.skew_src[1] == a.G1) return 0;
+    free_k3(C);
+    for (int s = 0; s < 2; s++) {
+        hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
+        hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
+        hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
+    }
+    hipFree(C.d_tab); C.d_tab = nullptr;
     {
         // 2^(i/256) correctly rounded (long double on the host)
         double tab[256];
@@ -591,8 +600,6 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
         for (int u = 0; u < U; u++) C.allpres = C.allpres && pres[u] == 3;
     }
     for (int s = 0; s < 2; s++) {
-        SWCHK(hipMalloc(&C.d_ys[s], sizeof(double) * ldg));
-        if (launch_scale_y(s ? a.y1 : a.y0, ldg, C.d_ys[s], st)) SWCHK(hipGetLastError());
         SWCHK(hipMalloc(&C.d_muS[s], sizeof(double) * ldg));
         SWCHK(hipMalloc(&C.d_nS[s], sizeof(int) * ldg));
         hipLaunchKernelGGL(k_build_singles, dim3((ldg + 255) / 256), dim3(256), 0, st, s ? a.Ad1 : a.Ad0,
@@ -602,8 +609,6 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
     const int nblk = ldg / 64;
     const int ntile = nblk * (nblk + 1) / 2;
     for (int s = 0; s < 2; s++) {
-        SWCHK(hipMalloc(&C.d_skewT[s], sizeof(double) * (size_t)ntile * 4096));
-        if (launch_build_skewT(s ? a.G1 : a.G0, ldg, ldg - U, C.d_skewT[s], st)) SWCHK(hipGetLastError());
         SWCHK(hipMalloc(&C.d_skew[s], sizeof(double) * (size_t)ntile * 4096));
         hipLaunchKernelGGL(k_build_skew, dim3(ntile, 64), dim3(64), 0, st, s ? a.G1 : a.G0, ldg, nblk, C.d_skew[s]);
         SWCHK(hipGetLastError());
@@ -611,6 +616,25 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
     if (!C.d_redo) {
         SWCHK(hipMalloc(&C.d_redo, sizeof(int)));
         SWCHK(hipMemsetAsync(C.d_redo, 0, sizeof(int), st));
+    }
+    C.skew_ldg = ldg;
+    C.skew_src[0] = a.G0;
+    C.skew_src[1] = a.G1;
+    return 0;
+}
+
+// what only the fast k = 3 kernel reads (scaled y, transposed tiles, the
+// a-independent {b, c} weights and their sums), built on the first k = 3 pass
+// of a locus: a c <= 2 run never loads the k = 3 code object
+static int ensure_k3(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hipStream_t st) {
+    if (C.d_g01) return 0;
+    const int nblk = ldg / 64;
+    const int ntile = nblk * (nblk + 1) / 2;
+    for (int s = 0; s < 2; s++) {
+        SWCHK(hipMalloc(&C.d_ys[s], sizeof(double) * ldg));
+        if (launch_scale_y(s ? a.y1 : a.y0, ldg, C.d_ys[s], st)) SWCHK(hipGetLastError());
+        SWCHK(hipMalloc(&C.d_skewT[s], sizeof(double) * (size_t)ntile * 4096));
+        if (launch_build_skewT(s ? a.G1 : a.G0, ldg, ldg - U, C.d_skewT[s], st)) SWCHK(hipGetLastError());
     }
     {  // the a-independent {b, c} weights of every k = 3 step
         Sweep3Args S3 = sweep3_args(C, a, U, ldg);
@@ -632,9 +656,6 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
         if (launch_bc3_colsum(ntile, C.d_mu01, C.d_bcn, C.d_bccm, C.d_bccn, st)) SWCHK(hipGetLastError());
         if (launch_interleave2(C.d_skewT[0], C.d_skewT[1], (size_t)ntile * 4096, C.d_g01, st)) SWCHK(hipGetLastError());
     }
-    C.skew_ldg = ldg;
-    C.skew_src[0] = a.G0;
-    C.skew_src[1] = a.G1;
     return 0;
 }
 
@@ -662,6 +683,7 @@ int sweep_prepare(SweepPlanCache& C, int k, int U, int ldg, int rank, int world,
                   bool exact, SweepPlan** out) {
     if (ensure_skew(C, a, ldg, U, st)) return -1;
     const int variant = (k == 3 && !exact) ? 1 : 0;
+    if (variant && ensure_k3(C, a, ldg, U, st)) return -1;
     auto key = std::make_tuple(k, U, rank, world, variant);
     auto it = C.plans.find(key);
     if (it == C.plans.end()) {

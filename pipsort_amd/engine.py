@@ -14,7 +14,9 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# PSX_ENGINE_LIB: an alternative build of the same library (A/B experiments)
+# PSX_ENGINE_LIB: an alternative build of the same library (A/B experiments).
+# It must export every symbol the ABI declares unless PSX_AB=1 (an older build
+# under comparison), so a stray variable cannot run the suite on a stale build.
 LIB_PATH = os.environ.get("PSX_ENGINE_LIB") or os.path.join(_HERE, "lib", "libpipsort_engine.so")
 PIPSORT_BIN = os.path.join(_HERE, "bin", "PIPSORT")
 
@@ -29,7 +31,7 @@ PSX_EEXCHANGE = -7
 
 # Every symbol declared in include/pipsort_engine.h and include/pipsort_model.h
 EXPORTED = [
-    "psx_abi_version", "psx_last_error", "psx_device_count", "psx_warmup", "psx_create", "psx_destroy",
+    "psx_abi_version", "psx_last_error", "psx_device_count", "psx_warmup", "psx_warmup_for", "psx_create", "psx_destroy",
     "psx_set_shard", "psx_run_exhaustive", "psx_run_configs", "psx_run_sss",
     "psx_eval_union_batch", "psx_reset", "psx_get_accum", "psx_partials_bytes",
     "psx_export_partials", "psx_merge_partials", "psx_get_timing", "psx_count_configs",
@@ -150,6 +152,7 @@ def load_library(path: str = LIB_PATH):
         "psx_last_error": (ctypes.c_char_p, []),
         "psx_device_count": (c_int, [P(c_int)]),
         "psx_warmup": (c_int, [c_int]),
+        "psx_warmup_for": (c_int, [c_int, c_i32, c_i32]),
         "psx_create": (c_int, [P(_Problem), c_int, P(vp)]),
         "psx_destroy": (None, [vp]),
         "psx_set_shard": (c_int, [vp, c_int, c_int]),
@@ -189,9 +192,12 @@ def load_library(path: str = LIB_PATH):
         "psx_multi_last_error": (ctypes.c_char_p, []),
         "psx_multi_destroy": (None, [vp]),
     }
+    ab = os.environ.get("PSX_AB") == "1"
     for name, (res, args) in sig.items():
-        if os.environ.get("PSX_ENGINE_LIB") and not hasattr(lib, name):
-            continue  # an older build under A/B comparison
+        if not hasattr(lib, name):
+            if ab:
+                continue  # an older build under A/B comparison
+            raise EngineError(PSX_ENODEV, f"{path} lacks {name}: a stale engine build (PSX_AB=1 to compare anyway)")
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -99,3 +99,65 @@ def test_cli_two_devices_byte_identical(gpu, tmp_path, src, args):
     if src == "example":
         for f in ("study0_post", "study1_post", "study0_set", "study1_set", "nocausal"):
             assert open(d2 / f"out_{f}.txt").read() == open(d2 / f"expected_{f}.txt").read(), f
+
+
+@pytest.mark.parametrize("c", [1, 4])
+def test_multi_count_off_the_fused_path(gpu, c):
+    """max_causal 1 / 4 are not fused-pass shapes: each shard runs the
+    synchronous sweep.  The folded count (timing) must still be every shard's,
+    i.e. equal the merged accumulators' count and one handle's."""
+    ld, z, _, _, u2l = synth.mixed_locus(40, 36, 28, seed=7)
+    seam = E.seam_from_arrays(ld, z, u2l, (5000, 9000), max_causal=c, sharing_param=0.5)
+    one = E.PostCal(seam)
+    one.run_exhaustive()
+    many = E.MultiPostCal(seam, [0, 0, 0])
+    many.run_exhaustive()
+    got = many.accum()
+    _same(got, one.accum())
+    assert got.n_configs == seam.count_configs()
+    assert many.timing()["configs"] == got.n_configs
+    one.close()
+    many.close()
+
+
+def test_multi_exact_rerun_matches_single_sync(gpu):
+    """The extreme-signal locus raises the EXACT flag inside the asynchronous
+    multi-shard pass, which then reruns the step synchronously on every shard:
+    the folded result equals one synchronous handle (to rounding: a shard
+    without a flagged set keeps the fast variant), the flag is
+    reported and the count is the whole locus's."""
+    from test_gpu_async import _extreme
+    mi = _extreme()
+    one = E.PostCal(mi)
+    one.run_exhaustive()
+    assert one.timing()["exact_rerun"] == 1
+    r = one.accum()
+    many = E.MultiPostCal(mi, [0, 0])
+    many.run_exhaustive()
+    g = many.accum()
+    t = many.timing()
+    assert t["exact_rerun"] == 1
+    assert t["configs"] == g.n_configs == r.n_configs
+    _same(g, r)  # shards without a flagged set keep the fast variant: equal to rounding
+    one.close()
+    many.close()
+
+
+def test_multi_distinct_devices(gpu):
+    """Shards on two distinct devices (peer copies of the partial image into
+    device 0's gather buffer over xGMI): equal to one handle.  Runs where the
+    box has two or more GPUs (the driver's node), skipped on a one-GPU box."""
+    if E.device_count() < 2:
+        pytest.skip("one device visible")
+    ld, z, _, _, u2l = synth.syn_v1(300)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    one = E.PostCal(seam)
+    one.run_exhaustive()
+    for devs in ([0, 1], [1, 0], list(range(min(E.device_count(), 8)))):
+        many = E.MultiPostCal(seam, devs)
+        many.run_exhaustive()
+        g = many.accum()
+        _same(g, one.accum())
+        assert many.timing()["configs"] == g.n_configs
+        many.close()
+    one.close()

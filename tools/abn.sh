@@ -4,6 +4,7 @@
 # entry = dir[@VAR=v,VAR2=w]; dir "-" = the in-tree library; each dir holds a
 # libpipsort_engine.so.  Results in gpurun_out/ab/abn.txt
 W=$1; R=$2; shift 2
+export PSX_AB=1  # variants may predate a symbol
 mkdir -p gpurun_out/ab
 for i in $(seq 1 $R); do
   for e in "$@"; do
