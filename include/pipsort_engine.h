@@ -107,7 +107,9 @@ void psx_destroy(psx_engine *e);
  * determinant is bit-identical to the reference elimination; when Sigma'_s is
  * positive definite, Sigma~_s = B_s^T B_s = Sigma'_s, y_s = B_s^T S'_s = z_s and
  * ||S'_s||^2 = z_s^T Sigma'_s^-1 z_s exactly, so no eigendecomposition is done
- * (otherwise the reference's eigen route runs on the host for that study). */
+ * (otherwise the reference's eigen route runs for that study, on the GPU too:
+ * rocSOLVER dsyevd, then B and S' from (Q, W, z); PSX_HOST_EIGEN=1 keeps a host
+ * restatement). */
 typedef struct {
     int32_t n_studies;              /* must be 2                                         */
     const int32_t *m;               /* [n_studies] M_s                                   */
@@ -231,9 +233,9 @@ int psx_shard_stats(const psx_problem *prob, int32_t k, int32_t rank, int32_t wo
 /* Host-side diagnostics (no kernel runs): the k = 3 fast sweep's work units of
  * shard `rank` of `world` for a union of n_union SNPs present in both studies,
  * in dispatch order, as int4 {a0, a1, K | j0 << 16, C | j1 << 16} (v space; a
- * diagonal tile's j counts half steps).  The a-chunk sizes follow the CU count
- * of the current HIP device (hipGetDeviceProperties; a fixed default without
- * one), so the decomposition depends on the device; every plan covers each
+ * diagonal tile's j counts half steps).  The a-chunk sizes are sized for
+ * MI355X's 256 CUs as a fixed constant (not a device query), so every rank of a
+ * sharded run, in any process, cuts the same unit list; every plan covers each
  * walk step once.  Writes at most `cap` units; returns the count (or a
  * negative error). */
 int psx_plan_units_k3(int32_t n_union, int32_t rank, int32_t world, int32_t *units, int32_t cap);

@@ -110,6 +110,8 @@ struct Sweep3Args {
 // most a per k = 3 unit (plan_units3c): the fast kernel stages the unit's
 // per-a scalars in LDS
 constexpr int kMaxChunkA3 = 4;
+// words per unit of the PSX_UNIT_TRACE dump (tools/unit_trace.py)
+constexpr int kTraceWords = 16;
 struct Level2Blocks;  // psx_sweep_dev.h
 int launch_sweep3(bool allpres, const Sweep3Args& A, int n_units, const int4* units, Acc5* rec, SetRec* srec,
                   int rec_stride, int* flag, const int* pos, hipStream_t st, const Level2Blocks* l2, hipEvent_t ev0 = nullptr,

@@ -326,18 +326,29 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // the wave slots per shard, at most 4 a per unit (measured on MI355X,
     // syn1000c3, tools/ca_sweep.sh: ca = 4 at world 1, 2 at worlds 2 and 4, 1 at
     // world 8).
-    static const double kTarget = [] {  // units per shard the a-chunk is sized for
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess) {
-            hipDeviceProp_t pr;
-            if (hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0)
-                cus = pr.multiProcessorCount;
-        }
-        return PSX_K3_ROUNDS * (4.0 * PSX_K3_WAVES * cus);
+    // Units per shard the a-chunk is sized for, from MI355X's 256 CUs as a fixed
+    // constant, not a device query: every rank (in any process, on any device)
+    // must cut the same unit list, or the union of the ranks' work bands would not
+    // cover every walk step exactly once.  (On a device with another CU count the
+    // plan stays exact, only its dispatch rounds differ.)
+    // PSX_K3_ROUNDS / PSX_K3_DIAG_DIV (environment, tuning experiments; the same
+    // for every rank of a job) override the dispatch rounds the a-chunk is sized
+    // for and divide the diagonal units' a-chunk (shorter units for the last
+    // dispatch rounds).
+    constexpr double kPlanCUs = 256.0;
+    static const double rounds = [] {
+        const char* e = std::getenv("PSX_K3_ROUNDS");
+        return e && std::atof(e) > 0 ? std::atof(e) : (double)PSX_K3_ROUNDS;
     }();
+    static const int diag_div = [] {
+        const char* e = std::getenv("PSX_K3_DIAG_DIV");
+        return e && std::atoi(e) > 0 ? std::atoi(e) : 1;
+    }();
+    const double kTarget = rounds * (4.0 * PSX_K3_WAVES * kPlanCUs);
     ca = (int)std::lround(total_a / (kTarget * world));
     ca = std::min(ca, kMaxChunkA3);
     ca = std::max(1, std::min(64, ca));
+    const int cad = std::max(1, ca / diag_div);
     // Every union triple x < y < z belongs to exactly one unit family, by which
     // of its members share a 64-block:
     //   all in different blocks      -> off-diagonal tile (K = blk y, C = blk z), a = x
@@ -352,8 +363,9 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
         if (64 * C + 64 <= pad) continue;
         for (int K = 0; K <= C; K++) {
             const int amax = (K < C) ? 64 * K : ldg;
-            for (int a0 = pad; a0 < amax; a0 += ca) {
-                const int a1 = std::min(a0 + ca, amax);
+            const int cu = K < C ? ca : cad;
+            for (int a0 = pad; a0 < amax; a0 += cu) {
+                const int a1 = std::min(a0 + cu, amax);
                 // unit cost in off-diagonal-a units: a fixed per-unit part and a
                 // per-a part; a diagonal tile's folded walk has half the steps.
                 // Fitted to unit durations (tools/unit_trace.py, MI355X):
@@ -790,12 +802,13 @@ int sweep_kernel(SweepPlanCache& C, SweepPlan& P, hipStream_t st, const SweepArg
             P.fused_flops = l2->flops;
         }
         static const char* trace_path = std::getenv("PSX_UNIT_TRACE");  // diagnostics: unit timeline dump
-        if (trace_path) SWCHK(hipMalloc(&S3.trace, sizeof(unsigned long long) * 8 * (size_t)P.n_units));
+        if (trace_path) SWCHK(hipMalloc(&S3.trace, sizeof(unsigned long long) * kTraceWords * (size_t)P.n_units));
+        if (trace_path) SWCHK(hipMemsetAsync(S3.trace, 0, sizeof(unsigned long long) * kTraceWords * (size_t)P.n_units, st));
         if (launch_sweep3(C.allpres, S3, P.n_units, P.d_units, rec, srec, P.rec_stride, flag, P.d_pos, st,
                           ride ? &b : nullptr, ev0, ev1))
             SWCHK(hipGetLastError());
         if (trace_path) {
-            std::vector<unsigned long long> h(8 * (size_t)P.n_units);
+            std::vector<unsigned long long> h(kTraceWords * (size_t)P.n_units);
             SWCHK(hipStreamSynchronize(st));
             SWCHK(hipMemcpy(h.data(), S3.trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
             SWCHK(hipFree(S3.trace));
@@ -855,21 +868,13 @@ void sweep_free(SweepPlanCache& C) {
         for (int i = 0; i < 3; i++) if (P.ev[i]) hipEventDestroy(P.ev[i]);
     }
     C.plans.clear();
+    free_k3(C);
     for (int s = 0; s < 2; s++) {
         hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
-        hipFree(C.d_skewT[s]); C.d_skewT[s] = nullptr;
         hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
         hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
-        hipFree(C.d_ys[s]); C.d_ys[s] = nullptr;
     }
     hipFree(C.d_tab); C.d_tab = nullptr;
-    hipFree(C.d_bcn); C.d_bcn = nullptr;
-    hipFree(C.d_bcsm); C.d_bcsm = nullptr;
-    hipFree(C.d_bcsn); C.d_bcsn = nullptr;
-    hipFree(C.d_bccm); C.d_bccm = nullptr;
-    hipFree(C.d_bccn); C.d_bccn = nullptr;
-    hipFree(C.d_g01); C.d_g01 = nullptr;
-    hipFree(C.d_mu01); C.d_mu01 = nullptr;
     hipFree(C.d_redo); C.d_redo = nullptr;
     if (C.own_flag) hipFree(C.d_flag);
     C.d_flag = nullptr;

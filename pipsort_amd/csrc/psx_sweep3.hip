@@ -99,6 +99,74 @@ __device__ __forceinline__ void wave_fold_set_dpp(SetRec& r) {
     r.npat = __ockl_wfred_add_f64(r.npat);
 }
 
+// Batched wave reductions: K independent values reduced together, so the K
+// dependency chains interleave (one chain of DPP steps is ~100 cycles of
+// latency; eight of them back to back were ~1.8 us of the a prologue at two
+// waves per SIMD, tools/unit_trace.py).  Within each row of 16 lanes four
+// row_shl steps leave the row's sum / max in its lane 0; the four row values
+// are then combined in a fixed order, (r0 + r1) + (r2 + r3), identical in
+// every lane.  Every lane must be active.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {  // out-of-row lanes read 0
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane_f64(double x, int lane) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), lane),
+                            __builtin_amdgcn_readlane(__double2loint(x), lane));
+}
+template <int K>
+__device__ __forceinline__ void wave_sum_k(double (&v)[K]) {
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x101>(v[k]);  // row_shl:1
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x102>(v[k]);  // row_shl:2
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x104>(v[k]);  // row_shl:4
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x108>(v[k]);  // row_shl:8
+#pragma unroll
+    for (int k = 0; k < K; k++)
+        v[k] = (readlane_f64(v[k], 0) + readlane_f64(v[k], 16)) + (readlane_f64(v[k], 32) + readlane_f64(v[k], 48));
+}
+template <int K>
+__device__ __forceinline__ void wave_max_k(int (&v)[K]) {
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] = max(v[k], __builtin_amdgcn_update_dpp(EMPTY, v[k], 0x101, 0xf, 0xf, false));
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] = max(v[k], __builtin_amdgcn_update_dpp(EMPTY, v[k], 0x102, 0xf, 0xf, false));
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] = max(v[k], __builtin_amdgcn_update_dpp(EMPTY, v[k], 0x104, 0xf, 0xf, false));
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] = max(v[k], __builtin_amdgcn_update_dpp(EMPTY, v[k], 0x108, 0xf, 0xf, false));
+#pragma unroll
+    for (int k = 0; k < K; k++)
+        v[k] = max(max(__builtin_amdgcn_readlane(v[k], 0), __builtin_amdgcn_readlane(v[k], 16)),
+                   max(__builtin_amdgcn_readlane(v[k], 32), __builtin_amdgcn_readlane(v[k], 48)));
+}
+
+// K (shift, sum) pairs at once, as wave_pair_dpp
+template <int K>
+__device__ __forceinline__ void wave_pair_k(int (&m)[K], double (&x)[K]) {
+    int M[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) M[k] = x[k] != 0.0 ? m[k] : EMPTY;
+    wave_max_k(M);
+#pragma unroll
+    for (int k = 0; k < K; k++) x[k] = x[k] != 0.0 ? ldexp(x[k], m[k] - M[k]) : 0.0;
+    wave_sum_k(x);
+#pragma unroll
+    for (int k = 0; k < K; k++) m[k] = x[k] != 0.0 ? M[k] : EMPTY;
+}
+
+// Order LDS accesses across the lanes of a ONE-wave workgroup: a wave's LDS
+// instructions execute in issue order, so program order suffices.  __syncthreads
+// would add s_barrier and, through its fence, a vmcnt(0) drain that waits for
+// every global load in flight (the prefetched tile rows and next-a Sigma~
+// entries): ~1 us per a prologue (tools/unit_trace.py, r04i).
+__device__ __forceinline__ void wave_lds_order() { asm volatile("" ::: "memory"); }
+
 // lane-local accumulator with a lazy shift: value = 2^m * s
 struct LAcc {
     int m;
@@ -791,7 +859,16 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         g1ab[s] = okb ? gb : 0.0;
         g1ac[s] = okc ? gc : 0.0;
     }
-    __syncthreads();  // exp2 table staged
+    // off-diagonal units' closed-form tile sums, issued with the other unit loads
+    double2 l_bcsm = make_double2(0.0, 0.0), l_bccm = make_double2(0.0, 0.0);
+    int2 l_bcsn = make_int2(0, 0), l_bccn = make_int2(0, 0);
+    if (SEP) {
+        l_bcsm = A.bcsm[(size_t)tile * 64 + t];
+        l_bcsn = A.bcsn[(size_t)tile * 64 + t];
+        l_bccm = A.bccm[(size_t)tile * 64 + t];
+        l_bccn = A.bccn[(size_t)tile * 64 + t];
+    }
+    wave_lds_order();  // exp2 table staged
     // the {b} weight of this lane's slot: unit-constant (the a prologues rescale it)
     int nBb[2];
     double muBb[2];
@@ -808,23 +885,26 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     // slot's one-study dot products over {b} and {a, b} (see below).
     constexpr bool sep = SEP;  // the caller checked !diag && j0 == 0 && j1 == 64
     if (sep) {
-        F.bcsm[t] = A.bcsm[(size_t)tile * 64 + t];
-        F.bcsn[t] = A.bcsn[(size_t)tile * 64 + t];
-        F.bccm[t] = A.bccm[(size_t)tile * 64 + t];
-        F.bccn[t] = A.bccn[(size_t)tile * 64 + t];
+        F.bcsm[t] = l_bcsm;
+        F.bcsn[t] = l_bcsn;
+        F.bccm[t] = l_bccm;
+        F.bccn[t] = l_bccn;
+        int m2[2] = {nBb[0], nBb[1]};
+        double x2[2] = {muBb[0], muBb[1]};
+        wave_pair_k(m2, x2);
+        if (t == 0) {
 #pragma unroll
-        for (int s = 0; s < 2; s++) {
-            int m = nBb[s];
-            double x = muBb[s];
-            wave_pair_dpp(m, x);
-            if (t == 0) {
-                F.pbS[s] = x;
-                F.pbM[s] = m;
+            for (int s = 0; s < 2; s++) {
+                F.pbS[s] = x2[s];
+                F.pbM[s] = m2[s];
             }
         }
     }
 
-    unsigned long long t_ph[4] = {0ull, 0ull, 0ull, 0ull};  // diagnostics: phases of the first a
+    // diagnostics (PSX_UNIT_TRACE): phases of the first a (t_ph), and finer stamps
+    // inside its prologue / fold (t_fn: loads + barrier, per-study terms, slot
+    // shift, closed forms; fold arithmetic)
+    unsigned long long t_ph[4] = {0ull, 0ull, 0ull, 0ull}, t_fn[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
     if (A.trace) t_ph[0] = wall_clock64();
     for (int ai = 0; ai < a1 - a0; ai++) {
         const int va = a0 + ai, ua = va - pad;
@@ -842,7 +922,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             nGab[s] = row[ib];
             nGac[s] = row[ic];
         }
-        __syncthreads();  // previous a's (a, b) terms and slots fully consumed
+        wave_lds_order();  // previous a's (a, b) terms and slots fully consumed
+        if (A.trace && ai == 0) t_fn[0] = wall_clock64();
         const unsigned pa = F.aP[ai];
         const double2 aAd = F.aAd[ai], aY = F.aY[ai];
         double pG[2], pI[2], pIW[2], pH[2], pR[2], pMu[2], pMuB[2];
@@ -907,6 +988,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         F.abMuB[t] = make_double2(pMuB[0], pMuB[1]);
         F.abN[t] = make_int2(pN[0], pN[1]);
         const double wac = wc * memb_weight(pa);
+        if (A.trace && ai == 0) t_fn[1] = wall_clock64();
         // this a's reference G: the a accumulator sits at it; c / noCausal / the b
         // slots move their shift up to it (values scale down exactly) once per a
         const int G = R[0] + R[1];
@@ -956,9 +1038,21 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         // the walk's split constants as opaque registers (split3r)
         double k256 = 256.0, kc3 = kC3, kc2 = kC2;
         asm volatile("" : "+s"(k256), "+s"(kc3), "+v"(kc2));
+        // this a's wave maxima in one batch: G (the slot shift) and, for the closed
+        // forms of off-diagonal units, R_s and the slots' {a, b} exponents
+        int mx[5] = {G, R[0], R[1], pMu[0] != 0.0 ? pN[0] : EMPTY, pMu[1] != 0.0 ? pN[1] : EMPTY};
+        if (sep) {
+            wave_max_k(mx);
+        } else {
+            int g1[1] = {G};
+            wave_max_k(g1);
+            mx[0] = g1[0];
+        }
+        double abS[2] = {0.0, 0.0};  // sum over the slots of the {a, b} weights, at 2^abM
+        int abM[2] = {EMPTY, EMPTY};
         double fS;  // a lane's contribution to the b slots is scaled by 2^(G - sM)
         {
-            const int Gm = __ockl_wfred_max_i32(G);  // DPP wave reduction, no LDS round trips
+            const int Gm = mx[0];
             const int Ms = max(sMt, Gm), d = sMt - Ms;
             sW0[t] = ldexp(sW0[t], d);
             sW1[t] = ldexp(sW1[t], d);
@@ -968,6 +1062,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             sMt = Ms;
             fS = ldexp(1.0, G - Ms);
         }
+        if (A.trace && ai == 0) t_fn[2] = wall_clock64();
         if (sep) {
             // b in one study, subsets {} and {a} of {a, c} with b: over the walk
             // slot b receives from every lane c once
@@ -975,17 +1070,29 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             // A in {{}, {a}}, i.e. E_0[A + b] 2^(-sM[b]) times a wave sum over c
             // (likewise study 1); the walk then only takes their {b, c} and {a, b, c}
             // terms.  Lane t adds slot t's share.
-            double QW[2][2];
-            int Qm[2];
+            // (likewise the plain one-study sums of notSharedLL, uL: uL_s[0] = uW_s[0])
+            // (and the walk sum of the {a, b} weights over the slots, V_s[1]: one batch)
+            const int Qm[2] = {mx[1], mx[2]};
+            double ws[8];
 #pragma unroll
             for (int s = 0; s < 2; s++) {
-                Qm[s] = __ockl_wfred_max_i32(R[s]);
+                ws[2 * s] = ldexp(uW[s][0], R[s] - Qm[s]);
+                ws[2 * s + 1] = ldexp(uW[s][1], R[s] - Qm[s]);
+                ws[4 + s] = ldexp(uL[s][1], R[s] - Qm[s]);
+                ws[6 + s] = pMu[s] != 0.0 ? ldexp(pMu[s], pN[s] - mx[3 + s]) : 0.0;
+            }
+            wave_sum_k(ws);
+            const double QW[2][2] = {{ws[0], ws[1]}, {ws[2], ws[3]}}, QL[2] = {ws[4], ws[5]};
 #pragma unroll
-                for (int i = 0; i < 2; i++) QW[s][i] = __ockl_wfred_add_f64(ldexp(uW[s][i], R[s] - Qm[s]));
+            for (int s = 0; s < 2; s++) {
+                abS[s] = ws[6 + s];
+                abM[s] = ws[6 + s] != 0.0 ? mx[3 + s] : EMPTY;
             }
             // E_s[A + b] of this lane's slot: {b} = pMuB 2^pN, {a, b} = pMu 2^pN
-            sW0[t] += fma(pMuB[0], QW[1][0], pMu[0] * QW[1][1]) * ldexp(1.0, pN[0] + Qm[1] - sMt);
-            sW1[t] += fma(pMuB[1], QW[0][0], pMu[1] * QW[0][1]) * ldexp(1.0, pN[1] + Qm[0] - sMt);
+            const double e0 = ldexp(1.0, pN[0] + Qm[1] - sMt), e1 = ldexp(1.0, pN[1] + Qm[0] - sMt);
+            sW0[t] += fma(pMuB[0], QW[1][0], pMu[0] * QW[1][1]) * e0;
+            sW1[t] += fma(pMuB[1], QW[0][0], pMu[1] * QW[0][1]) * e1;
+            sNs[t] += fma(fma(pMuB[0], QW[1][0], pMu[0] * QL[1]), e0, fma(pMuB[1], QW[0][0], pMu[1] * QL[0]) * e1);
             // b in both studies, a and c each in one (different) study, b's partner
             // subsets {a, b} in one study and {b, c} in the other: per step
             //   v_0[{b,c}] v_1[{a,b}] 2^(G - sM[b]) = E_0[b, c] E_1[a, b] 2^(-sM[b])
@@ -998,13 +1105,14 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             sW2[t] += z0;
             sSl[t] += z0;
         }
+        if (A.trace && ai == 0) t_fn[3] = wall_clock64();
         // the slot scale rides in the prior-weighted vectors (only the b-slot dot
         // products use them from here on; a power of two, so exact above underflow)
 #pragma unroll
         for (int s = 0; s < 2; s++)
 #pragma unroll
             for (int i = 0; i < 4; i++) uW[s][i] *= fS;
-        __syncthreads();  // (a, b) terms and slot shifts visible
+        wave_lds_order();  // (a, b) terms and slot shifts visible
         if (nxt) {
 #pragma unroll
             for (int s = 0; s < 2; s++) {
@@ -1087,7 +1195,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             // ---- member b (this step's slot): b in study 0 only / study 1 only ----
             const double WB0 = sepc ? dot2(v[0], uW[1], 0.0) : dot4(v[0], uW[1], 0.0);
             const double WB1 = sepc ? dot2(v[1], uW[0], 0.0) : dot4(v[1], uW[0], 0.0);
-            const double NB = dot4(v[0], uL[1], dot4(v[1], uL[0], 0.0));
+            const double NB = sepc ? dot2(v[0], uL[1], dot2(v[1], uL[0], 0.0)) : dot4(v[0], uL[1], dot4(v[1], uL[0], 0.0));
             // ---- b in both studies: the 9 assignments of (a, c); their sums for a and c ----
 #pragma unroll
             for (int xa = 0; xa < 3; xa++)
@@ -1110,7 +1218,9 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 V0[i] += v[0][i];
                 V1[i] += v[1][i];
             }
-            tiny |= NB < kTinyNs;
+            // (SEP: NB is a part of the set's notSharedLL; the slot's total is checked
+            // after the unit instead)
+            if (!sepc) tiny |= NB < kTinyNs;
             // ---- b slot (LDS, x fS: WB0 / WB1 carry it from uW) ----
             // LDS float adds: no read round trip; one lane per slot per step, and a
             // wave's LDS instructions execute in issue order (deterministic)
@@ -1214,6 +1324,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             }
             __builtin_amdgcn_wave_barrier();
         }
+        if (A.trace && ai == 0) t_ph[2] = wall_clock64();
         nact += je - j0;
         if (ALLPRES) npat += 27.0 * nact;
         if (sep) {
@@ -1222,16 +1333,11 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             // (wave sum of the slot owners' LDS terms) and the tile row's {b, c} sum
             const double2 bsm = F.bcsm[t];
             const int2 bsn = F.bcsn[t];
-            const double2 muab = F.abMu[t];
-            const int2 nab = F.abN[t];
 #pragma unroll
             for (int s = 0; s < 2; s++) {
-                int m = s ? nab.y : nab.x;
-                double x = s ? muab.y : muab.x;
-                wave_pair_dpp(m, x);
                 double* Vs = s ? V1 : V0;
                 Vs[0] = ldexp(F.pbS[s], F.pbM[s] - R[s]);
-                Vs[1] = ldexp(x, m - R[s]);
+                Vs[1] = ldexp(abS[s], abM[s] - R[s]);  // (a prologue's batch)
                 Vs[2] = ldexp(s ? bsm.y : bsm.x, (s ? bsn.y : bsn.x) - R[s]);
             }
         }
@@ -1270,31 +1376,39 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         nc1 = fma(V0[3], f1, nc1);
         if (__builtin_amdgcn_ballot_w64(tiny))
             if (tiny) atomicOr(flag, 1);
-        if (A.trace && ai == 0) t_ph[2] = wall_clock64();
+        if (A.trace && ai == 0) t_fn[4] = wall_clock64();
         {
             // the a record: every lane's five sums share its shift G, so the wave
             // folds them at the largest G among lanes with content (a lane's
             // notSharedLL is >= 2^-900 of its own G, so nothing that matters is
             // lost) with DPP wave sums
             const bool has = (WA[0] + WA[1] + WA[2] + LA2 + NA) != 0.0;
-            const int Gw = __ockl_wfred_max_i32(has ? G : EMPTY);
+            int gw[1] = {has ? G : EMPTY};
+            wave_max_k(gw);
+            const int Gw = gw[0];
             const int dg = has ? G - Gw : -2000;
-            const double W0 = __ockl_wfred_add_f64(ldexp(WA[0], dg));
-            const double W1 = __ockl_wfred_add_f64(ldexp(WA[1], dg));
-            const double W2 = __ockl_wfred_add_f64(ldexp(WA[2], dg));
-            const double Sl = __ockl_wfred_add_f64(ldexp(LA2, dg));
-            const double Ns = __ockl_wfred_add_f64(ldexp(NA, dg));
+            double r5[5] = {ldexp(WA[0], dg), ldexp(WA[1], dg), ldexp(WA[2], dg), ldexp(LA2, dg), ldexp(NA, dg)};
+            wave_sum_k(r5);
+            const double W0 = r5[0], W1 = r5[1], W2 = r5[2], Sl = r5[3], Ns = r5[4];
             const int qa = F.aPos[ai];
             if (t == 0 && qa >= 0) store_rec(rec + qa, wrec(Gw, W0, W1, W2, Sl, Ns, rho, A.Ck, A.pit0));
         }
         if (A.trace && ai == 0) t_ph[3] = wall_clock64();
     }
-    __syncthreads();
+    wave_lds_order();
     {
         // a diagonal tile's lane t and b slot t are one SNP: one record (the plan
         // keys no b records there), folded here instead of in the merge
         Acc5 rc = wrec(mC, cW0, cW1, cW2, cSl, cNs, rho, A.Ck, A.pit0);
         const Acc5 rb = wrec(sMt, sW0[t], sW1[t], sW2[t], sSl[t], sNs[t], rho, A.Ck, A.pit0);
+        if (sep) {
+            // the b slot's notSharedLL total (closed-form and walk parts) against the
+            // fast path's floor: at or above 2^-900 of the slot shift, every term lost
+            // to underflow (< 2^-1074 each) is below 2^-174 of it; below, exact rerun
+            const bool low = okb && sNs[t] < kTinyNs;
+            if (__builtin_amdgcn_ballot_w64(low))
+                if (low) atomicOr(flag, 1);
+        }
         if (diag) fold_acc(rc, rb);
         if (posC >= 0) store_rec(rec + posC, rc);
         if (!diag && posB >= 0) store_rec(rec + posB, rb);
@@ -1309,20 +1423,42 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     sr.pad = 0;
     sr.score = 1e300;
     sr.npat = npat;
-    wave_fold_set_dpp(sr);
+    {
+        // the unit's set record across the wave: three (shift, sum) pairs and the
+        // pattern count in one batch (score: 1e300 in every lane)
+        int m3[3] = {sr.m, sr.m0, sr.m1};
+        double x3[3] = {sr.tot, sr.nc0, sr.nc1};
+        int M3[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) M3[k] = x3[k] != 0.0 ? m3[k] : EMPTY;
+        wave_max_k(M3);
+        double x4[4];
+#pragma unroll
+        for (int k = 0; k < 3; k++) x4[k] = x3[k] != 0.0 ? ldexp(x3[k], m3[k] - M3[k]) : 0.0;
+        x4[3] = sr.npat;
+        wave_sum_k(x4);
+        sr.tot = x4[0];
+        sr.m = x4[0] != 0.0 ? M3[0] : EMPTY;
+        sr.nc0 = x4[1];
+        sr.m0 = x4[1] != 0.0 ? M3[1] : EMPTY;
+        sr.nc1 = x4[2];
+        sr.m1 = x4[2] != 0.0 ? M3[2] : EMPTY;
+        sr.npat = x4[3];
+    }
     if (t == 0) store_rec(srec + unit, sr);
     redo = __builtin_amdgcn_ballot_w64(dmax > kMaxRefGap) != 0;
     if (A.trace && t == 0) {
         unsigned hw, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        unsigned long long* tr = A.trace + 8 * (size_t)unit;
+        unsigned long long* tr = A.trace + kTraceWords * (size_t)unit;
         tr[0] = t_start;
         tr[1] = wall_clock64();
         tr[2] = hw | ((unsigned long long)xcc << 32);
         tr[3] = (unsigned long long)unit | ((unsigned long long)diag << 32) | ((unsigned long long)(a1 - a0) << 33) |
                 ((unsigned long long)redo << 40);
         for (int i = 0; i < 4; i++) tr[4 + i] = t_ph[i];
+        for (int i = 0; i < 6; i++) tr[8 + i] = t_fn[i];
     }
 }
 

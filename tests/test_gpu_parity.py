@@ -591,22 +591,32 @@ def _member_pins(pc_accum, seam, snps, rtol=1e-10):
         np.testing.assert_allclose(got, want, rtol=rtol, atol=0, err_msg=f"SNP {u}")
 
 
-# union SNPs pinned at the headline locus (U = 1000, padded to 1024: the sweep's
-# v = u + 24, so its 64-blocks start at u = 40, 104, ...): both ends; the
-# 64-block edges in u (63 | 64, 127 | 128, 191 | 192) and in the sweep's v
-# space (39 | 40, 103 | 104, 231 | 232); the planted shared causal 250 and the
-# study-0 causal 750 with their neighbours; members of one diagonal tile
-# (499, 500, 501 share v-block 8); the last pair 998, 999
-HEADLINE_PINS = [0, 39, 40, 63, 64, 103, 104, 127, 128, 191, 192, 231, 232, 249, 250, 251, 499, 500, 501, 749, 750,
-                 751, 998, 999]
+def _full_vector(acc, u2l, m0, M):
+    """Every union SNP's five accumulators (post of both studies, sharedPips,
+    sharedLL, notSharedLL: postcal.cpp:981-1030) against the committed golden
+    sums of the oracle (tests/golden/fullsize/make_member_sums.py: exact
+    long-double log-sum-exp over every union set containing the SNP), rtol 1e-10
+    on the log values.  No oracle call on the GPU box."""
+    path = os.path.join(loci.GOLDEN, "fullsize", f"syn{M}c3_member_sums.txt")
+    rows = np.loadtxt(path, comments="#")
+    assert rows.shape[0] == u2l.shape[1], "golden file does not cover every union SNP"
+    u = rows[:, 0].astype(int)
+    assert np.array_equal(u, np.arange(u2l.shape[1]))
+    l0, l1 = u2l[0, u], u2l[1, u]
+    got = np.stack([np.where(l0 >= 0, acc.post[np.maximum(l0, 0)], 0.0),
+                    np.where(l1 >= 0, acc.post[m0 + np.maximum(l1, 0)], 0.0),
+                    acc.shared[u], acc.shared_ll[u], acc.notshared_ll[u]], axis=1)
+    want = rows[:, 1:6]
+    bad = ~np.isclose(got, want, rtol=1e-10, atol=0)
+    assert not bad.any(), (f"{int(bad.sum())} of {bad.size} values off; first at SNP "
+                           f"{int(u[np.argwhere(bad)[0][0]])}: {got[bad][:3]} vs {want[bad][:3]}")
 
 
-def test_headline_locus_value_pins(gpu):
+def test_headline_full_vector(gpu):
     """BASELINE configs[3], the bench locus (SYN-v1 M = 1000, c = 3, 4.49e9
-    configurations) through the GPU Model setup: post (both studies), shared,
-    sharedLL and notSharedLL of 24 SNPs (HEADLINE_PINS) each against an exact
-    sum over its 13.5M assignments by the oracle (oracle.member_sums on every
-    host core of the affinity set)."""
+    configurations) through the GPU Model setup: all 1,000 union SNPs' five
+    accumulators against the golden per-SNP oracle sums (each an exact sum over
+    its 13.5M assignments)."""
     M = 1000
     ld, z, _, _, u2l = synth.syn_v1(M)
     mi = E.model_inputs(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
@@ -614,15 +624,14 @@ def test_headline_locus_value_pins(gpu):
     pc.run_exhaustive()
     a = pc.accum()
     assert a.n_configs == 4_491_007_501
-    seam = O.cholesky_seam(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
-    _member_pins(a, seam, HEADLINE_PINS)
+    _full_vector(a, np.asarray(u2l), M, M)
     pc.close()
 
 
-def test_syn500c3_full_size(gpu):
+def test_syn500c3_full_vector(gpu):
     """BASELINE configs[2] at full size (SYN-v1 M = 500, c = 3, 560,253,751
-    configurations): exact count, four SNPs pinned against the oracle's
-    per-SNP sums, and a world-2 shard fold equal to the single pass."""
+    configurations): exact count, all 500 union SNPs against the golden oracle
+    sums, and a world-2 shard fold equal to the single pass."""
     import torch
     M = 500
     ld, z, _, _, u2l = synth.syn_v1(M)
@@ -631,8 +640,7 @@ def test_syn500c3_full_size(gpu):
     pc.run_exhaustive()
     a = pc.accum()
     assert a.n_configs == 560_253_751 == mi.count_configs()
-    seam = O.cholesky_seam(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
-    _member_pins(a, seam, [125, 375, 0, 499])
+    _full_vector(a, np.asarray(u2l), M, M)
     nb = pc.partials_bytes()
     buf = torch.empty(2 * nb, dtype=torch.uint8, device="cuda")
     for r in range(2):

@@ -139,3 +139,17 @@ def test_all_configs_rows_through_oracle_equal_exhaustive():
     assert a["n_configs"] == b["n_configs"] == rows.shape[0]
     for k in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
         np.testing.assert_allclose(b[k], a[k], rtol=1e-12, atol=0, err_msg=k)
+
+
+@pytest.mark.parametrize("u", [0, 125, 499])
+def test_fullsize_golden_sums_reproduce(u):
+    """The committed full-size golden sums (tests/golden/fullsize/, made by
+    make_member_sums.py) are the oracle's: recompute three SNPs of SYN-v1 M = 500."""
+    import numpy as np
+    from pipsort_amd import synth
+    rows = np.loadtxt(os.path.join(loci.GOLDEN, "fullsize", "syn500c3_member_sums.txt"), comments="#")
+    ld, z, _, _, u2l = synth.syn_v1(500)
+    seam = O.cholesky_seam(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    r = O.member_sums(seam, u)
+    got = [r["post0"], r["post1"], r["shared"], r["shared_ll"], r["notshared_ll"], r["n_patterns"]]
+    np.testing.assert_allclose(got, rows[u, 1:7], rtol=1e-14, atol=0)

@@ -26,7 +26,7 @@ pc = E.PostCal(bench.build_inputs(a.workload), device=0)
 pc.set_shard(a.rank, a.world)
 for _ in range(3):
     pc.run_exhaustive()
-tr = np.fromfile(path, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+tr = np.fromfile(path, dtype=np.uint64).reshape(-1, 16).astype(np.int64)
 st, en = tr[:, 0], tr[:, 1]
 t0 = st.min()
 span = (en.max() - t0) / 100.0
@@ -58,11 +58,17 @@ pro = (ph[:, 0] - st) / 100.0
 apro = (ph[:, 1] - ph[:, 0]) / 100.0
 steps = (ph[:, 2] - ph[:, 1]) / 100.0
 fold = (ph[:, 3] - ph[:, 2]) / 100.0
+fn = tr[:, 8:14]
 for dflag in (0, 1):
     m = diag == dflag
-    print(f"{'diagonal' if dflag else 'off-diag'} first-a phases (us, mean): unit prologue {pro[m].mean():.1f}, "
-          f"a prologue {apro[m].mean():.1f}, steps {steps[m].mean():.1f}, a fold+record {fold[m].mean():.1f}, "
-          f"rest {((en - ph[:, 3]) / 100.0)[m].mean():.1f}")
+    print(f"{'diagonal' if dflag else 'off-diag'} first-a phases (us, mean): unit prologue {pro[m].mean():.2f}, "
+          f"a prologue {apro[m].mean():.2f}, steps {steps[m].mean():.1f}, a fold+record {fold[m].mean():.2f}, "
+          f"rest {((en - ph[:, 3]) / 100.0)[m].mean():.2f}")
+    if fn[m, 0].any():
+        d = lambda x, y: float(((x - y) / 100.0)[m].mean())
+        print(f"   a prologue split: loads+barrier {d(fn[:, 0], ph[:, 0]):.2f}, per-study terms {d(fn[:, 1], fn[:, 0]):.2f}, "
+              f"vectors+shifts+slot max {d(fn[:, 2], fn[:, 1]):.2f}, closed forms {d(fn[:, 3], fn[:, 2]):.2f}, "
+              f"scale+barrier {d(ph[:, 1], fn[:, 3]):.2f}; fold {d(fn[:, 4], ph[:, 2]):.2f}, record {d(ph[:, 3], fn[:, 4]):.2f}")
 bu = np.array([d.mean() for d in np.array_split(dur[np.argsort(uid)], 10)])
 print("mean duration by unit-index decile:", np.round(bu, 1).tolist())
 
