@@ -494,10 +494,12 @@ def example_wall():
         same = all(open(os.path.join(d, f"out_{f}.txt")).read() ==
                    open(os.path.join(src, f"expected_{f}.txt")).read()
                    for f in ("study0_post", "study1_post", "study0_set", "study1_set", "nocausal"))
-    phases = None
+    phases, warm = None, None
     for line in r.stderr.splitlines():
         if line.startswith("psx-timing "):
             phases = json.loads(line[len("psx-timing "):])
+        elif line.startswith("psx-warm "):  # psx_warmup_for's split of context_and_code_load
+            warm = json.loads(line[len("psx-warm "):])
     if phases:
         # process exit (teardown of the HIP runtime, unmapping) until the parent sees it
         phases["exit_ms"] = t1 / 1e6 - phases.pop("end_epoch_ms")
@@ -507,6 +509,8 @@ def example_wall():
                           "main thread still waits for them after parsing; sum_ms adds the main-thread phases")
         # the concurrent warm-up phases are not on the main thread's path
         phases["sum_ms"] -= phases["hip_runtime_ms"] + phases["context_and_code_load_ms"]
+        if warm:
+            phases["context_and_code_load_split"] = warm
     return (wall if r.returncode == 0 else None), same, phases
 
 

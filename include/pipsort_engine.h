@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define PSX_ABI_VERSION 1
+#define PSX_ABI_VERSION 2
 
 #define PSX_OK 0
 #define PSX_EINVAL (-1)    /* bad argument / unsupported problem shape        */
@@ -76,6 +76,8 @@ typedef struct {
     double flops;           /* FP64 operation estimate of the dominant kernel              */
     int32_t exact_rerun;    /* 1 if the sweep was redone with the exact notSharedLL variant */
     int32_t robust_units;   /* k = 3 units redone by the robust variant (cumulative since create) */
+    double span_ms;         /* asynchronous passes: first sweep's start to the last one's end,
+                               per pass (consecutive sweeps may overlap: kernel_ms double-counts) */
 } psx_timing;
 
 int32_t psx_abi_version(void);

@@ -673,6 +673,15 @@ struct psx_engine {
     // pipelined asynchronous passes: sweeps on a compute stream, merges (and the
     // caller's exchange) on `stream`; record buffers alternate by pass parity
     hipStream_t cstream = nullptr;
+    // overlapped passes (PSX_OVERLAP = n reserved CUs): two compute streams
+    // masked off n CUs, alternating, so pass i + 1's units fill pass i's drain;
+    // the merges and the caller's exchange keep the reserved CUs
+    hipStream_t cstream2 = nullptr;
+    int ovl = -1;                     // reserved CUs (0: no overlap), read once
+    int a_alt = 0;
+    int a_first = -1;                 // ring slot of the first pass since the last sync (start: span0)
+    hipEvent_t span0 = nullptr;       // start of that pass
+    double a_span = 0;                // span0 to the last consumed pass's end (ms)
 
     static constexpr int kBufs = psx::kRecBufs;  // record buffer sets: sweep i waits for merge i - kBufs
     hipEvent_t mdone[kBufs] = {};
@@ -711,9 +720,11 @@ psx_engine::~psx_engine() {
     }
     for (int i = 0; i < 4; i++) hipEventDestroy(ev[i]);
     for (int i = 0; i < 2 * kRing; i++) if (aev[i]) hipEventDestroy(aev[i]);
+    if (span0) hipEventDestroy(span0);
     for (int i = 0; i < kBufs; i++)
         if (mdone[i]) hipEventDestroy(mdone[i]);
     if (cstream) { hipStreamSynchronize(cstream); hipStreamDestroy(cstream); }
+    if (cstream2) { hipStreamSynchronize(cstream2); hipStreamDestroy(cstream2); }
 
     if (own_stream) hipStreamDestroy(own_stream);
 }
@@ -1114,9 +1125,12 @@ bool fused_eligible(const psx_engine* e) {
 int consume_async(psx_engine* e) {
     const int r = ((e->a_head - e->a_pending) % psx_engine::kRing + psx_engine::kRing) % psx_engine::kRing;
     HIPCHK(hipEventSynchronize(e->aev[2 * r + 1]));
-    float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, e->aev[2 * r], e->aev[2 * r + 1]));
+    float ms = 0, sp = 0;
+    HIPCHK(hipEventElapsedTime(&ms, r == e->a_first ? e->span0 : e->aev[2 * r], e->aev[2 * r + 1]));
+    HIPCHK(hipEventElapsedTime(&sp, e->span0, e->aev[2 * r + 1]));
+    if (r == e->a_first) e->a_first = -2;  // consumed: later passes of this span use their own starts
     e->a_kms += ms;
+    e->a_span = sp;
     e->a_count++;
     e->a_pending--;
     return 0;
@@ -1144,19 +1158,48 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     int par = 0;
     if (async) {
         if (!e->cstream) {
-            // the compute stream sits below the engine / exchange stream in
-            // priority, so merges and the exchange get wave slots first.  (Two
-            // alternating compute streams on distinct queues, overlapping one
-            // sweep's tail with the next, measured +3 % at world 1 and 0 at
-            // world 8, but make every launch's duration span its neighbour's:
-            // not used.)
-            int lo_pr = 0, hi_pr = 0;
-            HIPCHK(hipDeviceGetStreamPriorityRange(&lo_pr, &hi_pr));
-            HIPCHK(hipStreamCreateWithPriority(&e->cstream, hipStreamNonBlocking, (lo_pr + hi_pr) / 2));
+            if (e->ovl < 0) {
+                const char* o = getenv("PSX_OVERLAP");
+                e->ovl = o ? std::max(0, atoi(o)) : 0;
+            }
+            int ncu = 0;
+            HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->dev));
+            if (e->ovl > 0 && e->ovl < ncu) {
+                // Two compute streams on their own queues, masked off e->ovl CUs
+                // (bits ncu - 1 - k * stride, PSX_RESERVE_STRIDE, default 1):
+                // consecutive sweeps overlap, each one's last dispatch round filled
+                // by the next one's units, and the merge / exchange kernels (often
+                // multi-wave blocks, which a CU full of one-wave sweep blocks never
+                // frees room for) run on the reserved CUs.
+                const char* st = getenv("PSX_RESERVE_STRIDE");
+                const int stride = st ? std::max(1, atoi(st)) : 1;
+                std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+                for (int c = 0; c < ncu; c++) mask[c / 32] |= 1u << (c % 32);
+                for (int k = 0; k < e->ovl; k++) {
+                    const int c = ncu - 1 - k * stride;
+                    if (c >= 0) mask[c / 32] &= ~(1u << (c % 32));
+                }
+                HIPCHK(hipExtStreamCreateWithCUMask(&e->cstream, (uint32_t)mask.size(), mask.data()));
+                HIPCHK(hipExtStreamCreateWithCUMask(&e->cstream2, (uint32_t)mask.size(), mask.data()));
+            } else {
+                // the compute stream sits below the engine / exchange stream in
+                // priority, so merges and the exchange get wave slots first.  (Two
+                // alternating compute streams on distinct queues, overlapping one
+                // sweep's tail with the next, measured +3 % at world 1 and 0 at
+                // world 8 without reserved CUs: the exchange's multi-wave blocks
+                // starve; PSX_OVERLAP reserves CUs for them.)
+                int lo_pr = 0, hi_pr = 0;
+                HIPCHK(hipDeviceGetStreamPriorityRange(&lo_pr, &hi_pr));
+                HIPCHK(hipStreamCreateWithPriority(&e->cstream, hipStreamNonBlocking, (lo_pr + hi_pr) / 2));
+            }
             for (int i = 0; i < psx_engine::kBufs; i++)
                 HIPCHK(hipEventCreateWithFlags(&e->mdone[i], hipEventDisableTiming));
         }
         S = e->cstream;
+        if (e->cstream2) {
+            S = e->a_alt ? e->cstream2 : e->cstream;
+            e->a_alt ^= 1;
+        }
         par = e->a_par = (e->a_par + 1) % psx_engine::kBufs;
         // the merge that last read this buffer set (pass i - kBufs) must be done.
         // Host-side flow control: blocking here only when the device is more than
@@ -1179,6 +1222,11 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
         for (int i = 0; i < 2; i++)
             if (!e->aev[2 * slot + i]) HIPCHK(hipEventCreate(&e->aev[2 * slot + i]));
         k0 = e->aev[2 * slot];
+        if (e->a_first == -1) {  // the first pass since the last sync starts the span
+            if (!e->span0) HIPCHK(hipEventCreate(&e->span0));
+            e->a_first = slot;
+            k0 = e->span0;
+        }
         k1 = e->aev[2 * slot + 1];
     } else {
         HIPCHK(hipEventRecord(e->ev[0], S));
@@ -1651,6 +1699,7 @@ int psx_sync(psx_engine* e, int32_t* exact_needed) {
         return fail(PSX_EHIP, std::string("sweep plan: ") + psx::sweep_error());
     const psx::SweepPlan* top = P3 ? P3 : P2;
     e->timing.kernel_ms = e->a_kms;
+    e->timing.span_ms = e->a_count ? e->a_span / e->a_count : 0.0;
     e->timing.kernel_launches = e->a_count;
     e->timing.sweep_ms = e->a_count ? e->a_kms / e->a_count : 0.0;
     e->timing.union_sets = top->union_sets;
@@ -1663,6 +1712,8 @@ int psx_sync(psx_engine* e, int32_t* exact_needed) {
     e->timing.configs = (uint64_t)(st.npat + 0.5);
     e->a_kms = 0;
     e->a_count = 0;
+    e->a_first = -1;
+    e->a_span = 0;
     return 0;
 }
 

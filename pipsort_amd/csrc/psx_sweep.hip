@@ -312,6 +312,8 @@ int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* 
 // the padded space v = u + pad.  Lane t owns c = 64C + t; b runs over block K;
 // a over [a0, a1) with a < b.  Exact per-shard set / configuration / byte counts
 // in O(64 * 9) per unit from per-class prefix counts over v.
+constexpr double kTailFrac = 0.0;  // share of a shard's work cut into single-a units at the end (PSX_K3_TAIL)
+
 int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_host, std::vector<PlanUnit>& mine,
                  int& ca, double& sets, double& configs, double& bytes) {
     const int nblk = ldg / 64, pad = ldg - U;
@@ -432,6 +434,35 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // timeline (tools/unit_trace.py) showed a ~60 us tail of full-length units
     // on a world-8 shard in tile order.  Stable: tile order kept within a class.
     std::stable_sort(mine.begin(), mine.end(), [](const PlanUnit& x, const PlanUnit& y) { return x.work > y.work; });
+    // The last dispatch round drains while its units finish: PSX_K3_TAIL (a
+    // fraction of the shard's work, default kTailFrac) cuts the units at the end
+    // of the order into single-a units, so the drain is made of the shortest
+    // units.  Each (a, b, c) stays in the same shard, so the counts above hold.
+    static const double tail_frac = [] {
+        const char* e = std::getenv("PSX_K3_TAIL");
+        return e ? std::atof(e) : kTailFrac;
+    }();
+    if (tail_frac > 0 && ca > 1) {
+        double wtot = 0, wacc = 0;
+        for (auto& u : mine) wtot += u.work;
+        size_t cut = mine.size();
+        while (cut > 0 && wacc + mine[cut - 1].work <= tail_frac * wtot) wacc += mine[--cut].work;
+        std::vector<PlanUnit> tail;
+        for (size_t i = cut; i < mine.size(); i++) {
+            const PlanUnit& u = mine[i];
+            const double w1 = u.work / (u.a1 - u.a0);
+            for (int a = u.a0; a < u.a1; a++) {
+                PlanUnit v = u;
+                v.a0 = a;
+                v.a1 = a + 1;
+                v.work = w1;
+                tail.push_back(v);
+            }
+        }
+        mine.resize(cut);
+        std::stable_sort(tail.begin(), tail.end(), [](const PlanUnit& x, const PlanUnit& y) { return x.work > y.work; });
+        mine.insert(mine.end(), tail.begin(), tail.end());
+    }
     // (An XCD-aware order — runs of one tile's units packed onto the 8 XCDs,
     // workgroup i running on XCD (i + launch offset) % 8, so each 4 MB L2 serves
     // ~1/8 of the tile rows — measured neutral (r01y, worlds 1-8) once the next

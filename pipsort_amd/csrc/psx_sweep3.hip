@@ -103,47 +103,64 @@ __device__ __forceinline__ void wave_fold_set_dpp(SetRec& r) {
 // dependency chains interleave (one chain of DPP steps is ~100 cycles of
 // latency; eight of them back to back were ~1.8 us of the a prologue at two
 // waves per SIMD, tools/unit_trace.py).  Within each row of 16 lanes four
-// row_shl steps leave the row's sum / max in its lane 0; the four row values
-// are then combined in a fixed order, (r0 + r1) + (r2 + r3), identical in
-// every lane.  Every lane must be active.
+// row_shr steps leave the row's sum / max in its lane 15; row_bcast:15 (into
+// rows 1 and 3) and row_bcast:31 (into rows 2 and 3) then carry the rows into
+// lane 63, whose value (a fixed summation order) is read as a uniform.  Every
+// lane must be active.
 template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double x) {  // out-of-row lanes read 0
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xf, 0xf, false);
+__device__ __forceinline__ double dpp_f64(double x) {  // lanes without a source read 0 (bound_ctrl)
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xf, 0xf, true);
     return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double readlane_f64(double x, int lane) {
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), lane),
                             __builtin_amdgcn_readlane(__double2loint(x), lane));
 }
+// (row_bcast:15 adds lane 16r - 1 into row r, row_bcast:31 lane 31 into rows 2
+// and 3; rows without a source add 0: lane 63 ends with (S3 + S2) + (S1 + S0))
 template <int K>
 __device__ __forceinline__ void wave_sum_k(double (&v)[K]) {
 #pragma unroll
-    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x101>(v[k]);  // row_shl:1
+    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x111>(v[k]);  // row_shr:1
 #pragma unroll
-    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x102>(v[k]);  // row_shl:2
+    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x112>(v[k]);  // row_shr:2
 #pragma unroll
-    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x104>(v[k]);  // row_shl:4
+    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x114>(v[k]);  // row_shr:4
 #pragma unroll
-    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x108>(v[k]);  // row_shl:8
+    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x118>(v[k]);  // row_shr:8
 #pragma unroll
-    for (int k = 0; k < K; k++)
-        v[k] = (readlane_f64(v[k], 0) + readlane_f64(v[k], 16)) + (readlane_f64(v[k], 32) + readlane_f64(v[k], 48));
+    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x142>(v[k]);  // row_bcast:15
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x143>(v[k]);  // row_bcast:31
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] = readlane_f64(v[k], 63);
+}
+// maxima of values >= EMPTY, reduced as x - EMPTY >= 0 so that a lane without a
+// DPP source (reading 0) is neutral
+template <int CTRL>
+__device__ __forceinline__ int dpp_max_b(int y) {
+    return max(y, __builtin_amdgcn_mov_dpp(y, CTRL, 0xf, 0xf, true));
 }
 template <int K>
 __device__ __forceinline__ void wave_max_k(int (&v)[K]) {
+    int y[K];
 #pragma unroll
-    for (int k = 0; k < K; k++) v[k] = max(v[k], __builtin_amdgcn_update_dpp(EMPTY, v[k], 0x101, 0xf, 0xf, false));
+    for (int k = 0; k < K; k++) y[k] = v[k] - EMPTY;
 #pragma unroll
-    for (int k = 0; k < K; k++) v[k] = max(v[k], __builtin_amdgcn_update_dpp(EMPTY, v[k], 0x102, 0xf, 0xf, false));
+    for (int k = 0; k < K; k++) y[k] = dpp_max_b<0x111>(y[k]);
 #pragma unroll
-    for (int k = 0; k < K; k++) v[k] = max(v[k], __builtin_amdgcn_update_dpp(EMPTY, v[k], 0x104, 0xf, 0xf, false));
+    for (int k = 0; k < K; k++) y[k] = dpp_max_b<0x112>(y[k]);
 #pragma unroll
-    for (int k = 0; k < K; k++) v[k] = max(v[k], __builtin_amdgcn_update_dpp(EMPTY, v[k], 0x108, 0xf, 0xf, false));
+    for (int k = 0; k < K; k++) y[k] = dpp_max_b<0x114>(y[k]);
 #pragma unroll
-    for (int k = 0; k < K; k++)
-        v[k] = max(max(__builtin_amdgcn_readlane(v[k], 0), __builtin_amdgcn_readlane(v[k], 16)),
-                   max(__builtin_amdgcn_readlane(v[k], 32), __builtin_amdgcn_readlane(v[k], 48)));
+    for (int k = 0; k < K; k++) y[k] = dpp_max_b<0x118>(y[k]);
+#pragma unroll
+    for (int k = 0; k < K; k++) y[k] = dpp_max_b<0x142>(y[k]);
+#pragma unroll
+    for (int k = 0; k < K; k++) y[k] = dpp_max_b<0x143>(y[k]);
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] = __builtin_amdgcn_readlane(y[k], 63) + EMPTY;
 }
 
 // K (shift, sum) pairs at once, as wave_pair_dpp
@@ -905,7 +922,13 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     // inside its prologue / fold (t_fn: loads + barrier, per-study terms, slot
     // shift, closed forms; fold arithmetic)
     unsigned long long t_ph[4] = {0ull, 0ull, 0ull, 0ull}, t_fn[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
+    unsigned long long t_la[2] = {0ull, 0ull};
     if (A.trace) t_ph[0] = wall_clock64();
+    // The a record (the a's five sums over the wave) is reduced with the NEXT a's
+    // prologue batch, or with the unit's set record after the last a: one round
+    // of batched wave reductions per a instead of two.  rG = EMPTY: none pending.
+    double rW[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    int rG = EMPTY, rq = -1;
     for (int ai = 0; ai < a1 - a0; ai++) {
         const int va = a0 + ai, ua = va - pad;
         double l1[2], D1[2], w1h[2], Ep[2][4];  // Ep: {}, {a}, {c}, {a,c} relative to 2^R
@@ -915,6 +938,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         double2 gnx = g01[j0 * 64], mnx = m01[j0 * 64];
         int2 nnx = bnn[j0 * 64];
         const bool nxt = ai + 1 < a1 - a0;
+        if (A.trace && ai > 0 && !nxt) t_la[0] = wall_clock64();  // the last a's prologue (units of > 1 a)
         double nGab[2], nGac[2];
 #pragma unroll
         for (int s = 0; s < 2; s++) {
@@ -1040,14 +1064,18 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         asm volatile("" : "+s"(k256), "+s"(kc3), "+v"(kc2));
         // this a's wave maxima in one batch: G (the slot shift) and, for the closed
         // forms of off-diagonal units, R_s and the slots' {a, b} exponents
-        int mx[5] = {G, R[0], R[1], pMu[0] != 0.0 ? pN[0] : EMPTY, pMu[1] != 0.0 ? pN[1] : EMPTY};
+        // (and the previous a's record shift)
+        int mx[6] = {G, rG, R[0], R[1], pMu[0] != 0.0 ? pN[0] : EMPTY, pMu[1] != 0.0 ? pN[1] : EMPTY};
         if (sep) {
             wave_max_k(mx);
         } else {
-            int g1[1] = {G};
-            wave_max_k(g1);
-            mx[0] = g1[0];
+            int g2[2] = {G, rG};
+            wave_max_k(g2);
+            mx[0] = g2[0];
+            mx[1] = g2[1];
         }
+        // the previous a's record: its sums at the wave's largest shift
+        const int rGw = mx[1], rdg = rG != EMPTY ? rG - rGw : -2000;
         double abS[2] = {0.0, 0.0};  // sum over the slots of the {a, b} weights, at 2^abM
         int abM[2] = {EMPTY, EMPTY};
         double fS;  // a lane's contribution to the b slots is scaled by 2^(G - sM)
@@ -1072,22 +1100,26 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             // terms.  Lane t adds slot t's share.
             // (likewise the plain one-study sums of notSharedLL, uL: uL_s[0] = uW_s[0])
             // (and the walk sum of the {a, b} weights over the slots, V_s[1]: one batch)
-            const int Qm[2] = {mx[1], mx[2]};
-            double ws[8];
+            const int Qm[2] = {mx[2], mx[3]};
+            double ws[13];
 #pragma unroll
             for (int s = 0; s < 2; s++) {
                 ws[2 * s] = ldexp(uW[s][0], R[s] - Qm[s]);
                 ws[2 * s + 1] = ldexp(uW[s][1], R[s] - Qm[s]);
                 ws[4 + s] = ldexp(uL[s][1], R[s] - Qm[s]);
-                ws[6 + s] = pMu[s] != 0.0 ? ldexp(pMu[s], pN[s] - mx[3 + s]) : 0.0;
+                ws[6 + s] = pMu[s] != 0.0 ? ldexp(pMu[s], pN[s] - mx[4 + s]) : 0.0;
             }
+#pragma unroll
+            for (int i = 0; i < 5; i++) ws[8 + i] = ldexp(rW[i], rdg);
             wave_sum_k(ws);
             const double QW[2][2] = {{ws[0], ws[1]}, {ws[2], ws[3]}}, QL[2] = {ws[4], ws[5]};
 #pragma unroll
             for (int s = 0; s < 2; s++) {
                 abS[s] = ws[6 + s];
-                abM[s] = ws[6 + s] != 0.0 ? mx[3 + s] : EMPTY;
+                abM[s] = ws[6 + s] != 0.0 ? mx[4 + s] : EMPTY;
             }
+#pragma unroll
+            for (int i = 0; i < 5; i++) rW[i] = ws[8 + i];
             // E_s[A + b] of this lane's slot: {b} = pMuB 2^pN, {a, b} = pMu 2^pN
             const double e0 = ldexp(1.0, pN[0] + Qm[1] - sMt), e1 = ldexp(1.0, pN[1] + Qm[0] - sMt);
             sW0[t] += fma(pMuB[0], QW[1][0], pMu[0] * QW[1][1]) * e0;
@@ -1105,6 +1137,15 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             sW2[t] += z0;
             sSl[t] += z0;
         }
+        if (!sep) {
+            double r5[5];
+#pragma unroll
+            for (int i = 0; i < 5; i++) r5[i] = ldexp(rW[i], rdg);
+            wave_sum_k(r5);
+#pragma unroll
+            for (int i = 0; i < 5; i++) rW[i] = r5[i];
+        }
+        if (t == 0 && rq >= 0) store_rec(rec + rq, wrec(rGw, rW[0], rW[1], rW[2], rW[3], rW[4], rho, A.Ck, A.pit0));
         if (A.trace && ai == 0) t_fn[3] = wall_clock64();
         // the slot scale rides in the prior-weighted vectors (only the b-slot dot
         // products use them from here on; a power of two, so exact above underflow)
@@ -1112,6 +1153,14 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         for (int s = 0; s < 2; s++)
 #pragma unroll
             for (int i = 0; i < 4; i++) uW[s][i] *= fS;
+        // SEP: so does the notSharedLL vector (its whole-value check is on the slot
+        // totals), the {b, c} / {a, b, c} entries the walk uses
+        if (sep) {
+#pragma unroll
+            for (int s = 0; s < 2; s++)
+#pragma unroll
+                for (int i = 2; i < 4; i++) uL[s][i] *= fS;
+        }
         wave_lds_order();  // (a, b) terms and slot shifts visible
         if (nxt) {
 #pragma unroll
@@ -1121,6 +1170,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             }
         }
         if (A.trace && ai == 0) t_ph[1] = wall_clock64();
+        if (A.trace && ai > 0 && !nxt) t_la[1] = wall_clock64();
 
         // The b-walk.  chain(j) is step j's dependent {a, b, c} extension up to
         // the split of 2^h3 (N = round(256 h3), q = 2^(f/256) P^(-1/2)); finish(j)
@@ -1228,7 +1278,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             __hip_atomic_fetch_add(&sW1[bs], WB1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&sW2[bs], WB2 * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&sSl[bs], LB2 * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&sNs[bs], NB * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&sNs[bs], sepc ? NB : NB * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (!ALLPRES) npat += wac * bW[bs];
         };
         auto finish = [&](int j, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
@@ -1378,20 +1428,18 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             if (tiny) atomicOr(flag, 1);
         if (A.trace && ai == 0) t_fn[4] = wall_clock64();
         {
-            // the a record: every lane's five sums share its shift G, so the wave
-            // folds them at the largest G among lanes with content (a lane's
+            // the a record, pending: every lane's five sums share its shift G, so the
+            // wave folds them at the largest G among lanes with content (a lane's
             // notSharedLL is >= 2^-900 of its own G, so nothing that matters is
-            // lost) with DPP wave sums
+            // lost), in the next batch of wave reductions
             const bool has = (WA[0] + WA[1] + WA[2] + LA2 + NA) != 0.0;
-            int gw[1] = {has ? G : EMPTY};
-            wave_max_k(gw);
-            const int Gw = gw[0];
-            const int dg = has ? G - Gw : -2000;
-            double r5[5] = {ldexp(WA[0], dg), ldexp(WA[1], dg), ldexp(WA[2], dg), ldexp(LA2, dg), ldexp(NA, dg)};
-            wave_sum_k(r5);
-            const double W0 = r5[0], W1 = r5[1], W2 = r5[2], Sl = r5[3], Ns = r5[4];
-            const int qa = F.aPos[ai];
-            if (t == 0 && qa >= 0) store_rec(rec + qa, wrec(Gw, W0, W1, W2, Sl, Ns, rho, A.Ck, A.pit0));
+            rW[0] = WA[0];
+            rW[1] = WA[1];
+            rW[2] = WA[2];
+            rW[3] = LA2;
+            rW[4] = NA;
+            rG = has ? G : EMPTY;
+            rq = F.aPos[ai];
         }
         if (A.trace && ai == 0) t_ph[3] = wall_clock64();
     }
@@ -1425,18 +1473,24 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     sr.npat = npat;
     {
         // the unit's set record across the wave: three (shift, sum) pairs and the
-        // pattern count in one batch (score: 1e300 in every lane)
+        // pattern count, with the last a's pending record, in one batch (score:
+        // 1e300 in every lane)
         int m3[3] = {sr.m, sr.m0, sr.m1};
         double x3[3] = {sr.tot, sr.nc0, sr.nc1};
-        int M3[3];
+        int M3[4];
 #pragma unroll
         for (int k = 0; k < 3; k++) M3[k] = x3[k] != 0.0 ? m3[k] : EMPTY;
+        M3[3] = rG;
         wave_max_k(M3);
-        double x4[4];
+        const int rdg = rG != EMPTY ? rG - M3[3] : -2000;
+        double x4[9];
 #pragma unroll
         for (int k = 0; k < 3; k++) x4[k] = x3[k] != 0.0 ? ldexp(x3[k], m3[k] - M3[k]) : 0.0;
         x4[3] = sr.npat;
+#pragma unroll
+        for (int i = 0; i < 5; i++) x4[4 + i] = ldexp(rW[i], rdg);
         wave_sum_k(x4);
+        if (t == 0 && rq >= 0) store_rec(rec + rq, wrec(M3[3], x4[4], x4[5], x4[6], x4[7], x4[8], rho, A.Ck, A.pit0));
         sr.tot = x4[0];
         sr.m = x4[0] != 0.0 ? M3[0] : EMPTY;
         sr.nc0 = x4[1];
@@ -1459,6 +1513,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 ((unsigned long long)redo << 40);
         for (int i = 0; i < 4; i++) tr[4 + i] = t_ph[i];
         for (int i = 0; i < 6; i++) tr[8 + i] = t_fn[i];
+        tr[14] = t_la[0];
+        tr[15] = t_la[1];
     }
 }
 

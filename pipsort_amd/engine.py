@@ -126,6 +126,7 @@ class Timing(ctypes.Structure):
         ("flops", ctypes.c_double),
         ("exact_rerun", ctypes.c_int32),
         ("robust_units", ctypes.c_int32),
+        ("span_ms", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -201,6 +202,8 @@ def load_library(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.psx_abi_version() != 2 and os.environ.get("PSX_AB") != "1":
+        raise EngineError(PSX_ENODEV, f"{path}: ABI version {lib.psx_abi_version()}, this module needs 2")
     _lib = lib
     return lib
 

@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
     for name in decl:
         assert re.search(rf"\bT {name}\b", dyn), name
         assert getattr(lib, name)
-    assert lib.psx_abi_version() == 1
+    assert lib.psx_abi_version() == 2  # 2: psx_timing.span_ms
 
 
 def test_no_cpu_fallback():

@@ -128,3 +128,27 @@ def test_async_reports_exact_flag_and_sync_path_recovers(gpu):
         x.merge_partials(buf.data_ptr(), 2)
         flags.append(x.sync())
     assert flags == [True, True]
+
+
+@pytest.mark.parametrize("c", [2, 3])
+def test_overlapped_passes_bitwise_equal_sync(gpu, c, monkeypatch):
+    """PSX_OVERLAP: consecutive asynchronous sweeps on two CU-masked compute
+    streams (overlapping), merges on the reserved CUs: every pass still equals
+    the synchronous one bit for bit, and the per-pass span is reported."""
+    monkeypatch.setenv("PSX_OVERLAP", "8")
+    mi = _inputs(c=c)
+    a = E.PostCal(mi)
+    a.run_exhaustive()
+    ra = a.accum()
+    b = E.PostCal(mi)
+    for _ in range(7):
+        b.run_exhaustive_async()
+    assert b.sync() is False
+    t = b.timing()
+    assert t["kernel_launches"] == 7 and 0 < t["span_ms"] <= t["kernel_ms"]
+    rb = b.accum()
+    assert rb.n_configs == ra.n_configs and rb.total == ra.total
+    for f in FIELDS:
+        assert np.array_equal(getattr(ra, f), getattr(rb, f)), f
+    a.close()
+    b.close()

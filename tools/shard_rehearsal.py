@@ -70,13 +70,14 @@ def main():
             assert not pc.sync()
             t = pc.timing()
             ranks.append({"rank": rank, "step_ms": dt, "kernel_ms": t["kernel_ms"] / max(t["kernel_launches"], 1),
-                          "sweep_ms": t["sweep_ms"]})
+                          "sweep_ms": t["sweep_ms"], "span_ms": t.get("span_ms", 0.0)})
         ranks.sort(key=lambda r: r["rank"])
         worst = max(r["step_ms"] for r in ranks)
         out["worlds"][world] = {"max_step_ms": worst, "ranks": ranks}
         print(f"world {world}: max step {worst:.3f} ms; kernel ms per rank "
               f"{[round(r['kernel_ms'], 3) for r in ranks]}; step ms per rank "
-              f"{[round(r['step_ms'], 3) for r in ranks]}; sweep ms {[round(r['sweep_ms'], 3) for r in ranks]}",
+              f"{[round(r['step_ms'], 3) for r in ranks]}; span ms per pass {[round(r['span_ms'], 3) for r in ranks]}; "
+              f"sweep ms {[round(r['sweep_ms'], 3) for r in ranks]}",
               flush=True)
     base = out["worlds"].get(1, {}).get("max_step_ms")
     if base:

@@ -69,6 +69,11 @@ for dflag in (0, 1):
         print(f"   a prologue split: loads+barrier {d(fn[:, 0], ph[:, 0]):.2f}, per-study terms {d(fn[:, 1], fn[:, 0]):.2f}, "
               f"vectors+shifts+slot max {d(fn[:, 2], fn[:, 1]):.2f}, closed forms {d(fn[:, 3], fn[:, 2]):.2f}, "
               f"scale+barrier {d(ph[:, 1], fn[:, 3]):.2f}; fold {d(fn[:, 4], ph[:, 2]):.2f}, record {d(ph[:, 3], fn[:, 4]):.2f}")
+la = (tr[:, 15] - tr[:, 14]) / 100.0
+for dflag in (0, 1):
+    m = (diag == dflag) & (tr[:, 14] > 0)
+    if m.any():
+        print(f"{'diagonal' if dflag else 'off-diag'} LAST-a prologue (units of > 1 a, us, mean): {la[m].mean():.2f}")
 bu = np.array([d.mean() for d in np.array_split(dur[np.argsort(uid)], 10)])
 print("mean duration by unit-index decile:", np.round(bu, 1).tolist())
 
