@@ -408,12 +408,22 @@ struct Sweep3FastSmem {
     int2 abN[64];
     float bW[64];  // membership weight of the slot's b (0, 1 or 3)
     double sW0[64], sW1[64], sW2[64], sSl[64], sNs[64];
-    // off-diagonal units (closed-form sums, sweep3_unit_fast): this lane's c terms
-    double2 bcsm[64];           // the {b, c} weights of this lane's c summed over the block, both studies
-    int2 bcsn[64];
-    double2 bccm[64];           // the {b, c} weights of slot b summed over the tile's c, both studies
-    int2 bccn[64];
+    union {
+        struct {  // off-diagonal units (closed-form sums, sweep3_unit_fast): this lane's c terms
+            double2 bcsm[64];   // the {b, c} weights of this lane's c summed over the block, both studies
+            int2 bcsn[64];
+            double2 bccm[64];   // the {b, c} weights of slot b summed over the tile's c, both studies
+            int2 bccn[64];
+        };
+        struct {  // the other units: lane constants the a prologues read, parked across the walks
+            double2 lmuB[64];   // this lane's slot {b} weight, both studies (2^lnB * lmuB)
+            int2 lnB[64];
+            double2 lmuC[64];   // this lane's c {c} weight, both studies (2^lnC * lmuC)
+            int2 lnC[64];
+        };
+    };
     double pbS[2];              // sum of the block's {b} weights, both studies: 2^pbM * pbS
+    double kc2;                 // the walk's kC2 (non-SEP units read it per a)
     int pbM[2];
 };
 union SweepSmem {  // a block runs either a k = 3 unit or a level-2 unit
@@ -820,6 +830,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     // ---- unit prologue: the unit's constants are loaded once, into LDS where other
     // lanes read them and into registers where a lane reads only its own ---------------
     for (int i = t; i < 256; i += 64) tab[i] = A.tab[i];
+    if (t == 0) F.kc2 = kC2;
     const int vbl = 64 * K + t, ubl = vbl - pad;
     const bool okb = vbl >= pad;
     const int ib = okb ? ubl : 0;  // clamped index: the loads are unconditional
@@ -867,7 +878,11 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     // record positions (CSR map) of this unit's c / b-slot records; this a's
     // Sigma~ row entries (g1ab: this lane's b slot, g1ac: its c)
     const size_t rbase = (size_t)unit * rec_stride;
-    const int posC = pos[rbase + t], posB = pos[rbase + 64 + t];
+    int posC = 0, posB = 0;
+    if (SEP) {
+        posC = pos[rbase + t];
+        posB = pos[rbase + 64 + t];
+    }
     double g1ab[2], g1ac[2];
 #pragma unroll
     for (int s = 0; s < 2; s++) {
@@ -901,6 +916,12 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     // (sep): the walk sums V_s of the {b}, {a, b} and {b, c} weights, and the b
     // slot's one-study dot products over {b} and {a, b} (see below).
     constexpr bool sep = SEP;  // the caller checked !diag && j0 == 0 && j1 == 64
+    if (!sep) {
+        F.lmuB[t] = make_double2(muBb[0], muBb[1]);
+        F.lnB[t] = make_int2(nBb[0], nBb[1]);
+        F.lmuC[t] = make_double2(muC[0], muC[1]);
+        F.lnC[t] = make_int2(nC[0], nC[1]);
+    }
     if (sep) {
         F.bcsm[t] = l_bcsm;
         F.bcsn[t] = l_bcsn;
@@ -948,6 +969,15 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         }
         wave_lds_order();  // previous a's (a, b) terms and slots fully consumed
         if (A.trace && ai == 0) t_fn[0] = wall_clock64();
+        // this lane's {b} and {c} weights: registers (SEP), or re-read from LDS
+        double uB[2] = {muBb[0], muBb[1]}, uC[2] = {muC[0], muC[1]};
+        int uNB[2] = {nBb[0], nBb[1]}, uNC[2] = {nC[0], nC[1]};
+        if (!sep) {
+            const double2 x = F.lmuB[t], y = F.lmuC[t];
+            const int2 nx = F.lnB[t], ny = F.lnC[t];
+            uB[0] = x.x; uB[1] = x.y; uC[0] = y.x; uC[1] = y.y;
+            uNB[0] = nx.x; uNB[1] = nx.y; uNC[0] = ny.x; uNC[1] = ny.y;
+        }
         const unsigned pa = F.aP[ai];
         const double2 aAd = F.aAd[ai], aY = F.aY[ai];
         double pG[2], pI[2], pIW[2], pH[2], pR[2], pMu[2], pMuB[2];
@@ -975,8 +1005,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 int nAB;
                 double muAB;
                 split3(hab, rPab, tab, nAB, muAB);
-                const int nB = nBb[s];
-                const double muB = muBb[s];
+                const int nB = uNB[s];
+                const double muB = uB[s];
                 pG[s] = Gab;
                 pI[s] = rab * rab;
                 pIW[s] = rab * rab * (0.5 * wab);  // I_ab w_ab / 2 (the pivot itself is not needed)
@@ -1000,7 +1030,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             R[s] = n1;
             Ep[s][0] = ldexp(1.0, -n1);
             Ep[s][1] = ldexp(muA, nA - n1);
-            Ep[s][2] = ldexp(muC[s], nC[s] - n1);
+            Ep[s][2] = ldexp(uC[s], uNC[s] - n1);
             Ep[s][3] = mu1;
         }
         F.abG[t] = make_double2(pG[0], pG[1]);
@@ -1061,6 +1091,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         const double cmag[2] = {kMagic - 256.0 * R[0], kMagic - 256.0 * R[1]};
         // the walk's split constants as opaque registers (split3r)
         double k256 = 256.0, kc3 = kC3, kc2 = kC2;
+        if (!SEP) kc2 = F.kc2;  // (re-read per a: not live across the walk)
         asm volatile("" : "+s"(k256), "+s"(kc3), "+v"(kc2));
         // this a's wave maxima in one batch: G (the slot shift) and, for the closed
         // forms of off-diagonal units, R_s and the slots' {a, b} exponents
@@ -1442,6 +1473,10 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             rq = F.aPos[ai];
         }
         if (A.trace && ai == 0) t_ph[3] = wall_clock64();
+    }
+    if (!SEP) {  // (non-SEP units: loaded late, so they are not live across the walks)
+        posC = pos[rbase + t];
+        posB = pos[rbase + 64 + t];
     }
     wave_lds_order();
     {
