@@ -762,6 +762,7 @@ def main():
             "setup": {"synthetic_locus_s": t_synth, "gpu_model_setup_and_create_ms": pc.setup_info["setup_ms"],
                       "psd_added": pc.setup_info["psd_added"], "eigen_route": pc.setup_info["eigen_route"]},
             "pass_mode": "async (no host sync per step)" if use_async else "synchronous",
+            "span_ms_per_pass": tm.get("span_ms") if use_async else None,
             "configs_checked": int(acc.n_configs) if acc is not None else None,
         }
         if use_dist:

@@ -312,7 +312,7 @@ int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* 
 // the padded space v = u + pad.  Lane t owns c = 64C + t; b runs over block K;
 // a over [a0, a1) with a < b.  Exact per-shard set / configuration / byte counts
 // in O(64 * 9) per unit from per-class prefix counts over v.
-constexpr double kTailFrac = 0.0;  // share of a shard's work cut into single-a units at the end (PSX_K3_TAIL)
+constexpr double kTailFrac = 0.05;  // share of a shard's work cut into single-a units at the end (PSX_K3_TAIL)
 
 int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_host, std::vector<PlanUnit>& mine,
                  int& ca, double& sets, double& configs, double& bytes) {

@@ -950,22 +950,41 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     // of batched wave reductions per a instead of two.  rG = EMPTY: none pending.
     double rW[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     int rG = EMPTY, rq = -1;
+    // global loads of each a, all consumed late (no wait in the prologue): the
+    // walk's first tile row, and the next a's Sigma~ row entries; the first a's
+    // are issued here, in flight with the unit prologue's, in off-diagonal units
+    // (their wait at the loop entry was ~1 us of the first a's prologue, r04p;
+    // the other units' registers would spill)
+    double2 gnx = make_double2(0.0, 0.0), mnx = make_double2(0.0, 0.0);
+    int2 nnx = make_int2(0, 0);
+    double nGab[2] = {0.0, 0.0}, nGac[2] = {0.0, 0.0};
+    if (SEP) {
+        gnx = g01[j0 * 64];
+        mnx = m01[j0 * 64];
+        nnx = bnn[j0 * 64];
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const double* row = A.G[s] + (size_t)(a1 - a0 > 1 ? a0 + 1 - pad : a0 - pad) * ldg;
+            nGab[s] = row[ib];
+            nGac[s] = row[ic];
+        }
+    }
     for (int ai = 0; ai < a1 - a0; ai++) {
         const int va = a0 + ai, ua = va - pad;
         double l1[2], D1[2], w1h[2], Ep[2][4];  // Ep: {}, {a}, {c}, {a,c} relative to 2^R
         int R[2];
-        // global loads of this a, all consumed late (no wait in the prologue): the
-        // walk's first tile row, and the next a's Sigma~ row entries
-        double2 gnx = g01[j0 * 64], mnx = m01[j0 * 64];
-        int2 nnx = bnn[j0 * 64];
         const bool nxt = ai + 1 < a1 - a0;
         if (A.trace && ai > 0 && !nxt) t_la[0] = wall_clock64();  // the last a's prologue (units of > 1 a)
-        double nGab[2], nGac[2];
+        if (!SEP || ai > 0) {
+            gnx = g01[j0 * 64];
+            mnx = m01[j0 * 64];
+            nnx = bnn[j0 * 64];
 #pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const double* row = A.G[s] + (size_t)(nxt ? ua + 1 : ua) * ldg;
-            nGab[s] = row[ib];
-            nGac[s] = row[ic];
+            for (int s = 0; s < 2; s++) {
+                const double* row = A.G[s] + (size_t)(nxt ? ua + 1 : ua) * ldg;
+                nGab[s] = row[ib];
+                nGac[s] = row[ic];
+            }
         }
         wave_lds_order();  // previous a's (a, b) terms and slots fully consumed
         if (A.trace && ai == 0) t_fn[0] = wall_clock64();
