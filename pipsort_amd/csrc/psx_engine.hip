@@ -1157,11 +1157,24 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     hipStream_t S = X;          // sweeps
     int par = 0;
     if (async) {
-        if (!e->cstream) {
-            if (e->ovl < 0) {
-                const char* o = getenv("PSX_OVERLAP");
-                e->ovl = o ? std::max(0, atoi(o)) : 0;
+        // reserved CUs for overlapped sweeps: PSX_OVERLAP, or by default one per
+        // XCD on shards of worlds >= 4, whose last dispatch round is a large share
+        // of a pass (same-box rehearsal: worlds 4 / 8 -5 %, world 1 +2 %, DESIGN.md
+        // 5c); the compute streams are rebuilt when the shard's world changes it
+        const char* ovl_env = getenv("PSX_OVERLAP");
+        const int want = ovl_env ? std::max(0, atoi(ovl_env)) : (e->world >= 4 ? 8 : 0);
+        if (e->cstream && want != e->ovl) {
+            HIPCHK(hipStreamSynchronize(e->cstream));
+            HIPCHK(hipStreamDestroy(e->cstream));
+            e->cstream = nullptr;
+            if (e->cstream2) {
+                HIPCHK(hipStreamSynchronize(e->cstream2));
+                HIPCHK(hipStreamDestroy(e->cstream2));
+                e->cstream2 = nullptr;
             }
+        }
+        if (!e->cstream) {
+            e->ovl = want;
             int ncu = 0;
             HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->dev));
             if (e->ovl > 0 && e->ovl < ncu) {
@@ -1193,7 +1206,7 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
                 HIPCHK(hipStreamCreateWithPriority(&e->cstream, hipStreamNonBlocking, (lo_pr + hi_pr) / 2));
             }
             for (int i = 0; i < psx_engine::kBufs; i++)
-                HIPCHK(hipEventCreateWithFlags(&e->mdone[i], hipEventDisableTiming));
+                if (!e->mdone[i]) HIPCHK(hipEventCreateWithFlags(&e->mdone[i], hipEventDisableTiming));
         }
         S = e->cstream;
         if (e->cstream2) {

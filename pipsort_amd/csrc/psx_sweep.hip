@@ -461,6 +461,34 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
         }
         mine.resize(cut);
         std::stable_sort(tail.begin(), tail.end(), [](const PlanUnit& x, const PlanUnit& y) { return x.work > y.work; });
+        // PSX_K3_TAIL2 (a fraction of the shard's work, default 0): the very last
+        // diagonal single-a units walk half their (folded) steps each, so the
+        // final drain is made of half-length pieces; each pair of the block is
+        // still visited once (steps 1..16 | 17..32)
+        static const double tail2 = [] {
+            const char* e = std::getenv("PSX_K3_TAIL2");
+            return e ? std::atof(e) : 0.0;
+        }();
+        if (tail2 > 0) {
+            double w2 = 0;
+            size_t c2 = tail.size();
+            while (c2 > 0 && tail[c2 - 1].B == tail[c2 - 1].T && tail[c2 - 1].j0 == 0 && tail[c2 - 1].j1 == 64 &&
+                   w2 + tail[c2 - 1].work <= tail2 * wtot)
+                w2 += tail[--c2].work;
+            std::vector<PlanUnit> halves;
+            for (size_t i = c2; i < tail.size(); i++) {
+                PlanUnit h = tail[i];
+                h.work *= 0.5;
+                h.j0 = 0;
+                h.j1 = 32;
+                halves.push_back(h);
+                h.j0 = 32;
+                h.j1 = 64;
+                halves.push_back(h);
+            }
+            tail.resize(c2);
+            tail.insert(tail.end(), halves.begin(), halves.end());
+        }
         mine.insert(mine.end(), tail.begin(), tail.end());
     }
     // (An XCD-aware order — runs of one tile's units packed onto the 8 XCDs,
@@ -499,11 +527,11 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     P.alg_bytes = bytes;
     // FP64 operations per union set (FMA = 2), fitted to the PMC FP64 counts of
     // the k = 3 fast kernel (64 x SQ_INSTS_VALU_FLOPS_FP64 / sets: 281 before the
-    // deferred fold, 159 after it (r02zd), 141.8 in r03zb, ~139 since the uniform
-    // slot shift): kept at or below the last count, so a bench line without PMC
+    // deferred fold, 159 after it (r02zd), 141.8 in r03zb, 139.2 in r04h, 132.5 in
+    // r04t): kept at or below the last count, so a bench line without PMC
     // counters of its own build cannot overstate the FP64 rate; k = 2 by the
     // round-1 ratio of VALU work per set.  bench.py reports it only as a model.
-    P.flops = sets * (k == 3 ? 138.0 : 110.0);
+    P.flops = sets * (k == 3 ? 132.0 : 110.0);
     const int pad = variant ? ldg - U : 0;  // record keys of variant 1 are in v space
     // device buffers
     std::vector<int4> hu(P.n_units);

@@ -158,9 +158,9 @@ def test_host_lu_det_matches_numpy_and_underflows_like_gsl():
 def test_k3_units_cover_every_walk_step_once(U, world):
     """The k = 3 work units of all shards cover every (a, tile, b-walk step) of
     the block-pattern decomposition exactly once (a units may split a b-walk:
-    the ranges of one (a, tile) must tile [0, 64)).  The a-chunk sizes depend on
-    the CU count of the current device (or a CPU-only default), the coverage
-    does not."""
+    the ranges of one (a, tile) must tile [0, 64); the tail split cuts the last
+    units into single-a units, PSX_K3_TAIL2 into half walks).  The a-chunk sizes
+    are sized for 256 CUs whatever the device, so every rank cuts the same list."""
     ldg = (U + 63) // 64 * 64
     pad = ldg - U
     seen = {}
