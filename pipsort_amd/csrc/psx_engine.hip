@@ -1157,24 +1157,14 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     hipStream_t S = X;          // sweeps
     int par = 0;
     if (async) {
-        // reserved CUs for overlapped sweeps: PSX_OVERLAP, or by default one per
-        // XCD on shards of worlds >= 4, whose last dispatch round is a large share
-        // of a pass (same-box rehearsal: worlds 4 / 8 -5 %, world 1 +2 %, DESIGN.md
-        // 5c); the compute streams are rebuilt when the shard's world changes it
-        const char* ovl_env = getenv("PSX_OVERLAP");
-        const int want = ovl_env ? std::max(0, atoi(ovl_env)) : (e->world >= 4 ? 8 : 0);
-        if (e->cstream && want != e->ovl) {
-            HIPCHK(hipStreamSynchronize(e->cstream));
-            HIPCHK(hipStreamDestroy(e->cstream));
-            e->cstream = nullptr;
-            if (e->cstream2) {
-                HIPCHK(hipStreamSynchronize(e->cstream2));
-                HIPCHK(hipStreamDestroy(e->cstream2));
-                e->cstream2 = nullptr;
-            }
-        }
         if (!e->cstream) {
-            e->ovl = want;
+            // reserved CUs for overlapped sweeps (PSX_OVERLAP = n, opt-in), decided
+            // at the handle's first asynchronous pass.  Measured:
+            // worlds 4 / 8 -2 .. -5 % on some boxes, neutral on others, world 1
+            // +2 %; rebuilding the streams when a handle's world changed was
+            // 20-25 % slower (r04u), so it is not switched per world.
+            const char* ovl_env = getenv("PSX_OVERLAP");
+            e->ovl = ovl_env ? std::max(0, atoi(ovl_env)) : 0;
             int ncu = 0;
             HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->dev));
             if (e->ovl > 0 && e->ovl < ncu) {

@@ -348,7 +348,7 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     }();
     const double kTarget = rounds * (4.0 * PSX_K3_WAVES * kPlanCUs);
     ca = (int)std::lround(total_a / (kTarget * world));
-    ca = std::min(ca, kMaxChunkA3);
+    ca = std::min(ca, kMaxChunkA3);  // (caps 6 / 8 with the tail split: +0.4 / +1.5 % at world 1, r04w)
     ca = std::max(1, std::min(64, ca));
     const int cad = std::max(1, ca / diag_div);
     // Every union triple x < y < z belongs to exactly one unit family, by which
