@@ -603,6 +603,11 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_pass_l1(DevProb P, int 
 
 }  // namespace
 
+namespace {
+struct SssDev;                 // the SSS walk's workspace (kept across walks)
+void sss_release(SssDev* d);
+}  // namespace
+
 // ===========================================================================
 // Host engine
 // ===========================================================================
@@ -693,6 +698,9 @@ struct psx_engine {
     // configs-file enumerator (psx_configs.hip): index maps on the device, workspace
     int* d_cfg_maps = nullptr;  // l2u[N] | u2l[2 * U]
     psx::CfgWork cfg;
+    // SSS walk workspace: the set map, per-item rows / marks and the pinned
+    // host buffers, grown on demand and reused by the next walk
+    SssDev* sss = nullptr;
     // timing
     hipEvent_t ev[4];
     psx_timing timing;
@@ -713,6 +721,7 @@ psx_engine::~psx_engine() {
     psx::sweep_free(plans);
     psx::configs_free(cfg);
     hipFree(d_cfg_maps);
+    sss_release(sss);
     for (auto& kv : glevels) {
         GenLevel& g = kv.second;
         hipFree(g.d_sets); hipFree(g.d_csr); hipFree(g.d_srec); hipFree(g.d_mrec);
@@ -2179,6 +2188,11 @@ __global__ void k_map_rehash(const MapEntry* __restrict__ old, size_t n, MapEntr
 struct SssDev {
     MapEntry* T = nullptr;
     size_t cap = 0, used = 0;
+    size_t nmax = 0, nmax_full = 0;  // item capacity of the per-item arrays (full / hscore)
+    // (start, stop) event pairs around the evals, read kRingE iterations later
+    // (by then complete) instead of once per iteration
+    static constexpr int kRingE = 32;
+    hipEvent_t ev[2 * kRingE] = {};
     int* rows = nullptr;      // per item: its set (evaluated items)
     int* mark = nullptr;      // per neighbour: -1 seen, -2 unseen null, else its item
     int* cnt = nullptr;
@@ -2199,8 +2213,57 @@ struct SssDev {
         if (hcnt) hipHostFree(hcnt);
         if (hmark) hipHostFree(hmark);
         if (hscore) hipHostFree(hscore);
+        for (int i = 0; i < 2 * kRingE; i++)
+            if (ev[i]) hipEventDestroy(ev[i]);
     }
 };
+
+void sss_release(SssDev* d) { delete d; }
+
+// the walk's workspace for up to nmax items per iteration (grown, never shrunk;
+// the map is cleared for every walk)
+int sss_workspace(psx_engine* e, size_t nmax, int world, hipStream_t s) {
+    if (!e->sss) e->sss = new SssDev();
+    SssDev& D = *e->sss;
+    if (!D.cnt) {
+        for (int i = 0; i < 2 * SssDev::kRingE; i++) HIPCHK(hipEventCreate(&D.ev[i]));
+        HIPCHK(hipMalloc(&D.cnt, kNCnt * sizeof(int)));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.shost), sizeof(SetRec)));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hcnt), kNCnt * sizeof(int)));
+    }
+    if (D.nmax < nmax) {
+        hipFree(D.rows); hipFree(D.mark);
+        if (D.lk) hipHostFree(D.lk);
+        if (D.hmark) hipHostFree(D.hmark);
+        D.rows = D.mark = D.hmark = nullptr;
+        D.lk = nullptr;
+        HIPCHK(hipMalloc(&D.rows, nmax * PSX_KMAX * sizeof(int)));
+        HIPCHK(hipMalloc(&D.mark, nmax * sizeof(int)));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.lk), nmax * sizeof(double)));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hmark), nmax * sizeof(int)));
+        D.nmax = nmax;
+    }
+    if (world > 1 && D.nmax_full < nmax) {
+        hipFree(D.full);
+        if (D.hscore) hipHostFree(D.hscore);
+        D.full = nullptr;
+        D.hscore = nullptr;
+        HIPCHK(hipMalloc(&D.full, nmax * sizeof(double)));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hscore), nmax * sizeof(double)));
+        D.nmax_full = nmax;
+    }
+    size_t cap = 1 << 16;
+    while (cap < 4 * nmax) cap <<= 1;
+    if (D.cap < cap) {
+        hipFree(D.T);
+        D.T = nullptr;
+        HIPCHK(hipMalloc(&D.T, cap * sizeof(MapEntry)));
+        D.cap = cap;
+    }
+    HIPCHK(hipMemsetAsync(D.T, 0, D.cap * sizeof(MapEntry), s));
+    D.used = 0;
+    return 0;
+}
 
 int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* iterations_out) {
     HIPCHK(hipSetDevice(e->dev));
@@ -2215,23 +2278,8 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
     // the most items of an iteration: the current configuration + the largest
     // neighbourhood (k = C: swaps C (U - C), minus C; k < C: + U - k plus sets)
     const size_t nmax = (size_t)C * U + C + U + 2;
-    SssDev D;
-    size_t cap = 1 << 16;
-    while (cap < 4 * nmax) cap <<= 1;
-    HIPCHK(hipMalloc(&D.T, cap * sizeof(MapEntry)));
-    HIPCHK(hipMemsetAsync(D.T, 0, cap * sizeof(MapEntry), e->stream));
-    D.cap = cap;
-    HIPCHK(hipMalloc(&D.rows, nmax * stride * sizeof(int)));
-    HIPCHK(hipMalloc(&D.mark, nmax * sizeof(int)));
-    HIPCHK(hipMalloc(&D.cnt, kNCnt * sizeof(int)));
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.lk), nmax * sizeof(double)));
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.shost), sizeof(SetRec)));
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hcnt), kNCnt * sizeof(int)));
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hmark), nmax * sizeof(int)));
-    if (world > 1) {
-        HIPCHK(hipMalloc(&D.full, nmax * sizeof(double)));
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hscore), nmax * sizeof(double)));
-    }
+    if ((rc = sss_workspace(e, nmax, world, e->stream))) return rc;
+    SssDev& D = *e->sss;
     if ((rc = ensure(e->dsrec, e->cap_srec, nmax))) return rc;
     if ((rc = ensure(e->dmrec, e->cap_mrec, nmax * stride))) return rc;
     if ((rc = ensure(e->dscore, e->cap_score, nmax))) return rc;
@@ -2288,10 +2336,16 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
         // plain event records around the eval (the stop event is what the host
         // waits on): hipExtLaunchKernelGGL's in-packet events cost the host ~12 us
         // more per launch here (profiles/r03i_sss_host_phases.txt)
-        HIPCHK(hipEventRecord(e->ev[2], e->stream));
+        hipEvent_t* evp = D.ev + 2 * (iter % SssDev::kRingE);
+        if (iter >= SssDev::kRingE) {  // this pair's eval of kRingE iterations ago
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, evp[0], evp[1]));
+            kms += ms;
+        }
+        HIPCHK(hipEventRecord(evp[0], e->stream));
         hipLaunchKernelGGL(k_sss_eval, dim3((unsigned)n_items), dim3(64), 0, e->stream, e->dp, it, D.T, mask, lo, hi,
                            D.rows, D.mark, D.cnt, D.lk, e->dsrec, e->dmrec, e->dscore, world == 1 ? D.hmark : nullptr);
-        HIPCHK(hipEventRecord(e->ev[3], e->stream));
+        HIPCHK(hipEventRecord(evp[1], e->stream));
         const unsigned post_blocks = (unsigned)(U + 1 + (world == 1 ? (n_nbd + 255) / 256 : 0));
         hipLaunchKernelGGL(k_sss_post, dim3(post_blocks), dim3(256), 0, e->stream, it, lo, hi, D.rows, D.mark, D.cnt,
                            e->dmrec, e->dsrec, e->dscore, null1, e->dacc, e->dsacc, D.shost, D.hcnt, D.T, mask,
@@ -2305,7 +2359,7 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
             // GPU folds the records and inserts the new scores (k_sss_post); it
             // waits for the post only where the stop test needs the normaliser.
             tick(0, tp);
-            HIPCHK(hipEventSynchronize(e->ev[3]));
+            HIPCHK(hipEventSynchronize(evp[1]));
             tick(1, tp);
             for (int i = 0; i < n_nbd; i++) unseen += D.hmark[i] != -1;
         } else {
@@ -2342,11 +2396,6 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
                                (SetRec*)nullptr, (SetRec*)nullptr, (int*)nullptr, D.T, mask, 2, D.lk);
             HIPCHK(hipGetLastError());
             HIPCHK(hipStreamSynchronize(e->stream));
-        }
-        {
-            float ms = 0;
-            HIPCHK(hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
-            kms += ms;
         }
         D.used += (size_t)unseen;
         if (unseen == 0) break;                                                          // :260-263
@@ -2407,6 +2456,14 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
     }
     HIPCHK(hipStreamSynchronize(e->stream));  // the last iteration's post (one rank: not waited for in the loop)
     auto t1 = std::chrono::steady_clock::now();
+    {  // the evals still in the event ring (iterations 0..iter ran; `iter` itself when it broke out)
+        const int ran = std::min(iter + 1, 1000);
+        for (int q = std::max(0, ran - SssDev::kRingE); q < ran; q++) {
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, D.ev[2 * (q % SssDev::kRingE)], D.ev[2 * (q % SssDev::kRingE) + 1]));
+            kms += ms;
+        }
+    }
     if (prof)
         fprintf(stderr, "[psx sss] %d iterations, host us per iteration: launch %.1f, wait eval %.1f, sampling %.1f, "
                 "wait post %.1f\n", iter, ph[0] / std::max(iter, 1), ph[1] / std::max(iter, 1),

@@ -246,7 +246,17 @@ def test_sss_long_walk_m100_c5(gpu):
     it = pc.run_sss()
     ref = O.postcal(seam, "sss")
     assert it >= 20
-    assert_parity(pc.accum(), ref, pip_tol=1e-9, ll_rtol=1e-9)
+    first = pc.accum()
+    assert_parity(first, ref, pip_tol=1e-9, ll_rtol=1e-9)
+    assert pc.timing()["kernel_ms"] > 0
+    # the walk's workspace (set map, rows, pinned buffers, event ring) is kept
+    # by the handle: a second walk, after an exhaustive pass, is the same walk
+    pc.run_exhaustive()
+    assert pc.run_sss() == it
+    again = pc.accum()
+    assert again.n_configs == first.n_configs and again.total == first.total
+    for f in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+        assert np.array_equal(getattr(again, f), getattr(first, f)), f
     pc.close()
 
 
