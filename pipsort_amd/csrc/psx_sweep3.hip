@@ -394,6 +394,10 @@ struct Sweep3Smem {
     double sP0[64], sP1[64], sSh[64], sSl[64], sNs[64];
     int sM[64];
     int aPos[kMaxChunkA3];  // a record positions
+    // lane constants the a prologues read, parked across the walks (registers
+    // would spill): this lane's b slot ({b} quadratic form, pivot factor) and c
+    double lbH[2][64], lbR[2][64], lAcc[2][64], lyc[2][64], lmuC[2][64];
+    int lnC[2][64];
 };
 // LDS of the fast k = 3 variant: the per-b terms of both studies side by side
 // (one 16-byte read per term and step; lane t reads slot (t + j) & 63, so the
@@ -420,6 +424,10 @@ struct Sweep3FastSmem {
             int2 lnB[64];
             double2 lmuC[64];   // this lane's c {c} weight, both studies (2^lnC * lmuC)
             int2 lnC[64];
+            double2 lAbb[64];   // this lane's b slot / c: A_bb, y_b, A_cc, y_c, both studies
+            double2 lyb[64];
+            double2 lAcc[64];
+            double2 lyc[64];
         };
     };
     double pbS[2];              // sum of the block's {b} weights, both studies: 2^pbM * pbS
@@ -480,12 +488,11 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
     const int vbl = 64 * K + t, ubl = vbl - pad;
     const bool okb = vbl >= pad;
     const unsigned pbl = okb ? A.pres[ubl] : 0u;
-    double bH[2], bR[2];  // this lane's b slot: {b} quadratic form and pivot factor
 #pragma unroll
-    for (int s = 0; s < 2; s++) {
+    for (int s = 0; s < 2; s++) {  // this lane's b slot: {b} quadratic form and pivot factor
         const BTerms b = b_terms<ALLPRES>(A, s, vbl);
-        bH[s] = b.H;
-        bR[s] = b.R;
+        sm.s3.lbH[s][t] = b.H;
+        sm.s3.lbR[s][t] = b.R;
     }
     bW[t] = (float)memb_weight(pbl);
     sM[t] = EMPTY;
@@ -495,16 +502,13 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
     const int vc = 64 * C + t, uc = vc - pad;
     const bool okc = vc >= pad;
     const unsigned pcm = okc ? A.pres[uc] : 0u;
-    double Acc[2], yc[2], ych[2], chic[2], muC[2];
-    int nC[2];
 #pragma unroll
     for (int s = 0; s < 2; s++) {
-        chic[s] = (okc && (ALLPRES || ((pcm >> s) & 1u))) ? 1.0 : 0.0;
-        Acc[s] = okc ? A.Ad[s][uc] : 1.0;
-        yc[s] = okc ? A.ys[s][uc] : 0.0;
-        ych[s] = 0.5 * yc[s];
-        muC[s] = okc ? A.muS[s][uc] * chic[s] : 0.0;
-        nC[s] = okc ? A.nS[s][uc] : 0;
+        const double chic = (okc && (ALLPRES || ((pcm >> s) & 1u))) ? 1.0 : 0.0;
+        sm.s3.lAcc[s][t] = okc ? A.Ad[s][uc] : 1.0;
+        sm.s3.lyc[s][t] = okc ? A.ys[s][uc] : 0.0;
+        sm.s3.lmuC[s][t] = okc ? A.muS[s][uc] * chic : 0.0;
+        sm.s3.lnC[s][t] = okc ? A.nS[s][uc] : 0;
     }
     const double wc = memb_weight(pcm);
 
@@ -524,12 +528,6 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
     const size_t rbase = (size_t)unit * rec_stride;
     const int posC = pos[rbase + t], posB = pos[rbase + 64 + t];
     if (t < a1 - a0) sm.s3.aPos[t] = pos[rbase + 128 + t];
-    double g1ab[2], g1ac[2];
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-        g1ab[s] = okb ? A.G[s][(size_t)(a0 - pad) * ldg + ubl] : 0.0;
-        g1ac[s] = okc ? A.G[s][(size_t)(a0 - pad) * ldg + uc] : 0.0;
-    }
 
     for (int ai = 0; ai < a1 - a0; ai++) {
         const int va = a0 + ai, ua = va - pad;  // a0 >= pad: a is always a real SNP
@@ -553,7 +551,7 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
             split3(ha, rPa, tab, nA, muA);
             {
                 // {a, b} and {b} for this lane's b, into LDS
-                const double Gab = ai ? (okb ? A.G[s][(size_t)ua * ldg + ubl] : 0.0) : g1ab[s];
+                const double Gab = okb ? A.G[s][(size_t)ua * ldg + ubl] : 0.0;
                 const double Abb = okb ? A.Ad[s][ubl] : 1.0;
                 const double yb = okb ? A.ys[s][ubl] : 0.0;
                 const double l = Gab * iAaa;
@@ -567,7 +565,7 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
                 int nAB, nB;
                 double muAB, muB;
                 split3(hab, rPab, tab, nAB, muAB);
-                split3(bH[s], bR[s] * (2.0 / A.rsd[s]), tab, nB, muB);
+                split3(sm.s3.lbH[s][t], sm.s3.lbR[s][t] * (2.0 / A.rsd[s]), tab, nB, muB);
                 abG[s][t] = Gab;
                 abI[s][t] = rab * rab;
                 abW[s][t] = 0.5 * wab;
@@ -578,14 +576,15 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
                 abN[s][t] = nAB;
             }
             // {a, c}: lane-owned
-            const double Gac = ai ? (okc ? A.G[s][(size_t)ua * ldg + uc] : 0.0) : g1ac[s];
+            const double Gac = okc ? A.G[s][(size_t)ua * ldg + uc] : 0.0;
+            const double chic = (okc && (ALLPRES || ((pcm >> s) & 1u))) ? 1.0 : 0.0;
             l1[s] = Gac * iAaa;
-            D1[s] = fma(-l1[s], Gac, Acc[s]);
-            const double w1 = fma(-l1[s], ya, yc[s]);
+            D1[s] = fma(-l1[s], Gac, sm.s3.lAcc[s][t]);
+            const double w1 = fma(-l1[s], ya, sm.s3.lyc[s][t]);
             w1h[s] = 0.5 * w1;
             const double r1 = rsqrt_nr(D1[s]);
             const double h1 = fma(w1 * w1, r1 * r1, ha);
-            const double rP1 = rPa * r1 * A.rsd[s] * chic[s];
+            const double rP1 = rPa * r1 * A.rsd[s] * chic;
             int n1;
             double mu1;
             split3(h1, rP1, tab, n1, mu1);
@@ -593,7 +592,7 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
             R[s] = n1;
             Ep[s][0] = ldexp(1.0, -n1);
             Ep[s][1] = ldexp(muA, nA - n1);
-            Ep[s][2] = ldexp(muC[s], nC[s] - n1);
+            Ep[s][2] = ldexp(sm.s3.lmuC[s][t], sm.s3.lnC[s][t] - n1);
             Ep[s][3] = mu1;
         }
         const double wac = wc * memb_weight(pa);
@@ -856,7 +855,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     const bool okc = vc >= pad;
     const int ic = okc ? uc : 0;
     const unsigned pcm = okc ? A.pres[ic] : 0u;
-    double Acc[2], yc[2], chic[2], muC[2];
+    double Acc[2], yc[2], chic[2], muC[2];  // (chic: recomputed where used after the prologue)
     int nC[2];
 #pragma unroll
     for (int s = 0; s < 2; s++) {
@@ -921,6 +920,10 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         F.lnB[t] = make_int2(nBb[0], nBb[1]);
         F.lmuC[t] = make_double2(muC[0], muC[1]);
         F.lnC[t] = make_int2(nC[0], nC[1]);
+        F.lAbb[t] = make_double2(Abb[0], Abb[1]);
+        F.lyb[t] = make_double2(yb[0], yb[1]);
+        F.lAcc[t] = make_double2(Acc[0], Acc[1]);
+        F.lyc[t] = make_double2(yc[0], yc[1]);
     }
     if (sep) {
         F.bcsm[t] = l_bcsm;
@@ -997,6 +1000,13 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             uB[0] = x.x; uB[1] = x.y; uC[0] = y.x; uC[1] = y.y;
             uNB[0] = nx.x; uNB[1] = nx.y; uNC[0] = ny.x; uNC[1] = ny.y;
         }
+        // this lane's A_bb, y_b, A_cc, y_c: registers (SEP), or re-read from LDS
+        double vAbb[2] = {Abb[0], Abb[1]}, vyb[2] = {yb[0], yb[1]}, vAcc[2] = {Acc[0], Acc[1]}, vyc[2] = {yc[0], yc[1]};
+        if (!sep) {
+            const double2 p = F.lAbb[t], q = F.lyb[t], r = F.lAcc[t], u = F.lyc[t];
+            vAbb[0] = p.x; vAbb[1] = p.y; vyb[0] = q.x; vyb[1] = q.y;
+            vAcc[0] = r.x; vAcc[1] = r.y; vyc[0] = u.x; vyc[1] = u.y;
+        }
         const unsigned pa = F.aP[ai];
         const double2 aAd = F.aAd[ai], aY = F.aY[ai];
         double pG[2], pI[2], pIW[2], pH[2], pR[2], pMu[2], pMuB[2];
@@ -1015,9 +1025,9 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             {
                 const double Gab = g1ab[s];
                 const double l = Gab * iAaa;
-                const double Dab = fma(-l, Gab, Abb[s]);
+                const double Dab = fma(-l, Gab, vAbb[s]);
                 const double rab = rsqrt_nr(Dab);
-                const double wab = fma(-l, ya, yb[s]);
+                const double wab = fma(-l, ya, vyb[s]);
                 const double hab = fma(wab * wab, rab * rab, ha);
                 const bool chib = okb && (ALLPRES || ((pbl >> s) & 1u));
                 const double rPab = chib ? rPa * rab * A.rsd[s] : 0.0;
@@ -1037,12 +1047,13 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             }
             const double Gac = g1ac[s];
             l1[s] = Gac * iAaa;
-            D1[s] = fma(-l1[s], Gac, Acc[s]);
-            const double w1 = fma(-l1[s], ya, yc[s]);
+            D1[s] = fma(-l1[s], Gac, vAcc[s]);
+            const double w1 = fma(-l1[s], ya, vyc[s]);
             w1h[s] = 0.5 * w1;
             const double r1 = rsqrt_nr(D1[s]);
             const double h1 = fma(w1 * w1, r1 * r1, ha);
-            const double rP1 = rPa * r1 * A.rsd[s] * chic[s];
+            const double chic = (okc && (ALLPRES || ((pcm >> s) & 1u))) ? 1.0 : 0.0;
+            const double rP1 = rPa * r1 * A.rsd[s] * chic;
             int n1;
             double mu1;
             split3(h1, rP1, tab, n1, mu1);
