@@ -313,6 +313,7 @@ int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* 
 // a over [a0, a1) with a < b.  Exact per-shard set / configuration / byte counts
 // in O(64 * 9) per unit from per-class prefix counts over v.
 constexpr double kTailFrac = 0.05;  // share of a shard's work cut into single-a units at the end (PSX_K3_TAIL)
+constexpr double kMaskedDiagW = 0.59;  // per-a cost of a masked diagonal walk (PSX_K3_MASKW; 1.0 / 1.3 measured worse, r04aa)
 
 int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_host, std::vector<PlanUnit>& mine,
                  int& ca, double& sets, double& configs, double& bytes) {
@@ -346,6 +347,13 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
         const char* e = std::getenv("PSX_K3_DIAG_DIV");
         return e && std::atoi(e) > 0 ? std::atoi(e) : 1;
     }();
+    // per-a cost of a diagonal walk that runs the masked (unpipelined) step loop —
+    // a inside the block, or block 0 holding padding — relative to an
+    // off-diagonal walk (PSX_K3_MASKW); the pipelined folded walk costs 0.59
+    static const double maskw = [] {
+        const char* e = std::getenv("PSX_K3_MASKW");
+        return e && std::atof(e) > 0 ? std::atof(e) : kMaskedDiagW;
+    }();
     const double kTarget = rounds * (4.0 * PSX_K3_WAVES * kPlanCUs);
     ca = (int)std::lround(total_a / (kTarget * world));
     ca = std::min(ca, kMaxChunkA3);  // (caps 6 / 8 with the tail split: +0.4 / +1.5 % at world 1, r04w)
@@ -360,6 +368,9 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // so off-diagonal tiles only see a < 64K (every lane active every step) and
     // the triangular pair structure only occurs in diagonal tiles, which walk
     // it folded (psx_sweep3.hip): no in-block masking waste.
+    auto a_work = [&](int K, int C, int a) {
+        return K < C ? 1.0 : ((a >= 64 * K && a < 64 * K + 64) || 64 * K < pad) ? maskw : 0.59;
+    };
     std::vector<PlanUnit> all;
     for (int C = 0; C < nblk; C++) {
         if (64 * C + 64 <= pad) continue;
@@ -372,7 +383,11 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
                 // per-a part; a diagonal tile's folded walk has half the steps.
                 // Fitted to unit durations (tools/unit_trace.py, MI355X):
                 // off-diagonal 3.3 + 81.8 ca us, diagonal 3.0 + 48.4 ca us.
-                all.push_back({a0, a1, K, C, 0.04 + (double)(a1 - a0) * (K == C ? 0.59 : 1.0)});
+                // (the diagonal walks of a inside the block, and every walk of block 0
+                // when it holds padding, take the masked step loop: maskw per a)
+                double w = 0.04;
+                for (int a = a0; a < a1; a++) w += a_work(K, C, a);
+                all.push_back({a0, a1, K, C, w});
             }
         }
     }
@@ -450,12 +465,11 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
         std::vector<PlanUnit> tail;
         for (size_t i = cut; i < mine.size(); i++) {
             const PlanUnit& u = mine[i];
-            const double w1 = u.work / (u.a1 - u.a0);
             for (int a = u.a0; a < u.a1; a++) {
                 PlanUnit v = u;
                 v.a0 = a;
                 v.a1 = a + 1;
-                v.work = w1;
+                v.work = 0.04 + a_work(u.B, u.T, a);
                 tail.push_back(v);
             }
         }
