@@ -408,8 +408,8 @@ struct Sweep3FastSmem {
     double2 aAd[kMaxChunkA3], aY[kMaxChunkA3];  // the unit's a: A_aa, y_a (both studies), presence
     unsigned aP[kMaxChunkA3];
     int aPos[kMaxChunkA3];  // a record positions
-    double2 abG[64], abI[64], abIW[64], abH[64], abR[64], abMu[64], abMuB[64];
-    int2 abN[64];
+    double2 abG[64], abI[64], abIW[64], abH[64], abR[64];
+    double2 abMu[64], abMuB[64];  // the slot's {a, b} / {b} weights relative to 2^Ru_s (wave reference)
     float bW[64];  // membership weight of the slot's b (0, 1 or 3)
     double sW0[64], sW1[64], sW2[64], sSl[64], sNs[64];
     union {
@@ -782,6 +782,7 @@ __device__ __forceinline__ void sweep3_unit_robust(const Sweep3Args& A, int unit
 }
 
 constexpr int kMaxRefGap = 960;  // fast variant: largest n_abc - n_ac (bits, both studies) it accepts
+constexpr int kMaxSpread = 240;  // fast variant: largest Ru_s - R_s (bits, per study) within a wave
 
 // One k = 3 unit, FAST variant.  All of a lane's subset weights for one a are
 // taken relative to R_s = n_{ac} (the {a, c} exponent of study s, fixed for the
@@ -869,6 +870,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
 
     // c accumulator (shift mC), noCausal (shifts m0, m1), redo gap
     int mC = EMPTY, m0 = EMPTY, m1 = EMPTY, dmax = 0;
+    bool wide = false;  // some a's lanes spread more than kMaxSpread below the wave: redo
     double cW0 = 0.0, cW1 = 0.0, cW2 = 0.0, cSl = 0.0, cNs = 0.0;
     double nc0 = 0.0, nc1 = 0.0, npat = 0.0;
     const double2* g01 = A.g01 + (size_t)tile * 4096 + t;
@@ -1068,9 +1070,6 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         F.abIW[t] = make_double2(pIW[0], pIW[1]);
         F.abH[t] = make_double2(pH[0], pH[1]);
         F.abR[t] = make_double2(pR[0], pR[1]);
-        F.abMu[t] = make_double2(pMu[0], pMu[1]);
-        F.abMuB[t] = make_double2(pMuB[0], pMuB[1]);
-        F.abN[t] = make_int2(pN[0], pN[1]);
         const double wac = wc * memb_weight(pa);
         if (A.trace && ai == 0) t_fn[1] = wall_clock64();
         // this a's reference G: the a accumulator sits at it; c / noCausal / the b
@@ -1117,8 +1116,6 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             m0 = M0;
             m1 = M1;
         }
-        // round-to-nearest magic offset by R: N = round(256 (h3 - R)), so n3 - R = N >> 8
-        const double cmag[2] = {kMagic - 256.0 * R[0], kMagic - 256.0 * R[1]};
         // the walk's split constants as opaque registers (split3r)
         double k256 = 256.0, kc3 = kC3, kc2 = kC2;
         if (!SEP) kc2 = F.kc2;  // (re-read per a: not live across the walk)
@@ -1130,11 +1127,26 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         if (sep) {
             wave_max_k(mx);
         } else {
-            int g2[2] = {G, rG};
-            wave_max_k(g2);
-            mx[0] = g2[0];
-            mx[1] = g2[1];
+            int g4[4] = {G, rG, R[0], R[1]};
+            wave_max_k(g4);
+#pragma unroll
+            for (int i = 0; i < 4; i++) mx[i] = g4[i];
         }
+        // The walk's b-weights are taken relative to the wave's largest R_s (Ru_s)
+        // instead of the lane's own: the {b} / {a, b} weights of a slot are then
+        // one value for every lane (scaled here, once per a, instead of per step
+        // and lane), and each lane's factor lam_s = 2^(Ru_s - R_s) folds into the
+        // lane vectors it meets (uW, uL, the slot scale) and into the walk sums
+        // after the walk.  A lane more than kMaxSpread below the wave in a study
+        // would lose its low terms to underflow: the unit is redone (robust).
+        const int Ru[2] = {mx[2], mx[3]};
+        const int sp0 = Ru[0] - R[0], sp1 = Ru[1] - R[1];
+        wide |= __builtin_amdgcn_ballot_w64(max(sp0, sp1) > kMaxSpread) != 0;
+        const double lam0 = ldexp(1.0, min(sp0, kMaxSpread)), lam1 = ldexp(1.0, min(sp1, kMaxSpread));
+        F.abMuB[t] = make_double2(ldexp(pMuB[0], pN[0] - Ru[0]), ldexp(pMuB[1], pN[1] - Ru[1]));
+        F.abMu[t] = make_double2(ldexp(pMu[0], pN[0] - Ru[0]), ldexp(pMu[1], pN[1] - Ru[1]));
+        // round-to-nearest magic offset by Ru: N = round(256 (h3 - Ru)), so n3 - Ru = N >> 8
+        const double cmag[2] = {kMagic - 256.0 * Ru[0], kMagic - 256.0 * Ru[1]};
         // the previous a's record: its sums at the wave's largest shift
         const int rGw = mx[1], rdg = rG != EMPTY ? rG - rGw : -2000;
         double abS[2] = {0.0, 0.0};  // sum over the slots of the {a, b} weights, at 2^abM
@@ -1210,17 +1222,27 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         if (A.trace && ai == 0) t_fn[3] = wall_clock64();
         // the slot scale rides in the prior-weighted vectors (only the b-slot dot
         // products use them from here on; a power of two, so exact above underflow)
+        // (uW_s / uL_s meet study 1 - s's b-weights: lam_(1 - s); the {b, c} x
+        // {a, b, c} products carry lam_0 lam_1 with the slot scale, fSz)
+        const double fW[2] = {fS * lam1, fS * lam0};
+        const double fSz = fS * (lam0 * lam1);
 #pragma unroll
         for (int s = 0; s < 2; s++)
 #pragma unroll
-            for (int i = 0; i < 4; i++) uW[s][i] *= fS;
+            for (int i = 0; i < 4; i++) uW[s][i] *= fW[s];
         // SEP: so does the notSharedLL vector (its whole-value check is on the slot
         // totals), the {b, c} / {a, b, c} entries the walk uses
         if (sep) {
 #pragma unroll
             for (int s = 0; s < 2; s++)
 #pragma unroll
-                for (int i = 2; i < 4; i++) uL[s][i] *= fS;
+                for (int i = 2; i < 4; i++) uL[s][i] *= fW[s];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                uL[0][i] *= lam1;
+                uL[1][i] *= lam0;
+            }
         }
         wave_lds_order();  // (a, b) terms and slot shifts visible
         if (nxt) {
@@ -1241,6 +1263,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         // overlaps the wide fold of the previous one; the Sigma~ tile row is
         // fetched two steps ahead, the {b, c} weights one.
         bool tiny = false;
+        int dA = -(1 << 20);  // largest n_abc - Ru over the walk (both studies)
         auto chain = [&](int j, double2 g, int (&N)[2], double (&q)[2]) {
             const int bs = (t + j) & 63;
             const double2 aG = F.abG[bs], aI = F.abI[bs], aIW = F.abIW[bs], aH = F.abH[bs], aR = F.abR[bs];
@@ -1267,36 +1290,33 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         // finish(j)'s LDS operands: its slot's {b} / {a, b} terms and scale, and the
         // exp2 table entries of the chain's split (read as soon as the chain ends)
         struct FTt {
-            double2 muB, mu;
-            int2 n;
+            double2 muB, mu;  // the slot's {b} / {a, b} weights relative to 2^Ru_s
             double tb0, tb1;
         };
         auto ld_ft = [&](int j, const int (&N)[2]) {
             const int bs = (t + j) & 63;
-            return FTt{F.abMuB[bs], F.abMu[bs], F.abN[bs], tab[N[0] & 255], tab[N[1] & 255]};
+            return FTt{F.abMuB[bs], F.abMu[bs], tab[N[0] & 255], tab[N[1] & 255]};
         };
         auto finish_ft = [&](int j, const FTt& ft, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
             constexpr bool sepc = SEP;
             const int bs = (t + j) & 63;
             const double2 aMuB = ft.muB, aMu = ft.mu;
-            const int2 aN = ft.n;
-            // v[s][A] = E_s[A + b] relative to 2^{R_s}: {b}, {a, b}, {b, c}, {a, b, c}
+            // v[s][A] = E_s[A + b] relative to 2^{Ru_s}: {b}, {a, b}, {b, c}, {a, b, c}
             double v[2][4];
             int d3s = 0;
 #pragma unroll
             for (int s = 0; s < 2; s++) {
-                const int d3 = N[s] >> 8;  // n3 - R (N is R-relative)
+                const int d3 = N[s] >> 8;  // n3 - Ru (N is Ru-relative)
                 const double mu3 = (s ? ft.tb1 : ft.tb0) * q[s];
                 const int n2 = s ? ncur.y : ncur.x;
                 const double mu2 = s ? mcur.y : mcur.x;
-                const int dab = (s ? aN.y : aN.x) - R[s];
                 d3s += d3;
-                v[s][0] = ldexp(s ? aMuB.y : aMuB.x, dab);
-                v[s][1] = ldexp(s ? aMu.y : aMu.x, dab);
-                v[s][2] = ldexp(mu2, n2 - R[s]);
+                v[s][0] = s ? aMuB.y : aMuB.x;
+                v[s][1] = s ? aMu.y : aMu.x;
+                v[s][2] = ldexp(mu2, n2 - Ru[s]);
                 v[s][3] = ldexp(mu3, d3);
             }
-            dmax = max(dmax, d3s);
+            dA = max(dA, d3s);
             auto dot4 = [](const double (&u)[4], const double (&x)[4], double acc0) {
                 return fma(u[3], x[3], fma(u[2], x[2], fma(u[1], x[1], fma(u[0], x[0], acc0))));
             };
@@ -1337,8 +1357,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             // wave's LDS instructions execute in issue order (deterministic)
             __hip_atomic_fetch_add(&sW0[bs], WB0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&sW1[bs], WB1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&sW2[bs], WB2 * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&sSl[bs], LB2 * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&sW2[bs], WB2 * fSz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&sSl[bs], LB2 * fSz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&sNs[bs], sepc ? NB : NB * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (!ALLPRES) npat += wac * bW[bs];
         };
@@ -1436,6 +1456,25 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             __builtin_amdgcn_wave_barrier();
         }
         if (A.trace && ai == 0) t_ph[2] = wall_clock64();
+        // the walk sums back to the lane's own R_s (and n_abc - R for the redo test);
+        // the lane factors are recomputed here from R_s (not held across the walk)
+        {
+            int ru0 = Ru[0], ru1 = Ru[1];
+            asm volatile("" : "+s"(ru0), "+s"(ru1));
+            const int q0 = ru0 - R[0], q1 = ru1 - R[1];
+            dmax = max(dmax, dA + q0 + q1);
+            const double m0f = ldexp(1.0, min(q0, kMaxSpread)), m1f = ldexp(1.0, min(q1, kMaxSpread));
+#pragma unroll
+            for (int i = sep ? 3 : 0; i < 4; i++) {
+                V0[i] *= m0f;
+                V1[i] *= m1f;
+            }
+            const double l01 = m0f * m1f;
+#pragma unroll
+            for (int xa = 0; xa < 3; xa++)
+#pragma unroll
+                for (int xc = 0; xc < 3; xc++) ZS[xa][xc] *= l01;
+        }
         nact += je - j0;
         if (ALLPRES) npat += 27.0 * nact;
         if (sep) {
@@ -1485,7 +1524,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         // noCausal[s]: every member in the other study only
         nc0 = fma(V1[3], f0, nc0);
         nc1 = fma(V0[3], f1, nc1);
-        if (__builtin_amdgcn_ballot_w64(tiny))
+        if (!wide && __builtin_amdgcn_ballot_w64(tiny))  // (a wide unit is redone: its values are void)
             if (tiny) atomicOr(flag, 1);
         if (A.trace && ai == 0) t_fn[4] = wall_clock64();
         {
@@ -1519,7 +1558,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             // fast path's floor: at or above 2^-900 of the slot shift, every term lost
             // to underflow (< 2^-1074 each) is below 2^-174 of it; below, exact rerun
             const bool low = okb && sNs[t] < kTinyNs;
-            if (__builtin_amdgcn_ballot_w64(low))
+            if (!wide && __builtin_amdgcn_ballot_w64(low))
                 if (low) atomicOr(flag, 1);
         }
         if (diag) fold_acc(rc, rb);
@@ -1565,7 +1604,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         sr.npat = x4[3];
     }
     if (t == 0) store_rec(srec + unit, sr);
-    redo = __builtin_amdgcn_ballot_w64(dmax > kMaxRefGap) != 0;
+    redo = wide || __builtin_amdgcn_ballot_w64(dmax > kMaxRefGap) != 0;
     if (A.trace && t == 0) {
         unsigned hw, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
