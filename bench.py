@@ -514,7 +514,7 @@ def example_wall():
     return (wall if r.returncode == 0 else None), same, phases
 
 
-KERNEL_SOURCES = ("psx_sweep3.hip", "psx_sweep_dev.h", "psx_sweep_unit.h", "psx_math.h", "psx_sweep.h")
+KERNEL_SOURCES = ("psx_sweep3.hip", "psx_wave.h", "psx_sweep_dev.h", "psx_sweep_unit.h", "psx_math.h", "psx_sweep.h")
 
 
 def kernel_src_sha():

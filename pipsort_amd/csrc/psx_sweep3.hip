@@ -45,6 +45,7 @@
 #include "psx_sweep.h"
 #include "psx_sweep_dev.h"
 #include "psx_sweep_unit.h"
+#include "psx_wave.h"
 
 // device-library wave reductions (DPP, result in every lane)
 extern "C" __device__ __attribute__((const)) int __ockl_wfred_max_i32(int);
@@ -99,83 +100,6 @@ __device__ __forceinline__ void wave_fold_set_dpp(SetRec& r) {
     r.npat = __ockl_wfred_add_f64(r.npat);
 }
 
-// Batched wave reductions: K independent values reduced together, so the K
-// dependency chains interleave (one chain of DPP steps is ~100 cycles of
-// latency; eight of them back to back were ~1.8 us of the a prologue at two
-// waves per SIMD, tools/unit_trace.py).  Within each row of 16 lanes four
-// row_shr steps leave the row's sum / max in its lane 15; row_bcast:15 (into
-// rows 1 and 3) and row_bcast:31 (into rows 2 and 3) then carry the rows into
-// lane 63, whose value (a fixed summation order) is read as a uniform.  Every
-// lane must be active.
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double x) {  // lanes without a source read 0 (bound_ctrl)
-    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xf, 0xf, true);
-    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xf, 0xf, true);
-    return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double readlane_f64(double x, int lane) {
-    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), lane),
-                            __builtin_amdgcn_readlane(__double2loint(x), lane));
-}
-// (row_bcast:15 adds lane 16r - 1 into row r, row_bcast:31 lane 31 into rows 2
-// and 3; rows without a source add 0: lane 63 ends with (S3 + S2) + (S1 + S0))
-template <int K>
-__device__ __forceinline__ void wave_sum_k(double (&v)[K]) {
-#pragma unroll
-    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x111>(v[k]);  // row_shr:1
-#pragma unroll
-    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x112>(v[k]);  // row_shr:2
-#pragma unroll
-    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x114>(v[k]);  // row_shr:4
-#pragma unroll
-    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x118>(v[k]);  // row_shr:8
-#pragma unroll
-    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x142>(v[k]);  // row_bcast:15
-#pragma unroll
-    for (int k = 0; k < K; k++) v[k] += dpp_f64<0x143>(v[k]);  // row_bcast:31
-#pragma unroll
-    for (int k = 0; k < K; k++) v[k] = readlane_f64(v[k], 63);
-}
-// maxima of values >= EMPTY, reduced as x - EMPTY >= 0 so that a lane without a
-// DPP source (reading 0) is neutral
-template <int CTRL>
-__device__ __forceinline__ int dpp_max_b(int y) {
-    return max(y, __builtin_amdgcn_mov_dpp(y, CTRL, 0xf, 0xf, true));
-}
-template <int K>
-__device__ __forceinline__ void wave_max_k(int (&v)[K]) {
-    int y[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) y[k] = v[k] - EMPTY;
-#pragma unroll
-    for (int k = 0; k < K; k++) y[k] = dpp_max_b<0x111>(y[k]);
-#pragma unroll
-    for (int k = 0; k < K; k++) y[k] = dpp_max_b<0x112>(y[k]);
-#pragma unroll
-    for (int k = 0; k < K; k++) y[k] = dpp_max_b<0x114>(y[k]);
-#pragma unroll
-    for (int k = 0; k < K; k++) y[k] = dpp_max_b<0x118>(y[k]);
-#pragma unroll
-    for (int k = 0; k < K; k++) y[k] = dpp_max_b<0x142>(y[k]);
-#pragma unroll
-    for (int k = 0; k < K; k++) y[k] = dpp_max_b<0x143>(y[k]);
-#pragma unroll
-    for (int k = 0; k < K; k++) v[k] = __builtin_amdgcn_readlane(y[k], 63) + EMPTY;
-}
-
-// K (shift, sum) pairs at once, as wave_pair_dpp
-template <int K>
-__device__ __forceinline__ void wave_pair_k(int (&m)[K], double (&x)[K]) {
-    int M[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) M[k] = x[k] != 0.0 ? m[k] : EMPTY;
-    wave_max_k(M);
-#pragma unroll
-    for (int k = 0; k < K; k++) x[k] = x[k] != 0.0 ? ldexp(x[k], m[k] - M[k]) : 0.0;
-    wave_sum_k(x);
-#pragma unroll
-    for (int k = 0; k < K; k++) m[k] = x[k] != 0.0 ? M[k] : EMPTY;
-}
 
 // Order LDS accesses across the lanes of a ONE-wave workgroup: a wave's LDS
 // instructions execute in issue order, so program order suffices.  __syncthreads
@@ -1123,12 +1047,12 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         // this a's wave maxima in one batch: G (the slot shift) and, for the closed
         // forms of off-diagonal units, R_s and the slots' {a, b} exponents
         // (and the previous a's record shift)
-        int mx[6] = {G, rG, R[0], R[1], pMu[0] != 0.0 ? pN[0] : EMPTY, pMu[1] != 0.0 ? pN[1] : EMPTY};
+        int mx[8] = {G, rG, R[0], R[1], pMu[0] != 0.0 ? pN[0] : EMPTY, pMu[1] != 0.0 ? pN[1] : EMPTY, EMPTY, EMPTY};
         if (sep) {
-            wave_max_k(mx);
+            wave_max_t(mx);
         } else {
             int g4[4] = {G, rG, R[0], R[1]};
-            wave_max_k(g4);
+            wave_max_t(g4);
 #pragma unroll
             for (int i = 0; i < 4; i++) mx[i] = g4[i];
         }
@@ -1174,7 +1098,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             // (likewise the plain one-study sums of notSharedLL, uL: uL_s[0] = uW_s[0])
             // (and the walk sum of the {a, b} weights over the slots, V_s[1]: one batch)
             const int Qm[2] = {mx[2], mx[3]};
-            double ws[13];
+            double ws[16];
+            ws[13] = ws[14] = ws[15] = 0.0;  // (batch padded to a multiple of 4)
 #pragma unroll
             for (int s = 0; s < 2; s++) {
                 ws[2 * s] = ldexp(uW[s][0], R[s] - Qm[s]);
@@ -1184,7 +1109,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             }
 #pragma unroll
             for (int i = 0; i < 5; i++) ws[8 + i] = ldexp(rW[i], rdg);
-            wave_sum_k(ws);
+            wave_sum_t(ws);
             const double QW[2][2] = {{ws[0], ws[1]}, {ws[2], ws[3]}}, QL[2] = {ws[4], ws[5]};
 #pragma unroll
             for (int s = 0; s < 2; s++) {
@@ -1211,10 +1136,10 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             sSl[t] += z0;
         }
         if (!sep) {
-            double r5[5];
+            double r5[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int i = 0; i < 5; i++) r5[i] = ldexp(rW[i], rdg);
-            wave_sum_k(r5);
+            wave_sum_t(r5);
 #pragma unroll
             for (int i = 0; i < 5; i++) rW[i] = r5[i];
         }
@@ -1585,15 +1510,15 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
 #pragma unroll
         for (int k = 0; k < 3; k++) M3[k] = x3[k] != 0.0 ? m3[k] : EMPTY;
         M3[3] = rG;
-        wave_max_k(M3);
+        wave_max_t(M3);
         const int rdg = rG != EMPTY ? rG - M3[3] : -2000;
-        double x4[9];
+        double x4[12] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int k = 0; k < 3; k++) x4[k] = x3[k] != 0.0 ? ldexp(x3[k], m3[k] - M3[k]) : 0.0;
         x4[3] = sr.npat;
 #pragma unroll
         for (int i = 0; i < 5; i++) x4[4 + i] = ldexp(rW[i], rdg);
-        wave_sum_k(x4);
+        wave_sum_t(x4);
         if (t == 0 && rq >= 0) store_rec(rec + rq, wrec(M3[3], x4[4], x4[5], x4[6], x4[7], x4[8], rho, A.Ck, A.pit0));
         sr.tot = x4[0];
         sr.m = x4[0] != 0.0 ? M3[0] : EMPTY;
