@@ -313,7 +313,9 @@ int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* 
 // a over [a0, a1) with a < b.  Exact per-shard set / configuration / byte counts
 // in O(64 * 9) per unit from per-class prefix counts over v.
 constexpr double kTailFrac = 0.05;  // share of a shard's work cut into single-a units at the end (PSX_K3_TAIL)
-constexpr double kMaskedDiagW = 0.59;  // per-a cost of a masked diagonal walk (PSX_K3_MASKW; 1.0 / 1.3 measured worse, r04aa)
+constexpr double kDiagW = 0.65;   // per-a cost of a pipelined diagonal walk (PSX_K3_DIAGW; 0.59 before r04ae)
+constexpr double kUnitW = 0.04;   // fixed cost of a unit (PSX_K3_UNITW)
+constexpr double kMaskedDiagW = 0.65;  // per-a cost of a masked diagonal walk (PSX_K3_MASKW; 1.0 / 1.3 worse, r04aa; 0.65 with DIAGW 0.65 balances world 8 best, r04ae)
 
 int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_host, std::vector<PlanUnit>& mine,
                  int& ca, double& sets, double& configs, double& bytes) {
@@ -349,10 +351,20 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     }();
     // per-a cost of a diagonal walk that runs the masked (unpipelined) step loop —
     // a inside the block, or block 0 holding padding — relative to an
-    // off-diagonal walk (PSX_K3_MASKW); the pipelined folded walk costs 0.59
+    // off-diagonal walk (PSX_K3_MASKW)
     static const double maskw = [] {
         const char* e = std::getenv("PSX_K3_MASKW");
         return e && std::atof(e) > 0 ? std::atof(e) : kMaskedDiagW;
+    }();
+    // per-a cost of a pipelined (folded) diagonal walk and the fixed cost of a
+    // unit, in off-diagonal a-walks (PSX_K3_DIAGW, PSX_K3_UNITW)
+    static const double diagw = [] {
+        const char* e = std::getenv("PSX_K3_DIAGW");
+        return e && std::atof(e) > 0 ? std::atof(e) : kDiagW;
+    }();
+    static const double unitw = [] {
+        const char* e = std::getenv("PSX_K3_UNITW");
+        return e && std::atof(e) >= 0 ? std::atof(e) : kUnitW;
     }();
     const double kTarget = rounds * (4.0 * PSX_K3_WAVES * kPlanCUs);
     ca = (int)std::lround(total_a / (kTarget * world));
@@ -369,7 +381,7 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // the triangular pair structure only occurs in diagonal tiles, which walk
     // it folded (psx_sweep3.hip): no in-block masking waste.
     auto a_work = [&](int K, int C, int a) {
-        return K < C ? 1.0 : ((a >= 64 * K && a < 64 * K + 64) || 64 * K < pad) ? maskw : 0.59;
+        return K < C ? 1.0 : ((a >= 64 * K && a < 64 * K + 64) || 64 * K < pad) ? maskw : diagw;
     };
     std::vector<PlanUnit> all;
     for (int C = 0; C < nblk; C++) {
@@ -380,12 +392,13 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
             for (int a0 = pad; a0 < amax; a0 += cu) {
                 const int a1 = std::min(a0 + cu, amax);
                 // unit cost in off-diagonal-a units: a fixed per-unit part and a
-                // per-a part; a diagonal tile's folded walk has half the steps.
-                // Fitted to unit durations (tools/unit_trace.py, MI355X):
-                // off-diagonal 3.3 + 81.8 ca us, diagonal 3.0 + 48.4 ca us.
+                // per-a part; a diagonal tile's folded walk has half the steps (first
+                // fitted to unit durations, tools/unit_trace.py: off-diagonal 3.3 +
+                // 81.8 ca us, diagonal 3.0 + 48.4 ca us; the diagonal weight then
+                // raised to 0.65 where it balanced the world-8 shards best, r04ae).
                 // (the diagonal walks of a inside the block, and every walk of block 0
                 // when it holds padding, take the masked step loop: maskw per a)
-                double w = 0.04;
+                double w = unitw;
                 for (int a = a0; a < a1; a++) w += a_work(K, C, a);
                 all.push_back({a0, a1, K, C, w});
             }
@@ -469,7 +482,7 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
                 PlanUnit v = u;
                 v.a0 = a;
                 v.a1 = a + 1;
-                v.work = 0.04 + a_work(u.B, u.T, a);
+                v.work = unitw + a_work(u.B, u.T, a);
                 tail.push_back(v);
             }
         }
