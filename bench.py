@@ -713,7 +713,7 @@ def main():
                          + (f" / {world} (this rank's shard)" if world > 1 else ""))
         else:
             flops = tm["flops"]
-            flops_src = ("model: 132 FP64 operations per 3-SNP union set (fitted to the PMC count of the last "
+            flops_src = ("model: 131 FP64 operations per 3-SNP union set (fitted to the PMC count of the last "
                          "collected build, a lower bound for later ones) - NOT counters of this build")
         achieved = flops / avg_kernel_s / 1e12 if avg_kernel_s > 0 else 0.0
         # the roofline fraction is reported only from counters of this very build;

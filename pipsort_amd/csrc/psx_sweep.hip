@@ -555,10 +555,10 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     // FP64 operations per union set (FMA = 2), fitted to the PMC FP64 counts of
     // the k = 3 fast kernel (64 x SQ_INSTS_VALU_FLOPS_FP64 / sets: 281 before the
     // deferred fold, 159 after it (r02zd), 141.8 in r03zb, 139.2 in r04h, 132.5 in
-    // r04t): kept at or below the last count, so a bench line without PMC
+    // r04t, 131.8 in r04ag): kept at or below the last count, so a bench line without PMC
     // counters of its own build cannot overstate the FP64 rate; k = 2 by the
     // round-1 ratio of VALU work per set.  bench.py reports it only as a model.
-    P.flops = sets * (k == 3 ? 132.0 : 110.0);
+    P.flops = sets * (k == 3 ? 131.0 : 110.0);
     const int pad = variant ? ldg - U : 0;  // record keys of variant 1 are in v space
     // device buffers
     std::vector<int4> hu(P.n_units);
