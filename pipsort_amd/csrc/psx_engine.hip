@@ -576,19 +576,41 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_pass_l1(DevProb P, int 
     const int b0 = dptrB ? dptrB[u] : 0, nb = dptrB ? dptrB[u + 1] - b0 : 0;
     const int n = na + nb;
     Acc5 a = psx::acc_zero();
-    int i = tid;
-    for (; i + 3 * T < n; i += 4 * T) {  // four independent loads in flight per lane
-        Acc5 x[4];
+    // Eight records in flight per lane, their gather indices loaded one round
+    // ahead: a merge wave holds a wave slot of the next sweep for its lifetime
+    // (one-wave sweep blocks fill every SIMD), and its lifetime is load rounds x
+    // latency — the gathered loads of the old four-deep loop (index, then record)
+    // cost the sweep beside it ~3 % at world 1 and ~5 % at world 8 (r04ai).  Each
+    // lane folds its records in record order, as before.
+#ifndef PSX_MERGE_DEPTH
+#define PSX_MERGE_DEPTH 8
+#endif
+    constexpr int D = PSX_MERGE_DEPTH;
+    auto gidx_of = [&](int j) {
+        return j < na ? (gidxA ? gidxA[a0 + j] : a0 + j) : (gidxB ? gidxB[b0 + j - na] : b0 + j - na);
+    };
+    int g[D];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < D; q++) {
+        const int j = tid + q * T;
+        g[q] = j < n ? gidx_of(j) : 0;
+    }
+    for (int i = tid; i < n; i += D * T) {
+        Acc5 x[D];
+#pragma unroll
+        for (int q = 0; q < D; q++) {
             const int j = i + q * T;
-            x[q] = j < na ? recA[gidxA ? gidxA[a0 + j] : a0 + j] : recB[gidxB ? gidxB[b0 + j - na] : b0 + j - na];
+            if (j < n) x[q] = j < na ? recA[g[q]] : recB[g[q]];
         }
 #pragma unroll
-        for (int q = 0; q < 4; q++) psx::fold_acc(a, x[q]);
+        for (int q = 0; q < D; q++) {
+            const int j = i + (D + q) * T;
+            g[q] = j < n ? gidx_of(j) : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < D; q++)
+            if (i + q * T < n) psx::fold_acc(a, x[q]);
     }
-    for (; i < n; i += T)
-        psx::fold_acc(a, i < na ? recA[gidxA ? gidxA[a0 + i] : a0 + i] : recB[gidxB ? gidxB[b0 + i - na] : b0 + i - na]);
     psx::wave_fold_acc(a);
     if (tid == 0) {
         Acc5 g = {0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -1255,6 +1277,10 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     const SetRec extra = e->rank == 0 ? null_rec(e, 1.0) : psx::set_zero();
     psx::SweepPlan* mA = low ? low : top;
     psx::SweepPlan* mB = low ? top : nullptr;
+    // (PSX_ABLATE_MERGE=1: timing ablation only — the pass's merge is skipped and
+    // its results are wrong; measures what the merge beside the next sweep costs)
+    static const bool ablate_merge = std::getenv("PSX_ABLATE_MERGE") != nullptr;
+    if (!ablate_merge)
     hipLaunchKernelGGL(k_merge_pass_l1, dim3(e->U + 1), dim3(kMergeThreads), 0, X, e->dp, lo, hi, psx::plan_records(*mA, par),
                        mA->d_dptr, mA->d_gidx, mB ? psx::plan_records(*mB, par) : nullptr, mB ? mB->d_dptr : nullptr,
                        mB ? mB->d_gidx : nullptr, dpass,
