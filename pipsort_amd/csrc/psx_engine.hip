@@ -528,8 +528,15 @@ __device__ void eval_single(const DevProb& P, int u, Acc5& a, SetRec& r) {
 // slot any sweep block frees (a wider block waits for several free slots on
 // one CU at once and was starved for the whole sweep).
 // Fixed fold order: deterministic.
+// (PSX_MERGE_WAVES, A/B: one item per wave, several waves per block — a block
+// then needs that many free wave slots on one CU, which the sweep beside it
+// leaves only in its drain)
+#ifndef PSX_MERGE_WAVES
+#define PSX_MERGE_WAVES 1
+#endif
 constexpr int kMergeThreads = 64;
-__global__ __launch_bounds__(kMergeThreads) void k_merge_pass_l1(DevProb P, int lo, int hi, const Acc5* __restrict__ recA,
+constexpr int kMergeWaves = PSX_MERGE_WAVES;
+__global__ __launch_bounds__(kMergeThreads * kMergeWaves) void k_merge_pass_l1(DevProb P, int lo, int hi, const Acc5* __restrict__ recA,
                                                        const int* __restrict__ dptrA, const int* __restrict__ gidxA,
                                                        const Acc5* __restrict__ recB, const int* __restrict__ dptrB,
                                                        const int* __restrict__ gidxB, const SetRec* __restrict__ srec,
@@ -537,8 +544,9 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_pass_l1(DevProb P, int 
                                                        SetRec* __restrict__ sacc, int* __restrict__ flag,
                                                        int* __restrict__ sticky) {
     constexpr int T = kMergeThreads;
-    const int tid = threadIdx.x;
-    if (blockIdx.x == 0) {
+    const int tid = threadIdx.x & 63;
+    const int item = blockIdx.x * kMergeWaves + (threadIdx.x >> 6);
+    if (item == 0) {
         SetRec a = psx::set_zero();
         for (int u = lo + tid; u < hi; u += T) {
             Acc5 dummy;
@@ -570,7 +578,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_pass_l1(DevProb P, int 
         }
         return;
     }
-    const int u = blockIdx.x - 1;
+    const int u = item - 1;
     if (u >= P.U) return;
     const int a0 = dptrA ? dptrA[u] : 0, na = dptrA ? dptrA[u + 1] - a0 : 0;
     const int b0 = dptrB ? dptrB[u] : 0, nb = dptrB ? dptrB[u + 1] - b0 : 0;
@@ -1281,7 +1289,7 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     // its results are wrong; measures what the merge beside the next sweep costs)
     static const bool ablate_merge = std::getenv("PSX_ABLATE_MERGE") != nullptr;
     if (!ablate_merge)
-    hipLaunchKernelGGL(k_merge_pass_l1, dim3(e->U + 1), dim3(kMergeThreads), 0, X, e->dp, lo, hi, psx::plan_records(*mA, par),
+    hipLaunchKernelGGL(k_merge_pass_l1, dim3((e->U + 1 + kMergeWaves - 1) / kMergeWaves), dim3(kMergeThreads * kMergeWaves), 0, X, e->dp, lo, hi, psx::plan_records(*mA, par),
                        mA->d_dptr, mA->d_gidx, mB ? psx::plan_records(*mB, par) : nullptr, mB ? mB->d_dptr : nullptr,
                        mB ? mB->d_gidx : nullptr, dpass,
                        (long)(nl + nt), extra, e->dacc, e->dsacc, pflag, e->dflag + 1);
