@@ -514,6 +514,33 @@ def test_strong_signal_robust_units(gpu):
     pc.close()
 
 
+def test_wide_lane_spread_robust_units(gpu):
+    """A shared SNP with z ~ 20 in both studies: as the c of a wave it sits
+    ~290 bits above the other lanes' {a, c} exponents in each study — beyond
+    the fast variant's 240-bit spread under the wave's reference R (kMaxSpread),
+    within its 960-bit n_abc - n_ac window — so exactly those units take the
+    robust variant.  Parity with the oracle at 1e-9."""
+    M = 80
+    idx = np.arange(M)
+    ld, z = [], []
+    for s, rho in enumerate((0.5, 0.3)):
+        sig = rho ** np.abs(idx[:, None] - idx[None, :])
+        lam = np.zeros(M)
+        lam[70] = 20.0
+        lam[5] = 4.0 if s == 0 else 0.0
+        eps = np.random.default_rng(29 + s).standard_normal(M)
+        z.append(sig @ lam + np.linalg.cholesky(sig) @ eps)
+        ld.append(sig)
+    u2l = np.stack([idx, idx]).astype(np.int32)
+    seam = E.seam_from_arrays(ld, z, u2l, (12000, 9000), max_causal=3, sharing_param=0.3)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    t = pc.timing()
+    assert t["exact_rerun"] == 0 and t["robust_units"] > 0, t
+    assert_parity(pc.accum(), O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-10)
+    pc.close()
+
+
 def _cli_pair(tmp_path, src, args):
     d1, d2 = tmp_path / "engine", tmp_path / "oracle"
     shutil.copytree(os.path.join(loci.GOLDEN, src), d1)
