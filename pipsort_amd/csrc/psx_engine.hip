@@ -2225,7 +2225,7 @@ struct SssDev {
     size_t nmax = 0, nmax_full = 0;  // item capacity of the per-item arrays (full / hscore)
     // (start, stop) event pairs around the evals, read kRingE iterations later
     // (by then complete) instead of once per iteration
-    static constexpr int kRingE = 32;
+    static constexpr int kRingE = 8;
     hipEvent_t ev[2 * kRingE] = {};
     int* rows = nullptr;      // per item: its set (evaluated items)
     int* mark = nullptr;      // per neighbour: -1 seen, -2 unseen null, else its item
@@ -2312,7 +2312,9 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
     // the most items of an iteration: the current configuration + the largest
     // neighbourhood (k = C: swaps C (U - C), minus C; k < C: + U - k plus sets)
     const size_t nmax = (size_t)C * U + C + U + 2;
+    const auto tw = std::chrono::steady_clock::now();
     if ((rc = sss_workspace(e, nmax, world, e->stream))) return rc;
+    const double ws_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw).count();
     SssDev& D = *e->sss;
     if ((rc = ensure(e->dsrec, e->cap_srec, nmax))) return rc;
     if ((rc = ensure(e->dmrec, e->cap_mrec, nmax * stride))) return rc;
@@ -2500,8 +2502,8 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
     }
     if (prof)
         fprintf(stderr, "[psx sss] %d iterations, host us per iteration: launch %.1f, wait eval %.1f, sampling %.1f, "
-                "wait post %.1f\n", iter, ph[0] / std::max(iter, 1), ph[1] / std::max(iter, 1),
-                ph[2] / std::max(iter, 1), ph[3] / std::max(iter, 1));
+                "wait post %.1f; workspace %.0f us\n", iter, ph[0] / std::max(iter, 1), ph[1] / std::max(iter, 1),
+                ph[2] / std::max(iter, 1), ph[3] / std::max(iter, 1), ws_us);
     if (iterations_out) *iterations_out = iter;
     e->timing.sweep_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     e->timing.kernel_ms = kms;
