@@ -13,10 +13,14 @@ import re
 import subprocess
 import sys
 
+import os
+import shlex
+
 src, kre = sys.argv[1], sys.argv[2]
 rare = set(sys.argv[sys.argv.index("--rare") + 1:]) if "--rare" in sys.argv else set()
+extra = shlex.split(os.environ.get("LOOPSTAT_FLAGS", ""))  # e.g. scheduler options of an A/B build
 subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-I",
-                "/root/repo/pipsort_amd/csrc", "--cuda-device-only", "-S", src, "-o", "/tmp/loopstat.s"],
+                "/root/repo/pipsort_amd/csrc", "--cuda-device-only", "-S", src, "-o", "/tmp/loopstat.s"] + extra,
                check=True, stderr=subprocess.DEVNULL)
 s = open("/tmp/loopstat.s").read()
 for name in re.findall(r"^(\S+):", s, re.M):
