@@ -458,20 +458,36 @@ def pcie_inclusive(mi, configs, device, reps=3):
     """Whole-locus rate from host buffers to host results: the GPU Model setup
     from the host LD / z arrays (H2D included), one synchronous exhaustive
     pass, and the accumulators read back to the host (psx_get_accum, D2H).
-    Not the bench value (inputs are not resident): reported beside it."""
+    Not the bench value (inputs are not resident): reported beside it, split
+    into phases (best repetition)."""
     best = None
     for _ in range(reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         pc = E.PostCal(mi, device=device)
+        t1 = time.perf_counter()
         pc.run_exhaustive()
+        t2 = time.perf_counter()
         pc.accum()
-        dt = time.perf_counter() - t0
-        setup_ms = pc.setup_info["setup_ms"]
+        t3 = time.perf_counter()
+        dt = t3 - t0
+        si = pc.setup_info
+        tm = pc.timing()
+        ph = {"create_ms": (t1 - t0) * 1e3,
+              "setup_ms": si["setup_ms"],
+              "setup_alloc_ms": si.get("alloc_ms"), "setup_studies_ms": si.get("studies_ms"),
+              "setup_tail_ms": si.get("tail_ms"),
+              "study_upload_ms": si.get("study_upload_ms"), "study_psd_lu_ms": si.get("study_psd_ms"),
+              "study_finish_ms": si.get("study_finish_ms"),
+              "first_pass_ms": (t2 - t1) * 1e3,
+              "pass_prepare_ms": tm.get("prepare_ms"),
+              "pass_kernel_ms": tm.get("kernel_ms"),
+              "readback_ms": (t3 - t2) * 1e3}
         pc.close()
         if best is None or dt < best[0]:
-            best = (dt, setup_ms)
-    return {"value": configs / best[0], "unit": "configs/s", "s": best[0], "setup_ms": best[1],
+            best = (dt, ph)
+    return {"value": configs / best[0], "unit": "configs/s", "s": best[0], "setup_ms": best[1]["setup_ms"],
+            "phases": best[1],
             "note": "host LD/z -> GPU Model setup (H2D) -> one synchronous pass -> accumulators on the host "
                     "(D2H); best of %d" % reps}
 
@@ -575,6 +591,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     args = ap.parse_args()
+    # integrity: a timing-ablation switch (results wrong) never produces a line
+    ablate = sorted(k for k in os.environ if k.startswith("PSX_ABLATE"))
+    if ablate:
+        print(f"bench: refusing to run with timing-ablation variables set: {ablate}", file=sys.stderr)
+        sys.exit(3)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
     # the bench line must be the only thing on stdout: native libraries print
@@ -614,6 +635,15 @@ def main():
     configs_per_step = seam.count_configs()
     pc = E.PostCal(seam, device=local)  # Model setup + PostCal construction on the GPU
     pc.set_shard(rank, world)
+    plan_hash = pc.plan_hash()
+    if use_dist:
+        # every rank must cut the same shard plan (PSX_K3_* knobs are read per
+        # process); the merge refuses mismatched images too, this fails early
+        hs = [None] * world
+        dist.all_gather_object(hs, plan_hash)
+        if len(set(hs)) != 1:
+            print(f"bench: ranks cut different shard plans: {hs}", file=sys.stderr)
+            sys.exit(4)
     # one stream for torch (collectives, copies) and the engine: the exchange is
     # ordered by the stream, no host synchronisation between export and merge
     stream = torch.cuda.Stream(priority=-1)  # high: merges + exchange ahead of the sweeps
@@ -690,6 +720,11 @@ def main():
             sss_line = sss_probe_sharded(rank, world, backend)
         except Exception as ex:  # noqa: BLE001
             sss_line = {"error": f"{type(ex).__name__}: {ex}"}
+    if rank == 0 and (acc is None or int(acc.n_configs) != configs_per_step):
+        # integrity: the merged accumulators must hold every configuration once
+        print(f"bench: configurations checked {None if acc is None else acc.n_configs} != "
+              f"{configs_per_step} per step; no line", file=sys.stderr)
+        sys.exit(5)
     if rank == 0:
         value = configs_per_step * args.steps / elapsed
         avg_kernel_s = (kms / max(launches, 1)) / 1e3
@@ -771,6 +806,9 @@ def main():
             "pass_mode": "async (no host sync per step)" if use_async else "synchronous",
             "span_ms_per_pass": tm.get("span_ms") if use_async else None,
             "configs_checked": int(acc.n_configs) if acc is not None else None,
+            "plan_hash": f"{plan_hash:016x}",
+            # every engine environment knob in force (plan shape, overlap, sync mode)
+            "env_knobs": {k: v for k, v in sorted(os.environ.items()) if k.startswith("PSX_")},
         }
         if use_dist:
             out["sss"] = sss_line

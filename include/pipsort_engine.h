@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define PSX_ABI_VERSION 2
+#define PSX_ABI_VERSION 3
 
 #define PSX_OK 0
 #define PSX_EINVAL (-1)    /* bad argument / unsupported problem shape        */
@@ -78,6 +78,9 @@ typedef struct {
     int32_t robust_units;   /* k = 3 units redone by the robust variant (cumulative since create) */
     double span_ms;         /* asynchronous passes: first sweep's start to the last one's end,
                                per pass (consecutive sweeps may overlap: kernel_ms double-counts) */
+    double prepare_ms;      /* psx_run_exhaustive: host wall of the plan / layout preparation
+                               (first pass of a handle: k = 3 layouts, unit plans, CSR upload) */
+    double run_ms;          /* psx_run_exhaustive: host wall of the whole call                */
 } psx_timing;
 
 int32_t psx_abi_version(void);
@@ -131,6 +134,12 @@ typedef struct {
     double min_pivot_ratio[2]; /* smallest L D L^T pivot / largest |diagonal|            */
     double setup_ms;           /* wall time of the whole setup + create                  */
     double spsq[2];            /* ||S'_s||^2 = z~^T D^-1 z~ (0 on the eigen route)       */
+    /* phases of setup_ms (wall, ms): device allocations, the two studies (run
+     * concurrently, one host thread and stream each), accumulators + plan tag */
+    double alloc_ms, studies_ms, tail_ms;
+    /* per study: LD upload (H2D), PSD shift loop (LU determinants), step 2 +
+     * readback, and (the rest of studies_ms) the union-coordinate layouts */
+    double study_upload_ms[2], study_psd_ms[2], study_finish_ms[2];
 } psx_setup_info;
 
 int psx_create_from_ld(const psx_ld_problem *prob, int device, psx_engine **out, psx_setup_info *info);
@@ -141,11 +150,26 @@ int psx_psd_shift_gpu(double *sigma, int32_t m, double *added, int device);
 /* One GSL-order partial-pivot LU determinant on the GPU (a row-major m x m, not
  * modified): bit-identical to the host psx_lu_det (pipsort_model.h). */
 int psx_lu_det_gpu(const double *a, int32_t m, int device, double *det);
+/* The setup's swap-free elimination (util.cpp:214-215's LU when no row swap
+ * is needed; the forward solve of z rides along, as the setup's step 2 uses
+ * it) on the GPU: a row-major m x m (not modified), z m entries or NULL.
+ * pivots <- U_ii (m), z_out <- L^-1 z (m, when z), *swap_needed <- 1 when
+ * check != 0 and GSL's pivot search would swap some row (pivots are then
+ * meaningless).  Bit-identical to the per-column elimination; for parity
+ * tests of the tiled kernels. */
+int psx_elim_gpu(const double *a, int32_t m, const double *z, int32_t check, double *pivots, double *z_out,
+                 int32_t *swap_needed, int device);
 
 /* Multi-GPU sharding of the exhaustive sweep (one process per GPU): this handle
  * evaluates shard `rank` of `world` equal slices of every causal-set level; the
  * null configuration belongs to rank 0.  Default (0, 1). */
 int psx_set_shard(psx_engine *e, int rank, int world);
+/* The shard plan's hash (locus shape, c, world and the plan knobs PSX_K3_*):
+ * every rank of one job must report the same value.  Each partial image
+ * carries it with the image's rank and world; psx_merge_partials /
+ * psx_fold_partials_host refuse images that are not shards 0..count-1 of one
+ * plan (an error from the merge, or from psx_sync after an enqueued merge). */
+int psx_plan_hash(psx_engine *e, uint64_t *hash);
 
 /* PostCal::computeTotalLikelihood (postcal.cpp:716-1092): exhaustive sweep over
  * all union subsets of size <= max_causal and all per-study assignments passing
@@ -224,7 +248,8 @@ int psx_merge_partials(psx_engine *e, const void *device_src, int32_t count);
 /* Host-only (no GPU needed): fold `count` partial images of `image_bytes`
  * bytes each (psx_export_partials layout, rank order) into one image at dst —
  * the same fold psx_merge_partials runs on the device, for partials gathered
- * through a host collective. */
+ * through a host collective.  PSX_EINVAL when the images' plan tags are not
+ * shards 0..count-1 of one plan. */
 int psx_fold_partials_host(const void *src, int32_t count, int64_t image_bytes, void *dst);
 
 /* Host-only: union subsets and configurations of causal-set level k (1..c)
@@ -232,6 +257,18 @@ int psx_fold_partials_host(const void *src, int32_t count, int64_t image_bytes, 
 int psx_shard_stats(const psx_problem *prob, int32_t k, int32_t rank, int32_t world, uint64_t *union_sets,
                     double *configs);
 
+/* Host-side diagnostics (no device): the host time of building level k's
+ * (2 or 3) unit plan and record CSR for shard rank of world, every union SNP
+ * in both studies; *n_units / *n_records the plan's size. */
+int psx_plan_build_ms(int32_t n_union, int32_t k, int32_t rank, int32_t world, double *ms, int32_t *n_units,
+                      int64_t *n_records);
+/* GPU self-check of a sweep plan's record CSR (built on the device, hipcub
+ * radix sort) against the host restatement: level k, shard rank of world,
+ * variant 1 = the k = 3 fast kernel's decomposition, presence bits per union
+ * SNP (NULL: every SNP in both studies).  *mismatches = differing entries of
+ * pos / dptr / gidx (0 expected), *records = records with a SNP. */
+int psx_plan_csr_selftest(int32_t n_union, const uint8_t *presence, int32_t k, int32_t rank, int32_t world,
+                          int32_t variant, int device, int64_t *mismatches, int64_t *records);
 /* Host-side diagnostics (no kernel runs): the k = 3 fast sweep's work units of
  * shard `rank` of `world` for a union of n_union SNPs present in both studies,
  * in dispatch order, as int4 {a0, a1, K | j0 << 16, C | j1 << 16} (v space; a

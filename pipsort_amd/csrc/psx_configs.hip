@@ -51,6 +51,7 @@
 #include "psx_configs.h"
 #include "psx_sweep.h"
 #include "psx_sweep_dev.h"
+#include "psx_mem.h"
 
 namespace psx {
 
@@ -417,7 +418,7 @@ constexpr size_t kStageChunk = 8u << 20;
 int upload_rows(CfgWork& W, const void* src, size_t bytes, void* dst, hipStream_t st) {
     if (bytes <= 2 * kStageChunk)
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st) == hipSuccess ? 0 : -1;
-    if (!W.hpin && hipHostMalloc(reinterpret_cast<void**>(&W.hpin), 2 * kStageChunk) != hipSuccess) return -1;
+    if (!W.hpin && psx::hmalloc(reinterpret_cast<void**>(&W.hpin), 2 * kStageChunk) != hipSuccess) return -1;
     for (int b = 0; b < 2; b++)
         if (!W.dma[b] && hipEventCreateWithFlags(&W.dma[b], hipEventDisableTiming) != hipSuccess) return -1;
     const size_t nch = (bytes + kStageChunk - 1) / kStageChunk;
@@ -463,11 +464,11 @@ int upload_rows(CfgWork& W, const void* src, size_t bytes, void* dst, hipStream_
 template <typename T>
 bool grow(T*& p, size_t& cap, size_t n) {
     if (n <= cap) return true;
-    hipFree(p);
+    psx::dfree(p);
     p = nullptr;
     cap = 0;
     const size_t nc = n + n / 4;
-    if (hipMalloc(&p, nc * sizeof(T)) != hipSuccess) return false;
+    if (psx::dmalloc(&p, nc * sizeof(T)) != hipSuccess) return false;
     cap = nc;
     return true;
 }
@@ -489,9 +490,9 @@ int configs_pass(CfgWork& W, const int16_t* rows, int64_t n_rows, int n_groups, 
     if (!grow(W.rows, W.cap_rows, nel) || !grow(W.blk, W.cap_blk, 2 * (size_t)nblk) ||
         !grow(W.ptr, W.cap_ptr, (size_t)C.U + 1))
         return bad("out of device memory (configs rows)");
-    if (!W.status && hipMalloc(&W.status, 5 * sizeof(unsigned long long)) != hipSuccess)
+    if (!W.status && psx::dmalloc(&W.status, 5 * sizeof(unsigned long long)) != hipSuccess)
         return bad("out of device memory");
-    if (!W.hstatus && hipHostMalloc(&W.hstatus, 5 * sizeof(unsigned long long)) != hipSuccess)
+    if (!W.hstatus && psx::hmalloc(&W.hstatus, 5 * sizeof(unsigned long long)) != hipSuccess)
         return bad("out of pinned host memory");
     if (upload_rows(W, rows, nel * sizeof(int16_t), W.rows, st) ||
         hipMemsetAsync(W.status, 0xff, sizeof(unsigned long long), st) != hipSuccess ||
@@ -524,35 +525,35 @@ int configs_pass(CfgWork& W, const int16_t* rows, int64_t n_rows, int n_groups, 
     const int nchunk = (int)((ns + chunk - 1) / chunk);
     const size_t need = std::max((size_t)C.U * S * sizeof(Acc5), (size_t)nchunk * sizeof(SetRec));
     if (need > W.cap_parts) {
-        hipFree(W.parts);
+        psx::dfree(W.parts);
         W.parts = nullptr;
         W.cap_parts = 0;
-        if (hipMalloc(&W.parts, need) != hipSuccess) return bad("out of device memory (configs folds)");
+        if (psx::dmalloc(&W.parts, need) != hipSuccess) return bad("out of device memory (configs folds)");
         W.cap_parts = need;
     }
     if (ns > W.cap_sets) {
-        hipFree(W.srec);
-        hipFree(W.rrec);
-        hipFree(W.masks);
+        psx::dfree(W.srec);
+        psx::dfree(W.rrec);
+        psx::dfree(W.masks);
         W.srec = nullptr;
         W.rrec = nullptr;
         W.masks = nullptr;
         W.cap_sets = 0;
         const size_t c = ns + ns / 4;
-        if (hipMalloc(&W.srec, c * sizeof(SetRec)) != hipSuccess || hipMalloc(&W.rrec, c * sizeof(CfgRow)) != hipSuccess ||
-            hipMalloc(&W.masks, c * sizeof(int)) != hipSuccess)
+        if (psx::dmalloc(&W.srec, c * sizeof(SetRec)) != hipSuccess || psx::dmalloc(&W.rrec, c * sizeof(CfgRow)) != hipSuccess ||
+            psx::dmalloc(&W.masks, c * sizeof(int)) != hipSuccess)
             return bad("out of device memory (configs sets)");
         W.cap_sets = c;
     }
     if (nr > W.cap_rec) {  // keys and values, each sort input + output
-        hipFree(W.keys);
-        hipFree(W.vals);
+        psx::dfree(W.keys);
+        psx::dfree(W.vals);
         W.keys = nullptr;
         W.vals = nullptr;
         W.cap_rec = 0;
         const size_t c = nr + nr / 4;
-        if (hipMalloc(&W.keys, 2 * c * sizeof(unsigned)) != hipSuccess ||
-            hipMalloc(&W.vals, 2 * c * sizeof(int)) != hipSuccess)
+        if (psx::dmalloc(&W.keys, 2 * c * sizeof(unsigned)) != hipSuccess ||
+            psx::dmalloc(&W.vals, 2 * c * sizeof(int)) != hipSuccess)
             return bad("out of device memory (configs records)");
         W.cap_rec = c;
     }
@@ -565,10 +566,10 @@ int configs_pass(CfgWork& W, const int16_t* rows, int64_t n_rows, int n_groups, 
         hipSuccess)
         return bad("configs sort sizing");
     if (tmp > W.cap_sort) {
-        hipFree(W.sort_tmp);
+        psx::dfree(W.sort_tmp);
         W.sort_tmp = nullptr;
         W.cap_sort = 0;
-        if (hipMalloc(&W.sort_tmp, tmp) != hipSuccess) return bad("out of device memory (configs sort)");
+        if (psx::dmalloc(&W.sort_tmp, tmp) != hipSuccess) return bad("out of device memory (configs sort)");
         W.cap_sort = tmp;
     }
     if (k0 && hipEventRecord(k0, st) != hipSuccess) return bad("event");
@@ -593,21 +594,21 @@ int configs_pass(CfgWork& W, const int16_t* rows, int64_t n_rows, int n_groups, 
 }
 
 void configs_free(CfgWork& W) {
-    hipFree(W.rows);
-    hipFree(W.blk);
-    hipFree(W.ptr);
-    hipFree(W.status);
-    hipFree(W.srec);
-    hipFree(W.rrec);
-    hipFree(W.masks);
-    hipFree(W.keys);
-    hipFree(W.vals);
-    hipFree(W.sort_tmp);
-    hipFree(W.parts);
-    if (W.hstatus) hipHostFree(W.hstatus);
+    psx::dfree(W.rows);
+    psx::dfree(W.blk);
+    psx::dfree(W.ptr);
+    psx::dfree(W.status);
+    psx::dfree(W.srec);
+    psx::dfree(W.rrec);
+    psx::dfree(W.masks);
+    psx::dfree(W.keys);
+    psx::dfree(W.vals);
+    psx::dfree(W.sort_tmp);
+    psx::dfree(W.parts);
+    if (W.hstatus) psx::hfree(W.hstatus);
     for (int b = 0; b < 2; b++)
         if (W.dma[b]) hipEventDestroy(W.dma[b]);
-    if (W.hpin) hipHostFree(W.hpin);
+    if (W.hpin) psx::hfree(W.hpin);
     W = CfgWork{};
 }
 

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "psx_setup.h"
+#include "psx_mem.h"
 
 namespace psx {
 
@@ -91,12 +92,12 @@ int eigen_lowrank_device(const double* sig, const double* z, int M, hipStream_t 
     rocblas_handle h = nullptr;
     auto done = [&]() {
         if (h) L.destroy(h);
-        hipFree(dw);
-        hipFree(dz);
-        hipFree(dinfo);
+        psx::dfree(dw);
+        psx::dfree(dz);
+        psx::dfree(dinfo);
     };
-    if (hipMalloc(&dw, 2 * (size_t)M * sizeof(double)) != hipSuccess ||
-        hipMalloc(&dz, (size_t)M * sizeof(double)) != hipSuccess || hipMalloc(&dinfo, sizeof(rocblas_int)) != hipSuccess) {
+    if (psx::dmalloc(&dw, 2 * (size_t)M * sizeof(double)) != hipSuccess ||
+        psx::dmalloc(&dz, (size_t)M * sizeof(double)) != hipSuccess || psx::dmalloc(&dinfo, sizeof(rocblas_int)) != hipSuccess) {
         done();
         return bad("out of device memory (eigen route)");
     }

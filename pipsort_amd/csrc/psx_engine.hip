@@ -27,15 +27,19 @@
 #include "psx_setup.h"
 #include "psx_sweep.h"
 #include "psx_sweep_dev.h"
+#include "psx_mem.h"
 
 using psx::Acc5;
+using psx::kPlanMagic;
+using psx::PlanTag;
 using psx::SetRec;
 
 namespace {
 
 thread_local std::string g_err;
+constexpr int kPlanMismatchWord = 8;  // status word raised by k_merge_partials
 
-constexpr size_t kStatBytes = 64;  // SetRec (56 B) + EXACT flag (4 B) + pad
+constexpr size_t kStatBytes = 3 * 56;  // SetRec, PlanTag, status words (EXACT flag first)
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -444,7 +448,7 @@ __global__ __launch_bounds__(64) void k_eval_rows(DevProb P, const int* __restri
 // Image layout: Acc5[ldg] followed by one Acc5-sized slot holding the SetRec.
 __global__ void k_merge_partials(const Acc5* __restrict__ parts, int U, int ldg, int count, Acc5* __restrict__ acc,
                                  SetRec* __restrict__ sacc, int* __restrict__ flag) {
-    const size_t stride = (size_t)ldg + 1;
+    const size_t stride = (size_t)ldg + 2;  // ldg Acc5, SetRec, PlanTag
     int u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u < U) {
         Acc5 a = {0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -462,6 +466,14 @@ __global__ void k_merge_partials(const Acc5* __restrict__ parts, int U, int ldg,
         s.pad = f;
         flag[1] |= f;
         *sacc = s;
+        // the images must be shards 0 .. count - 1 of one plan (PlanTag)
+        const PlanTag& t0 = *reinterpret_cast<const PlanTag*>(parts + ldg + 1);
+        int bad = 0;
+        for (int r = 0; r < count; r++) {
+            const PlanTag& t = *reinterpret_cast<const PlanTag*>(parts + (size_t)r * stride + ldg + 1);
+            bad |= t.magic != kPlanMagic || t.hash != t0.hash || t.world != count || t.rank != r || t.U != U;
+        }
+        if (bad) flag[kPlanMismatchWord] = 1;
     }
 }
 
@@ -644,7 +656,8 @@ void sss_release(SssDev* d);
 struct psx_engine {
     int dev = 0;
     hipStream_t stream = nullptr;
-    hipStream_t own_stream = nullptr;  // created by psx_create
+    hipStream_t own_stream = nullptr;  // from the stream pool (psx_create)
+    int own_pr = 0;                    // its priority (pool key)
     bool external_stream = false;      // psx_set_stream: caller orders export/merge
     int S = 2;
     int m[2] = {0, 0};
@@ -661,12 +674,15 @@ struct psx_engine {
     double* dAd[2] = {nullptr, nullptr};
     double* dy[2] = {nullptr, nullptr};
     unsigned char* dpres = nullptr;
-    // accumulator image, one allocation of ldg + 2 slots: per-SNP Acc5[ldg], then
-    // the SetRec scalars (slot ldg), then the status word (EXACT flag, slot ldg+1);
-    // the first ldg + 1 slots are the exported partial image
+    // accumulator image, one allocation of ldg + 3 slots: per-SNP Acc5[ldg], then
+    // the SetRec scalars (slot ldg), the PlanTag (slot ldg + 1), then the status
+    // words (slot ldg + 2: [0] EXACT flag, [1] its sticky copy, [2..3] the other
+    // record buffers' flags, [8] plan mismatch); the first ldg + 2 slots are the
+    // exported partial image
     Acc5* dacc = nullptr;
     SetRec* dsacc = nullptr;   // = slot ldg
-    int* dflag = nullptr;      // = slot ldg + 1
+    PlanTag* dtag = nullptr;   // = slot ldg + 1
+    int* dflag = nullptr;      // = slot ldg + 2
     unsigned char* hstat = nullptr;  // pinned host copy of the status block
     // fused exhaustive pass: every unit set record of the pass in one buffer
     SetRec* dpass = nullptr;
@@ -708,6 +724,8 @@ struct psx_engine {
     // pipelined asynchronous passes: sweeps on a compute stream, merges (and the
     // caller's exchange) on `stream`; record buffers alternate by pass parity
     hipStream_t cstream = nullptr;
+    static constexpr int kCuMasked = 1 << 30;  // cstream_pr of a CU-masked (not pooled) stream
+    int cstream_pr = 0;                        // its priority (stream pool key)
     // overlapped passes (PSX_OVERLAP = n reserved CUs): two compute streams
     // masked off n CUs, alternating, so pass i + 1's units fill pass i's drain;
     // the merges and the caller's exchange keep the reserved CUs
@@ -734,6 +752,7 @@ struct psx_engine {
     // timing
     hipEvent_t ev[4];
     psx_timing timing;
+    double prep_ms = 0;  // host wall of the last run's plan / layout preparation
     uint64_t n_configs = 0;
 
     ~psx_engine();
@@ -741,20 +760,23 @@ struct psx_engine {
 
 psx_engine::~psx_engine() {
     hipSetDevice(dev);
-    for (int s = 0; s < 2; s++) { hipFree(dG[s]); hipFree(dAd[s]); hipFree(dy[s]); }
-    hipFree(dpres); hipFree(dacc);
-    if (hstat) hipHostFree(hstat);
+    // one device synchronisation, then every block goes back to the pool as is
+    hipDeviceSynchronize();
+    psx::IdleScope idle;
+    for (int s = 0; s < 2; s++) { psx::dfree(dG[s]); psx::dfree(dAd[s]); psx::dfree(dy[s]); }
+    psx::dfree(dpres); psx::dfree(dacc);
+    if (hstat) psx::hfree(hstat);
     if (stage_ev) { hipEventSynchronize(stage_ev); hipEventDestroy(stage_ev); }
-    if (hstage) hipHostFree(hstage);
-    if (hscore) hipHostFree(hscore);
-    hipFree(dgen); hipFree(dscore); hipFree(dsrec); hipFree(dmrec); hipFree(dpass);
+    if (hstage) psx::hfree(hstage);
+    if (hscore) psx::hfree(hscore);
+    psx::dfree(dgen); psx::dfree(dscore); psx::dfree(dsrec); psx::dfree(dmrec); psx::dfree(dpass);
     psx::sweep_free(plans);
     psx::configs_free(cfg);
-    hipFree(d_cfg_maps);
+    psx::dfree(d_cfg_maps);
     sss_release(sss);
     for (auto& kv : glevels) {
         GenLevel& g = kv.second;
-        hipFree(g.d_sets); hipFree(g.d_csr); hipFree(g.d_srec); hipFree(g.d_mrec);
+        psx::dfree(g.d_sets); psx::dfree(g.d_csr); psx::dfree(g.d_srec); psx::dfree(g.d_mrec);
         for (int i = 0; i < 2; i++) if (g.ev[i]) hipEventDestroy(g.ev[i]);
     }
     for (int i = 0; i < 4; i++) hipEventDestroy(ev[i]);
@@ -762,10 +784,14 @@ psx_engine::~psx_engine() {
     if (span0) hipEventDestroy(span0);
     for (int i = 0; i < kBufs; i++)
         if (mdone[i]) hipEventDestroy(mdone[i]);
-    if (cstream) { hipStreamSynchronize(cstream); hipStreamDestroy(cstream); }
     if (cstream2) { hipStreamSynchronize(cstream2); hipStreamDestroy(cstream2); }
-
-    if (own_stream) hipStreamDestroy(own_stream);
+    if (cstream && cstream_pr == kCuMasked) {
+        hipStreamSynchronize(cstream);
+        hipStreamDestroy(cstream);
+    } else if (cstream) {
+        psx::stream_put(cstream, cstream_pr);
+    }
+    if (own_stream) psx::stream_put(own_stream, own_pr);
 }
 
 namespace {
@@ -773,10 +799,10 @@ namespace {
 template <typename T>
 int ensure(T*& p, size_t& cap, size_t n) {
     if (n <= cap) return 0;
-    hipFree(p);
+    psx::dfree(p);
     p = nullptr;
     size_t nc = std::max(n, cap * 2);
-    HIPCHK(hipMalloc(&p, nc * sizeof(T)));
+    HIPCHK(psx::dmalloc(&p, nc * sizeof(T)));
     cap = nc;
     return 0;
 }
@@ -786,10 +812,10 @@ template <typename T>
 int ensure_host(T*& p, size_t& cap, size_t n) {
     if (n <= cap) return 0;
     const size_t nc = std::max(n, cap * 2);
-    if (p) hipHostFree(p);
+    if (p) psx::hfree(p);
     p = nullptr;
     cap = 0;
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&p), nc * sizeof(T)));
+    HIPCHK(psx::hmalloc(reinterpret_cast<void**>(&p), nc * sizeof(T)));
     cap = nc;
     return 0;
 }
@@ -998,6 +1024,43 @@ int run_level_generic(psx_engine* e, int k, double* kms) {
     return 0;
 }
 
+// the shard plan every rank of a job must share (PlanTag.hash): the locus shape,
+// c, the world size and the plan knobs / compiled plan constants
+uint64_t plan_hash(const psx_engine* e) {
+    uint64_t h = psx::plan_knobs_hash();
+    auto mix = [&](const void* p, size_t n) {
+        for (size_t i = 0; i < n; i++) h = (h ^ ((const unsigned char*)p)[i]) * 1099511628211ull;
+    };
+    const int v[4] = {e->U, e->ldg, e->maxc, e->world};
+    mix(v, sizeof(v));
+    mix(e->pres.data(), e->pres.size());
+    return h;
+}
+
+int write_tag(psx_engine* e) {
+    PlanTag t;
+    std::memset(&t, 0, sizeof(t));
+    t.magic = kPlanMagic;
+    t.world = e->world;
+    t.rank = e->rank;
+    t.U = e->U;
+    t.hash = plan_hash(e);
+    HIPCHK(hipMemcpyAsync(e->dtag, &t, sizeof(t), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+// after a synchronous merge of partial images
+int check_plan_mismatch(psx_engine* e) {
+    int bad = 0;
+    HIPCHK(hipMemcpyAsync(&bad, e->dflag + kPlanMismatchWord, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (bad)
+        return fail(PSX_EINVAL, "merged partial images are not shards 0..world-1 of one plan "
+                                "(ranks with different PSX_K3_* knobs, builds or shard settings)");
+    return 0;
+}
+
 int reset_acc(psx_engine* e) {
     HIPCHK(hipMemsetAsync(e->dacc, 0, sizeof(Acc5) * e->ldg, e->stream));
     SetRec z = psx::set_zero();
@@ -1035,12 +1098,12 @@ int enqueue_generic_level(psx_engine* e, int k) {
         packed.insert(packed.end(), idx.begin(), idx.end());
         packed.insert(packed.end(), rows.begin(), rows.end());
         if (g.nsets) {
-            HIPCHK(hipMalloc(&g.d_sets, sizeof(int) * sets.size()));
+            HIPCHK(psx::dmalloc(&g.d_sets, sizeof(int) * sets.size()));
             HIPCHK(hipMemcpy(g.d_sets, sets.data(), sizeof(int) * sets.size(), hipMemcpyHostToDevice));
-            HIPCHK(hipMalloc(&g.d_csr, sizeof(int) * packed.size()));
+            HIPCHK(psx::dmalloc(&g.d_csr, sizeof(int) * packed.size()));
             HIPCHK(hipMemcpy(g.d_csr, packed.data(), sizeof(int) * packed.size(), hipMemcpyHostToDevice));
-            HIPCHK(hipMalloc(&g.d_srec, sizeof(SetRec) * g.nsets));
-            HIPCHK(hipMalloc(&g.d_mrec, sizeof(Acc5) * g.nsets * k));
+            HIPCHK(psx::dmalloc(&g.d_srec, sizeof(SetRec) * g.nsets));
+            HIPCHK(psx::dmalloc(&g.d_mrec, sizeof(Acc5) * g.nsets * k));
         }
         for (int i = 0; i < 2; i++) HIPCHK(hipEventCreate(&g.ev[i]));
         it = e->glevels.emplace(key, g).first;
@@ -1077,9 +1140,9 @@ int get_level1(psx_engine* e, psx_engine::GenLevel** out) {
         if (g.nsets) {
             std::vector<int> sets(g.nsets);
             for (size_t i = 0; i < g.nsets; i++) sets[i] = (int)(lo + i);
-            HIPCHK(hipMalloc(&g.d_sets, sizeof(int) * g.nsets));
+            HIPCHK(psx::dmalloc(&g.d_sets, sizeof(int) * g.nsets));
             HIPCHK(hipMemcpy(g.d_sets, sets.data(), sizeof(int) * g.nsets, hipMemcpyHostToDevice));
-            HIPCHK(hipMalloc(&g.d_srec, sizeof(SetRec) * g.nsets));
+            HIPCHK(psx::dmalloc(&g.d_srec, sizeof(SetRec) * g.nsets));
         }
         for (int i = 0; i < 2; i++) HIPCHK(hipEventCreate(&g.ev[i]));
         it = e->glevels.emplace(key, g).first;
@@ -1183,9 +1246,11 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     const psx::SweepArgs sa = sweep_args(e);
     psx::SweepPlan* P2 = nullptr;
     psx::SweepPlan* P3 = nullptr;
+    const auto tp = std::chrono::steady_clock::now();
     if (psx::sweep_prepare(e->plans, 2, e->U, e->ldg, e->rank, e->world, e->stream, sa, false, &P2) ||
         (e->maxc == 3 && psx::sweep_prepare(e->plans, 3, e->U, e->ldg, e->rank, e->world, e->stream, sa, false, &P3)))
         return fail(PSX_EHIP, std::string("sweep plan: ") + psx::sweep_error());
+    e->prep_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
     psx::SweepPlan* top = P3 ? P3 : P2;
     psx::SweepPlan* low = P3 ? P2 : nullptr;
     const size_t nl = low ? (size_t)low->n_units : 0, nt = (size_t)top->n_units;
@@ -1223,6 +1288,7 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
                 }
                 HIPCHK(hipExtStreamCreateWithCUMask(&e->cstream, (uint32_t)mask.size(), mask.data()));
                 HIPCHK(hipExtStreamCreateWithCUMask(&e->cstream2, (uint32_t)mask.size(), mask.data()));
+                e->cstream_pr = psx_engine::kCuMasked;  // not pooled
             } else {
                 // the compute stream sits below the engine / exchange stream in
                 // priority, so merges and the exchange get wave slots first.  (Two
@@ -1232,7 +1298,8 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
                 // starve; PSX_OVERLAP reserves CUs for them.)
                 int lo_pr = 0, hi_pr = 0;
                 HIPCHK(hipDeviceGetStreamPriorityRange(&lo_pr, &hi_pr));
-                HIPCHK(hipStreamCreateWithPriority(&e->cstream, hipStreamNonBlocking, (lo_pr + hi_pr) / 2));
+                e->cstream_pr = (lo_pr + hi_pr) / 2;
+                HIPCHK(psx::stream_get(&e->cstream, e->cstream_pr));
             }
             for (int i = 0; i < psx_engine::kBufs; i++)
                 if (!e->mdone[i]) HIPCHK(hipEventCreateWithFlags(&e->mdone[i], hipEventDisableTiming));
@@ -1285,14 +1352,15 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     const SetRec extra = e->rank == 0 ? null_rec(e, 1.0) : psx::set_zero();
     psx::SweepPlan* mA = low ? low : top;
     psx::SweepPlan* mB = low ? top : nullptr;
-    // (PSX_ABLATE_MERGE=1: timing ablation only — the pass's merge is skipped and
-    // its results are wrong; measures what the merge beside the next sweep costs)
-    static const bool ablate_merge = std::getenv("PSX_ABLATE_MERGE") != nullptr;
-    if (!ablate_merge)
+    // (-DPSX_ABLATE_MERGE, a separate timing build only: the pass's merge is
+    // skipped and its results are wrong; measures what the merge beside the next
+    // sweep costs.  No environment switch: a shipped library always merges.)
+#ifndef PSX_ABLATE_MERGE
     hipLaunchKernelGGL(k_merge_pass_l1, dim3((e->U + 1 + kMergeWaves - 1) / kMergeWaves), dim3(kMergeThreads * kMergeWaves), 0, X, e->dp, lo, hi, psx::plan_records(*mA, par),
                        mA->d_dptr, mA->d_gidx, mB ? psx::plan_records(*mB, par) : nullptr, mB ? mB->d_dptr : nullptr,
                        mB ? mB->d_gidx : nullptr, dpass,
                        (long)(nl + nt), extra, e->dacc, e->dsacc, pflag, e->dflag + 1);
+#endif
     HIPCHK(hipGetLastError());
     if (async) {
         HIPCHK(hipEventRecord(e->mdone[par], X));
@@ -1369,8 +1437,9 @@ int create_impl(const psx_problem* p, const psx_ld_problem* ld, int device, psx_
     // priority compute streams in pipelined mode)
     int pr_lo = 0, pr_hi = 0;
     if (hipDeviceGetStreamPriorityRange(&pr_lo, &pr_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&e->own_stream, hipStreamNonBlocking, pr_hi) != hipSuccess)
+        psx::stream_get(&e->own_stream, pr_hi) != hipSuccess)
         return bail(fail(PSX_EHIP, "stream"));
+    e->own_pr = pr_hi;
     e->stream = e->own_stream;
     for (int i = 0; i < 4; i++)
         if (hipEventCreate(&e->ev[i]) != hipSuccess) return bail(fail(PSX_EHIP, "event"));
@@ -1390,6 +1459,13 @@ int create_impl(const psx_problem* p, const psx_ld_problem* ld, int device, psx_
             if (l >= 0) { e->pres[u] |= (unsigned char)(1 << s); cnt++; }
         }
         if (cnt != p->m[s]) return bail(fail(PSX_EINVAL, "Invariant does not hold (model.h:140-143)"));
+    }
+    // the exhaustive pass's unit plans (host decomposition + record CSR) depend
+    // only on the locus shape: built on host threads while the setup runs
+    e->plans.pres_host = e->pres;
+    if (fused_eligible(e)) {
+        psx::plan_prefetch(e->plans, device, 2, e->U, e->ldg, 0, 1, false);
+        if (e->maxc == 3) psx::plan_prefetch(e->plans, device, 3, e->U, e->ldg, 0, 1, false);
     }
     // d_s (postcal.cpp:66,89): s^2 * (n_s / min n) + t^2 with integer sample sizes
     int mn = std::min(p->sample_sizes[0], p->sample_sizes[1]);
@@ -1421,51 +1497,75 @@ int create_impl(const psx_problem* p, const psx_ld_problem* ld, int device, psx_
         }
     }
 
-    // device data: Sigma~ = B^T B, y = B^T S' per study, in union coordinates
+    // device data: Sigma~ = B^T B, y = B^T S' per study, in union coordinates.
+    // The two studies are independent (BIG_SIGMA is block-diagonal, model.h:239):
+    // study 1 runs on a second host thread and stream beside study 0.
+    using clk = std::chrono::steady_clock;
+    auto since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     size_t gsz = (size_t)e->ldg * e->ldg;
-    double *dB = nullptr, *dS = nullptr, *dsp = nullptr, *dyl = nullptr;
-    int* du2l = nullptr;
-    int Mx = std::max(p->m[0], p->m[1]);
-    if (hipMalloc(&dB, (size_t)Mx * Mx * sizeof(double)) != hipSuccess ||
-        hipMalloc(&dS, (size_t)Mx * Mx * sizeof(double)) != hipSuccess ||
-        hipMalloc(&dsp, (size_t)Mx * sizeof(double)) != hipSuccess ||
-        hipMalloc(&dyl, (size_t)Mx * sizeof(double)) != hipSuccess ||
-        hipMalloc(&du2l, (size_t)e->U * sizeof(int)) != hipSuccess)
-        return bail(fail(PSX_EHIP, "out of device memory (setup)"));
-    auto cleanup = [&]() { hipFree(dB); hipFree(dS); hipFree(dsp); hipFree(dyl); hipFree(du2l); };
-    size_t boff = 0;
-    int soff = 0;
-    std::vector<double> ad(e->ldg), yu(e->ldg);
-    for (int s = 0; s < 2; s++) {
-        int M = p->m[s];
-        if (hipMalloc(&e->dG[s], gsz * sizeof(double)) != hipSuccess ||
-            hipMalloc(&e->dAd[s], e->ldg * sizeof(double)) != hipSuccess ||
-            hipMalloc(&e->dy[s], e->ldg * sizeof(double)) != hipSuccess) {
-            cleanup();
-            return bail(fail(PSX_EHIP, "out of device memory"));
+    struct Scratch {
+        double *dB = nullptr, *dS = nullptr, *dsp = nullptr, *dyl = nullptr;
+        int* du2l = nullptr;
+        hipStream_t st = nullptr;
+        std::string err;
+        int code = 0;
+        double spsq = 0;
+        psx::LdStudyResult r;
+    } sc[2];
+    auto cleanup = [&]() {
+        for (auto& x : sc)
+            if (x.st) hipStreamSynchronize(x.st);
+        psx::IdleScope idle;  // the scratch was used on these two streams only
+        for (auto& x : sc) {
+            psx::dfree(x.dB); psx::dfree(x.dS); psx::dfree(x.dsp); psx::dfree(x.dyl); psx::dfree(x.du2l);
+            if (x.st && x.st != e->stream) psx::stream_put(x.st, 0);
         }
-        hipMemcpyAsync(du2l, p->union_to_local + s * e->U, e->U * sizeof(int), hipMemcpyHostToDevice, e->stream);
+    };
+    const clk::time_point ta = clk::now();
+    for (int s = 0; s < 2; s++) {
+        const int M = p->m[s];
+        Scratch& x = sc[s];
+        if (psx::dmalloc(&x.dB, (size_t)M * M * sizeof(double)) != hipSuccess ||
+            psx::dmalloc(&x.dS, (size_t)M * M * sizeof(double)) != hipSuccess ||
+            psx::dmalloc(&x.dsp, (size_t)M * sizeof(double)) != hipSuccess ||
+            psx::dmalloc(&x.dyl, (size_t)M * sizeof(double)) != hipSuccess ||
+            psx::dmalloc(&x.du2l, (size_t)e->U * sizeof(int)) != hipSuccess ||
+            psx::dmalloc(&e->dG[s], gsz * sizeof(double)) != hipSuccess ||
+            psx::dmalloc(&e->dAd[s], e->ldg * sizeof(double)) != hipSuccess ||
+            psx::dmalloc(&e->dy[s], e->ldg * sizeof(double)) != hipSuccess) {
+            cleanup();
+            return bail(fail(PSX_EHIP, "out of device memory (setup)"));
+        }
+    }
+    sc[0].st = e->stream;
+    if (psx::stream_get(&sc[1].st, 0) != hipSuccess) {
+        sc[1].st = nullptr;
+        cleanup();
+        return bail(fail(PSX_EHIP, "stream"));
+    }
+    const double alloc_ms = since(ta);
+    const clk::time_point tb = clk::now();
+    auto study = [&](int s) {
+        Scratch& x = sc[s];
+        auto die = [&](int code, const std::string& msg) { x.code = code; x.err = msg; };
+        if (hipSetDevice(device) != hipSuccess) return die(PSX_EHIP, "set device");
+        const int M = p->m[s];
+        const size_t boff = s ? (size_t)p->m[0] * p->m[0] : 0;
+        const int soff = s ? p->m[0] : 0;
+        hipStream_t st = x.st;
+        hipMemcpyAsync(x.du2l, p->union_to_local + s * e->U, e->U * sizeof(int), hipMemcpyHostToDevice, st);
         bool lowrank = true;  // Sigma~ = B^T B, y = B^T S' from (B, S')
         const double* Bs = ld ? nullptr : p->B + boff;
         const double* Ss = ld ? nullptr : p->s_prime + soff;
         std::vector<double> hB, hS;
         if (ld) {
-            psx::LdStudyResult r;
+            psx::LdStudyResult& r = x.r;
             std::string err;
-            if (psx::ld_study_setup(ld->ld + boff, ld->z + soff, M, e->stream, dS, dyl, &r, &err)) {
-                cleanup();
-                return bail(fail(PSX_EHIP, "GPU model setup: " + err));
-            }
-            if (info) {
-                info->psd_added[s] = r.added;
-                info->psd_iterations[s] = r.psd_iterations;
-                info->eigen_route[s] = r.path;
-                info->min_pivot_ratio[s] = r.min_pivot_ratio;
-            }
-            if (info) info->spsq[s] = r.path == 0 ? r.spsq : 0.0;
+            if (psx::ld_study_setup(ld->ld + boff, ld->z + soff, M, st, x.dS, x.dyl, &r, &err))
+                return die(PSX_EHIP, "GPU model setup: " + err);
             if (r.path == 0) {
                 lowrank = false;
-                spsq += r.spsq;
+                x.spsq += r.spsq;
             } else {
                 // Sigma' not (comfortably) positive definite: the reference's eigen
                 // route (model.h:213-259) on the GPU, B and S' left in dB / dsp
@@ -1476,60 +1576,83 @@ int create_impl(const psx_problem* p, const psx_ld_problem* ld, int device, psx_
                 if (he && atoi(he)) {
                     hB.resize((size_t)M * M);
                     hS.resize(M);
-                    if (psx_lowrank_study(sig.data(), ld->z + soff, M, hB.data(), hS.data())) {
-                        cleanup();
-                        return bail(fail(PSX_EINVAL, "eigen route failed"));
-                    }
-                    for (int i = 0; i < M; i++) spsq += hS[i] * hS[i];
+                    if (psx_lowrank_study(sig.data(), ld->z + soff, M, hB.data(), hS.data()))
+                        return die(PSX_EINVAL, "eigen route failed");
+                    for (int i = 0; i < M; i++) x.spsq += hS[i] * hS[i];
                     Bs = hB.data();
                     Ss = hS.data();
                 } else {
                     double sq = 0;
-                    if (psx::eigen_lowrank_device(sig.data(), ld->z + soff, M, e->stream, dS, dB, dsp, &sq, &err)) {
-                        cleanup();
-                        return bail(fail(PSX_EHIP, "GPU eigen route: " + err));
-                    }
-                    spsq += sq;
+                    if (psx::eigen_lowrank_device(sig.data(), ld->z + soff, M, st, x.dS, x.dB, x.dsp, &sq, &err))
+                        return die(PSX_EHIP, "GPU eigen route: " + err);
+                    x.spsq += sq;
                     Bs = Ss = nullptr;  // already on the device
                 }
             }
         }
         if (lowrank) {
-            if (Bs) hipMemcpyAsync(dB, Bs, (size_t)M * M * sizeof(double), hipMemcpyHostToDevice, e->stream);
-            if (Ss) hipMemcpyAsync(dsp, Ss, (size_t)M * sizeof(double), hipMemcpyHostToDevice, e->stream);
+            if (Bs) hipMemcpyAsync(x.dB, Bs, (size_t)M * M * sizeof(double), hipMemcpyHostToDevice, st);
+            if (Ss) hipMemcpyAsync(x.dsp, Ss, (size_t)M * sizeof(double), hipMemcpyHostToDevice, st);
             dim3 g((M + 15) / 16, (M + 15) / 16);
-            hipLaunchKernelGGL(k_btb, g, dim3(256), 0, e->stream, dB, M, dS);
-            hipLaunchKernelGGL(k_bts, dim3(M), dim3(64), 0, e->stream, dB, dsp, M, dyl);
+            hipLaunchKernelGGL(k_btb, g, dim3(256), 0, st, x.dB, M, x.dS);
+            hipLaunchKernelGGL(k_bts, dim3(M), dim3(64), 0, st, x.dB, x.dsp, M, x.dyl);
         }
-        hipLaunchKernelGGL(k_to_union, dim3((e->ldg + 255) / 256, e->ldg), dim3(256), 0, e->stream, dS, M, du2l,
-                           e->U, e->ldg, e->dG[s]);
-        if (hipGetLastError() != hipSuccess) { cleanup(); return bail(fail(PSX_EHIP, "setup kernel launch")); }
+        hipLaunchKernelGGL(k_to_union, dim3((e->ldg + 255) / 256, e->ldg), dim3(256), 0, st, x.dS, M, x.du2l, e->U,
+                           e->ldg, e->dG[s]);
+        if (hipGetLastError() != hipSuccess) return die(PSX_EHIP, "setup kernel launch");
         std::vector<double> Sd((size_t)M), yl(M);
         // diagonal of Sigma~ (into the B staging buffer, no longer needed) and y
-        hipLaunchKernelGGL(k_diag, dim3((M + 255) / 256), dim3(256), 0, e->stream, dS, M, dB);
-        hipMemcpyAsync(Sd.data(), dB, M * sizeof(double), hipMemcpyDeviceToHost, e->stream);
-        hipMemcpyAsync(yl.data(), dyl, M * sizeof(double), hipMemcpyDeviceToHost, e->stream);
-        if (hipStreamSynchronize(e->stream) != hipSuccess) { cleanup(); return bail(fail(PSX_EHIP, "setup sync")); }
+        hipLaunchKernelGGL(k_diag, dim3((M + 255) / 256), dim3(256), 0, st, x.dS, M, x.dB);
+        hipMemcpyAsync(Sd.data(), x.dB, M * sizeof(double), hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(yl.data(), x.dyl, M * sizeof(double), hipMemcpyDeviceToHost, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return die(PSX_EHIP, "setup sync");
+        std::vector<double> ad(e->ldg), yu(e->ldg);
         for (int u = 0; u < e->ldg; u++) {
             int l = (u < e->U) ? e->u2l[s * e->U + u] : -1;
             ad[u] = 1.0 / e->dval[s] + (l >= 0 ? Sd[l] : 0.0);
             yu[u] = (l >= 0) ? yl[l] : 0.0;
         }
-        hipMemcpyAsync(e->dAd[s], ad.data(), e->ldg * sizeof(double), hipMemcpyHostToDevice, e->stream);
-        hipMemcpyAsync(e->dy[s], yu.data(), e->ldg * sizeof(double), hipMemcpyHostToDevice, e->stream);
-        if (hipStreamSynchronize(e->stream) != hipSuccess) { cleanup(); return bail(fail(PSX_EHIP, "setup copy")); }
-        boff += (size_t)M * M;
-        soff += M;
+        hipMemcpyAsync(e->dAd[s], ad.data(), e->ldg * sizeof(double), hipMemcpyHostToDevice, st);
+        hipMemcpyAsync(e->dy[s], yu.data(), e->ldg * sizeof(double), hipMemcpyHostToDevice, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return die(PSX_EHIP, "setup copy");
+    };
+    {
+        std::thread t1(study, 1);
+        study(0);
+        t1.join();
     }
+    const double studies_ms = since(tb);
+    for (int s = 0; s < 2; s++) {
+        if (sc[s].code) {
+            const int code = sc[s].code;
+            const std::string msg = sc[s].err;
+            cleanup();
+            return bail(fail(code, msg));
+        }
+        spsq += sc[s].spsq;
+        if (ld && info) {
+            const psx::LdStudyResult& r = sc[s].r;
+            info->psd_added[s] = r.added;
+            info->psd_iterations[s] = r.psd_iterations;
+            info->eigen_route[s] = r.path;
+            info->min_pivot_ratio[s] = r.min_pivot_ratio;
+            info->spsq[s] = r.path == 0 ? r.spsq : 0.0;
+            info->study_upload_ms[s] = r.upload_ms;
+            info->study_psd_ms[s] = r.psd_ms;
+            info->study_finish_ms[s] = r.finish_ms;
+        }
+    }
+    const clk::time_point tc = clk::now();
     cleanup();
     e->K = -spsq / 2;
-    if (hipMalloc(&e->dpres, e->ldg) != hipSuccess ||
-        hipMalloc(&e->dacc, sizeof(Acc5) * ((size_t)e->ldg + 2)) != hipSuccess ||
-        hipHostMalloc(&e->hstat, kStatBytes) != hipSuccess)
+    if (psx::dmalloc(&e->dpres, e->ldg) != hipSuccess ||
+        psx::dmalloc(&e->dacc, sizeof(Acc5) * ((size_t)e->ldg + 3)) != hipSuccess ||
+        psx::hmalloc(&e->hstat, kStatBytes) != hipSuccess)
         return bail(fail(PSX_EHIP, "out of device memory"));
     static_assert(sizeof(SetRec) == sizeof(Acc5), "SetRec occupies one image slot");
     e->dsacc = reinterpret_cast<SetRec*>(e->dacc + e->ldg);
-    e->dflag = reinterpret_cast<int*>(e->dacc + e->ldg + 1);
+    e->dtag = reinterpret_cast<PlanTag*>(e->dacc + e->ldg + 1);
+    e->dflag = reinterpret_cast<int*>(e->dacc + e->ldg + 2);
     e->plans.d_flag = e->dflag;
     e->plans.own_flag = false;
     hipMemcpyAsync(e->dpres, e->pres.data(), e->ldg, hipMemcpyHostToDevice, e->stream);
@@ -1539,12 +1662,18 @@ int create_impl(const psx_problem* p, const psx_ld_problem* ld, int device, psx_
         dp.y[s] = e->dy[s];
     }
     dp.pres = e->dpres;
-    if (hipMemsetAsync(e->dacc, 0, sizeof(Acc5) * ((size_t)e->ldg + 2), e->stream) != hipSuccess)
+    if (hipMemsetAsync(e->dacc, 0, sizeof(Acc5) * ((size_t)e->ldg + 3), e->stream) != hipSuccess)
         return bail(fail(PSX_EHIP, "memset"));
+    if (write_tag(e)) return bail(PSX_EHIP);
     if (reset_acc(e)) return bail(PSX_EHIP);
     if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(fail(PSX_EHIP, "create sync"));
     std::memset(&e->timing, 0, sizeof(e->timing));
-    if (info) info->setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count();
+    if (info) {
+        info->setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count();
+        info->alloc_ms = alloc_ms;
+        info->studies_ms = studies_ms;
+        info->tail_ms = since(tc);
+    }
     *out = e;
     return 0;
 }
@@ -1601,11 +1730,11 @@ int psx_warmup_for(int device, int32_t max_causal, int32_t configs_file) {
     t[1] = now();
     // one launch loads this translation unit's device code
     double* d = nullptr;
-    HIPCHK(hipMalloc(&d, 64 * sizeof(double)));
+    HIPCHK(psx::dmalloc(&d, 64 * sizeof(double)));
     hipLaunchKernelGGL(k_diag, dim3(1), dim3(64), 0, nullptr, d, 8, d + 8);
     hipError_t le = hipGetLastError();
     hipError_t se = hipDeviceSynchronize();
-    hipFree(d);
+    psx::dfree(d);
     if (le != hipSuccess || se != hipSuccess)
         return fail(PSX_EHIP, std::string("warm-up: ") + hipGetErrorString(le != hipSuccess ? le : se));
     t[2] = now();
@@ -1615,7 +1744,8 @@ int psx_warmup_for(int device, int32_t max_causal, int32_t configs_file) {
     // the largest) only for a -b run
     if (psx::warm_module_setup()) return fail(PSX_EHIP, "warm-up: setup device code did not load");
     t[3] = now();
-    if (psx::warm_module_sweep()) return fail(PSX_EHIP, "warm-up: sweep device code did not load");
+    if (psx::warm_module_sweep() || psx::warm_module_plan())
+        return fail(PSX_EHIP, "warm-up: sweep device code did not load");
     t[4] = now();
     if (max_causal >= 3 && psx::warm_module_sweep3()) return fail(PSX_EHIP, "warm-up: k = 3 device code did not load");
     t[5] = now();
@@ -1639,17 +1769,29 @@ int psx_lu_det_gpu(const double* a, int32_t m, int device, double* det) {
     double* dd = nullptr;
     int* ds = nullptr;
     const size_t nn = (size_t)m * m;
-    if (hipMalloc(&dA, nn * sizeof(double)) != hipSuccess || hipMalloc(&dd, m * sizeof(double)) != hipSuccess ||
-        hipMalloc(&ds, m * sizeof(int)) != hipSuccess) {
-        hipFree(dA); hipFree(dd); hipFree(ds);
+    if (psx::dmalloc(&dA, nn * sizeof(double)) != hipSuccess || psx::dmalloc(&dd, m * sizeof(double)) != hipSuccess ||
+        psx::dmalloc(&ds, m * sizeof(int)) != hipSuccess) {
+        psx::dfree(dA); psx::dfree(dd); psx::dfree(ds);
         return fail(PSX_EHIP, "out of device memory");
     }
     std::string err;
     rc = 0;
     if (hipMemcpy(dA, a, nn * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) rc = fail(PSX_EHIP, "upload");
     else if (psx::lu_det_device(dA, m, ds, dd, nullptr, det, &err)) rc = fail(PSX_EHIP, err);
-    hipFree(dA); hipFree(dd); hipFree(ds);
+    psx::dfree(dA); psx::dfree(dd); psx::dfree(ds);
     return rc;
+}
+
+int psx_elim_gpu(const double* a, int32_t m, const double* z, int32_t check, double* pivots, double* z_out,
+                 int32_t* swap_needed, int device) {
+    if (!a || m <= 0 || !pivots || !swap_needed || (z && !z_out)) return fail(PSX_EINVAL, "bad argument");
+    int rc;
+    if ((rc = gpu_ready(device))) return rc;
+    std::string err;
+    int sw = 0;
+    if (psx::elim_device(a, m, z, check, pivots, z_out, &sw, &err)) return fail(PSX_EHIP, err);
+    *swap_needed = sw;
+    return 0;
 }
 
 int psx_psd_shift_gpu(double* sigma, int32_t m, double* added, int device) {
@@ -1676,8 +1818,20 @@ void psx_destroy(psx_engine* e) { delete e; }
 
 int psx_set_shard(psx_engine* e, int rank, int world) {
     if (!e || world < 1 || rank < 0 || rank >= world) return fail(PSX_EINVAL, "bad shard");
+    HIPCHK(hipSetDevice(e->dev));
+    const bool moved = rank != e->rank || world != e->world;
     e->rank = rank;
     e->world = world;
+    if (moved && fused_eligible(e)) {  // this shard's plans, built ahead
+        psx::plan_prefetch(e->plans, e->dev, 2, e->U, e->ldg, rank, world, false);
+        if (e->maxc == 3) psx::plan_prefetch(e->plans, e->dev, 3, e->U, e->ldg, rank, world, false);
+    }
+    return write_tag(e);
+}
+
+int psx_plan_hash(psx_engine* e, uint64_t* hash) {
+    if (!e || !hash) return fail(PSX_EINVAL, "bad argument");
+    *hash = plan_hash(e);
     return 0;
 }
 
@@ -1691,21 +1845,26 @@ int psx_reset(psx_engine* e) {
 
 int psx_run_exhaustive(psx_engine* e) {
     HIPCHK(hipSetDevice(e->dev));
+    const auto t0 = std::chrono::steady_clock::now();
     int rc;
     std::memset(&e->timing, 0, sizeof(e->timing));
+    e->prep_ms = 0;
     double gms = 0;
     int flag = 0;
     if (fused_eligible(e)) {
         if ((rc = fused_pass(e, &flag))) return rc;
     } else {
         if ((rc = exhaustive_pass(e, false, &gms))) return rc;
-        flag = *(const int*)(e->hstat + sizeof(SetRec));
+        flag = *(const int*)(e->hstat + 2 * sizeof(SetRec));
     }
     if (flag) {  // some set's notSharedLL group sits > 900 bits below its maximum: exact variant
         if ((rc = exhaustive_pass(e, true, &gms))) return rc;
         HIPCHK(hipMemsetAsync(e->dflag + 1, 0, sizeof(int), e->stream));  // handled: clear the sticky copy
     }
-    return fill_timing(e, gms, flag);
+    if ((rc = fill_timing(e, gms, flag))) return rc;
+    e->timing.prepare_ms = e->prep_ms;
+    e->timing.run_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
 }
 
 int psx_run_exhaustive_async(psx_engine* e) {
@@ -1723,6 +1882,9 @@ int psx_sync(psx_engine* e, int32_t* exact_needed) {
     HIPCHK(hipMemcpyAsync(&sticky, e->dflag + 1, sizeof(int), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemsetAsync(e->dflag + 1, 0, sizeof(int), e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
+    if (*(const int*)(e->hstat + 2 * sizeof(SetRec) + kPlanMismatchWord * sizeof(int)))
+        return fail(PSX_EINVAL, "merged partial images are not shards 0..world-1 of one plan "
+                                "(ranks with different PSX_K3_* knobs, builds or shard settings)");
     if (exact_needed) *exact_needed = sticky;
     if (e->a_pending == 0 && e->a_count == 0) {
         // nothing asynchronous since the last sync: the count still follows the
@@ -1853,7 +2015,7 @@ int psx_run_configs(psx_engine* e, const int16_t* rows, int64_t n_rows, int32_t 
                 if (e->u2l[s * e->U + u] >= 0) maps.push_back(u);  // local order = union order (Invariant)
         if ((int)maps.size() != e->N) return fail(PSX_EINVAL, "snp map does not cover the studies");
         maps.insert(maps.end(), e->u2l.begin(), e->u2l.end());
-        HIPCHK(hipMalloc(&e->d_cfg_maps, maps.size() * sizeof(int)));
+        HIPCHK(psx::dmalloc(&e->d_cfg_maps, maps.size() * sizeof(int)));
         HIPCHK(hipMemcpy(e->d_cfg_maps, maps.data(), maps.size() * sizeof(int), hipMemcpyHostToDevice));
     }
     psx::CfgMaps C{e->d_cfg_maps, e->d_cfg_maps + e->N, e->U, e->N, e->m[0], e->m[1]};
@@ -2237,16 +2399,16 @@ struct SssDev {
     int* hmark = nullptr;     // pinned host: per neighbour, its mark (one rank)
     double* hscore = nullptr; // pinned host: gathered item scores (world > 1)
     ~SssDev() {
-        hipFree(T);
-        hipFree(rows);
-        hipFree(mark);
-        hipFree(cnt);
-        hipFree(full);
-        if (lk) hipHostFree(lk);
-        if (shost) hipHostFree(shost);
-        if (hcnt) hipHostFree(hcnt);
-        if (hmark) hipHostFree(hmark);
-        if (hscore) hipHostFree(hscore);
+        psx::dfree(T);
+        psx::dfree(rows);
+        psx::dfree(mark);
+        psx::dfree(cnt);
+        psx::dfree(full);
+        if (lk) psx::hfree(lk);
+        if (shost) psx::hfree(shost);
+        if (hcnt) psx::hfree(hcnt);
+        if (hmark) psx::hfree(hmark);
+        if (hscore) psx::hfree(hscore);
         for (int i = 0; i < 2 * kRingE; i++)
             if (ev[i]) hipEventDestroy(ev[i]);
     }
@@ -2261,37 +2423,37 @@ int sss_workspace(psx_engine* e, size_t nmax, int world, hipStream_t s) {
     SssDev& D = *e->sss;
     if (!D.cnt) {
         for (int i = 0; i < 2 * SssDev::kRingE; i++) HIPCHK(hipEventCreate(&D.ev[i]));
-        HIPCHK(hipMalloc(&D.cnt, kNCnt * sizeof(int)));
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.shost), sizeof(SetRec)));
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hcnt), kNCnt * sizeof(int)));
+        HIPCHK(psx::dmalloc(&D.cnt, kNCnt * sizeof(int)));
+        HIPCHK(psx::hmalloc(reinterpret_cast<void**>(&D.shost), sizeof(SetRec)));
+        HIPCHK(psx::hmalloc(reinterpret_cast<void**>(&D.hcnt), kNCnt * sizeof(int)));
     }
     if (D.nmax < nmax) {
-        hipFree(D.rows); hipFree(D.mark);
-        if (D.lk) hipHostFree(D.lk);
-        if (D.hmark) hipHostFree(D.hmark);
+        psx::dfree(D.rows); psx::dfree(D.mark);
+        if (D.lk) psx::hfree(D.lk);
+        if (D.hmark) psx::hfree(D.hmark);
         D.rows = D.mark = D.hmark = nullptr;
         D.lk = nullptr;
-        HIPCHK(hipMalloc(&D.rows, nmax * PSX_KMAX * sizeof(int)));
-        HIPCHK(hipMalloc(&D.mark, nmax * sizeof(int)));
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.lk), nmax * sizeof(double)));
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hmark), nmax * sizeof(int)));
+        HIPCHK(psx::dmalloc(&D.rows, nmax * PSX_KMAX * sizeof(int)));
+        HIPCHK(psx::dmalloc(&D.mark, nmax * sizeof(int)));
+        HIPCHK(psx::hmalloc(reinterpret_cast<void**>(&D.lk), nmax * sizeof(double)));
+        HIPCHK(psx::hmalloc(reinterpret_cast<void**>(&D.hmark), nmax * sizeof(int)));
         D.nmax = nmax;
     }
     if (world > 1 && D.nmax_full < nmax) {
-        hipFree(D.full);
-        if (D.hscore) hipHostFree(D.hscore);
+        psx::dfree(D.full);
+        if (D.hscore) psx::hfree(D.hscore);
         D.full = nullptr;
         D.hscore = nullptr;
-        HIPCHK(hipMalloc(&D.full, nmax * sizeof(double)));
-        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.hscore), nmax * sizeof(double)));
+        HIPCHK(psx::dmalloc(&D.full, nmax * sizeof(double)));
+        HIPCHK(psx::hmalloc(reinterpret_cast<void**>(&D.hscore), nmax * sizeof(double)));
         D.nmax_full = nmax;
     }
     size_t cap = 1 << 16;
     while (cap < 4 * nmax) cap <<= 1;
     if (D.cap < cap) {
-        hipFree(D.T);
+        psx::dfree(D.T);
         D.T = nullptr;
-        HIPCHK(hipMalloc(&D.T, cap * sizeof(MapEntry)));
+        HIPCHK(psx::dmalloc(&D.T, cap * sizeof(MapEntry)));
         D.cap = cap;
     }
     HIPCHK(hipMemsetAsync(D.T, 0, D.cap * sizeof(MapEntry), s));
@@ -2357,13 +2519,13 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
             size_t nc = D.cap;
             while (2 * (D.used + (size_t)n_nbd + 1) > nc) nc <<= 1;
             MapEntry* nt = nullptr;
-            HIPCHK(hipMalloc(&nt, nc * sizeof(MapEntry)));
+            HIPCHK(psx::dmalloc(&nt, nc * sizeof(MapEntry)));
             HIPCHK(hipMemsetAsync(nt, 0, nc * sizeof(MapEntry), e->stream));
             hipLaunchKernelGGL(k_map_rehash, dim3((unsigned)((D.cap + 255) / 256)), dim3(256), 0, e->stream, D.T,
                                D.cap, nt, (unsigned long long)(nc - 1));
             HIPCHK(hipGetLastError());
             HIPCHK(hipStreamSynchronize(e->stream));
-            hipFree(D.T);
+            psx::dfree(D.T);
             D.T = nt;
             D.cap = nc;
         }
@@ -2548,12 +2710,12 @@ int psx_get_accum(psx_engine* e, psx_accum* out) {
     return 0;
 }
 
-int64_t psx_partials_bytes(psx_engine* e) { return (int64_t)(sizeof(Acc5) * ((size_t)e->ldg + 1)); }
+int64_t psx_partials_bytes(psx_engine* e) { return (int64_t)(sizeof(Acc5) * ((size_t)e->ldg + 2)); }
 
 int psx_export_partials(psx_engine* e, void* dst) {
     HIPCHK(hipSetDevice(e->dev));
-    // per-SNP slots and the SetRec slot are contiguous: the image is one copy
-    HIPCHK(hipMemcpyAsync(dst, e->dacc, sizeof(Acc5) * ((size_t)e->ldg + 1), hipMemcpyDeviceToDevice, e->stream));
+    // per-SNP slots, the SetRec slot and the PlanTag are contiguous: the image is one copy
+    HIPCHK(hipMemcpyAsync(dst, e->dacc, sizeof(Acc5) * ((size_t)e->ldg + 2), hipMemcpyDeviceToDevice, e->stream));
     if (!e->external_stream) HIPCHK(hipStreamSynchronize(e->stream));
     return 0;
 }
@@ -2578,25 +2740,36 @@ int psx_merge_partials(psx_engine* e, const void* src, int32_t count) {
     hipLaunchKernelGGL(k_merge_partials, dim3((e->U + 63) / 64), dim3(64), 0, e->stream, (const Acc5*)src, e->U,
                        e->ldg, count, e->dacc, e->dsacc, e->dflag);
     HIPCHK(hipGetLastError());
-    if (!e->external_stream) HIPCHK(hipStreamSynchronize(e->stream));
-    return 0;
+    if (e->external_stream) return 0;  // a tag mismatch is reported by psx_sync
+    return check_plan_mismatch(e);
 }
 
 int psx_fold_partials_host(const void* src, int32_t count, int64_t image_bytes, void* dst) {
-    if (count < 1 || image_bytes < (int64_t)(2 * sizeof(Acc5)) || image_bytes % (int64_t)sizeof(Acc5) != 0)
+    if (count < 1 || image_bytes < (int64_t)(3 * sizeof(Acc5)) || image_bytes % (int64_t)sizeof(Acc5) != 0)
         return fail(PSX_EINVAL, "bad partial image size");
-    const size_t n = (size_t)image_bytes / sizeof(Acc5);  // ldg Acc5 slots + 1 SetRec slot
+    const size_t n = (size_t)image_bytes / sizeof(Acc5);  // ldg Acc5 slots + 1 SetRec slot + 1 PlanTag slot
     const Acc5* parts = (const Acc5*)src;
+    const PlanTag& t0 = *reinterpret_cast<const PlanTag*>(parts + n - 1);
+    for (int r = 0; r < count; r++) {
+        const PlanTag& t = *reinterpret_cast<const PlanTag*>(parts + (size_t)r * n + n - 1);
+        if (t.magic != kPlanMagic || t.hash != t0.hash || t.world != count || t.rank != r)
+            return fail(PSX_EINVAL, "partial images are not shards 0.." + std::to_string(count - 1) +
+                                        " of one plan (PlanTag of rank " + std::to_string(r) + ")");
+    }
     std::vector<Acc5> out(n);
     std::memset(out.data(), 0, n * sizeof(Acc5));
-    for (size_t u = 0; u + 1 < n; u++) {
+    for (size_t u = 0; u + 2 < n; u++) {
         Acc5 a = {0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0, 0.0};
         for (int r = 0; r < count; r++) psx::fold_acc(a, parts[(size_t)r * n + u]);
         out[u] = a;
     }
     SetRec s = psx::set_zero();
-    for (int r = 0; r < count; r++) psx::fold_set(s, *reinterpret_cast<const SetRec*>(parts + (size_t)r * n + n - 1));
-    std::memcpy(&out[n - 1], &s, sizeof(SetRec));
+    for (int r = 0; r < count; r++) psx::fold_set(s, *reinterpret_cast<const SetRec*>(parts + (size_t)r * n + n - 2));
+    std::memcpy(&out[n - 2], &s, sizeof(SetRec));
+    PlanTag t = t0;  // the fold is a whole-plan image of world 1
+    t.world = 1;
+    t.rank = 0;
+    std::memcpy(&out[n - 1], &t, sizeof(PlanTag));
     std::memcpy(dst, out.data(), n * sizeof(Acc5));
     return 0;
 }
@@ -2636,6 +2809,36 @@ int psx_shard_stats(const psx_problem* p, int32_t k, int32_t rank, int32_t world
     }
     if (union_sets) *union_sets = (uint64_t)(sets + 0.5);
     if (configs) *configs = cfg;
+    return 0;
+}
+
+int psx_plan_csr_selftest(int32_t n_union, const uint8_t* presence, int32_t k, int32_t rank, int32_t world,
+                          int32_t variant, int device, int64_t* mismatches, int64_t* records) {
+    if (n_union < 3 || (k != 2 && k != 3) || (variant && k != 3) || world < 1 || rank < 0 || rank >= world ||
+        !mismatches || !records)
+        return fail(PSX_EINVAL, "bad arguments");
+    int rc;
+    if ((rc = gpu_ready(device))) return rc;
+    const int ldg = (n_union + 63) / 64 * 64;
+    std::vector<unsigned char> pres(ldg, 0);
+    for (int u = 0; u < n_union; u++) pres[u] = presence ? presence[u] : 3;
+    long bad = 0, nrec = 0;
+    if (psx::plan_csr_selftest(n_union, pres.data(), k, rank, world, variant, &bad, &nrec))
+        return fail(PSX_EHIP, psx::sweep_error());
+    *mismatches = bad;
+    *records = nrec;
+    return 0;
+}
+
+int psx_plan_build_ms(int32_t n_union, int32_t k, int32_t rank, int32_t world, double* ms, int32_t* n_units,
+                      int64_t* n_records) {
+    if (n_union < 3 || (k != 2 && k != 3) || world < 1 || rank < 0 || rank >= world || !ms || !n_units || !n_records)
+        return fail(PSX_EINVAL, "bad arguments");
+    long nr = 0;
+    int nu = 0;
+    if (psx::plan_host_ms(n_union, k, rank, world, ms, &nu, &nr)) return fail(PSX_EINVAL, psx::sweep_error());
+    *n_units = nu;
+    *n_records = nr;
     return 0;
 }
 

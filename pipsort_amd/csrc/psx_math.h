@@ -52,7 +52,18 @@ struct SetRec {
     double npat;   // configurations folded in (exact integer in a double)
 };
 
-static_assert(sizeof(Acc5) == 56 && sizeof(SetRec) == 56, "partial-image slot layout");
+// Last slot of a partial image: which shard of which plan the image holds.  A
+// merge folds images in rank order and refuses a set whose tags disagree (a
+// rank that cut another plan — other PSX_K3_* knobs, another build — would
+// leave configurations uncounted or counted twice).
+constexpr int32_t kPlanMagic = 0x54585350;  // "PSXT"
+struct PlanTag {
+    int32_t magic, world, rank, U;
+    uint64_t hash;  // U, ldg, c, presence bits, world and the plan knobs (rank excluded)
+    uint64_t pad[4];
+};
+
+static_assert(sizeof(Acc5) == 56 && sizeof(SetRec) == 56 && sizeof(PlanTag) == 56, "partial-image slot layout");
 
 __host__ __device__ inline int imax(int a, int b) { return a > b ? a : b; }
 

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/pipsort_engine.h"
+#include "psx_mem.h"
 
 namespace {
 
@@ -256,7 +257,7 @@ int create_multi(const int32_t* devices, int32_t n, psx_multi** out, Create crea
         if (r || n == 1) return r;
         // the shard's export / merge stream (only enqueue there) and its event
         if (hipSetDevice(m->dev[i]) != hipSuccess ||
-            hipStreamCreateWithFlags(&m->st[i], hipStreamNonBlocking) != hipSuccess ||
+            psx::stream_get(&m->st[i], 0) != hipSuccess ||
             hipEventCreateWithFlags(&m->exported[i], hipEventDisableTiming) != hipSuccess)
             return PSX_EHIP;
         return psx_set_stream(m->h[i], m->st[i]);
@@ -281,7 +282,7 @@ int create_multi(const int32_t* devices, int32_t n, psx_multi** out, Create crea
         }
         if (!rc) {
             m->bytes = psx_partials_bytes(m->h[0]);
-            if (hipSetDevice(m->dev[0]) != hipSuccess || hipMalloc(&m->gathered, (size_t)m->bytes * n) != hipSuccess) {
+            if (hipSetDevice(m->dev[0]) != hipSuccess || psx::dmalloc(&m->gathered, (size_t)m->bytes * n) != hipSuccess) {
                 g_multi_err = "out of device memory (partial images)";
                 rc = PSX_EHIP;
             }
@@ -322,11 +323,11 @@ void psx_multi_destroy(psx_multi* m) {
         }
         hipSetDevice(m->dev[i]);
         if (m->exported[i]) hipEventDestroy(m->exported[i]);
-        if (m->st[i]) hipStreamDestroy(m->st[i]);
+        if (m->st[i]) psx::stream_put(m->st[i], 0);
     }
     if (m->gathered) {
         hipSetDevice(m->dev[0]);
-        hipFree(m->gathered);
+        psx::dfree(m->gathered);
     }
     delete m->pool;
     delete m;

@@ -16,12 +16,20 @@ struct LdStudyResult {
     double min_pivot_ratio;   // min L D L^T pivot / max |diag|
     double spsq;              // path 0: ||S'_s||^2 = z^T Sigma'^-1 z
     int fused_route;          // 1: swap-free LU of a symmetric LD carried step 2 (one elimination)
+    double upload_ms, psd_ms, finish_ms;  // wall time of the phases (LD upload, PSD loop, step 2 + readback)
 };
 
 // Partial-pivot LU determinant of the device matrix dA (n x n row-major,
 // destroyed), bit-identical to the host restatement (model.cpp lu_det).
 // dswp: n ints, ddiag: n doubles of device scratch.
 int lu_det_device(double* dA, int n, int* dswp, double* ddiag, hipStream_t st, double* det, std::string* err);
+
+// The setup's swap-free elimination (k_lu_diag + k_lu_tile) of the host matrix
+// a (n x n row-major) with z's forward solve (z may be null): pivots U_ii ->
+// piv, z~ -> zt (when z), *swap = 1 when check and some column needed a row
+// swap (piv / zt are then meaningless).  For parity tests (psx_elim_gpu).
+int elim_device(const double* a, int n, const double* z, int check, double* piv, double* zt, int* swap,
+                std::string* err);
 
 // One study: LD (host, row-major M x M as parsed, util.cpp:86-96) and z (host,
 // M) -> dS = Sigma~_s (device, row-major M x M) and dy = y_s (device, M).

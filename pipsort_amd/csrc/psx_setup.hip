@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -39,6 +40,7 @@
 #include <vector>
 
 #include "psx_setup.h"
+#include "psx_mem.h"
 
 namespace psx {
 
@@ -129,153 +131,226 @@ __global__ __launch_bounds__(kElimCols) void k_elim(double* __restrict__ A, int 
     }
 }
 
-// Swap-free elimination, blocked with delayed updates (LD matrices: the
+// Swap-free elimination, tiled with delayed updates (LD matrices: the
 // diagonal stays the column maximum, so no row is ever swapped).  Element
 // (i, k) of the right-looking elimination receives, for every step q <
 // min(i, k), a_ik <- a_ik - l_iq * u_qk (multiply and subtract not fused), in
-// increasing q.  Delaying the updates of columns beyond a kPanel-wide panel
-// and applying them later, still in increasing q and with the same l_iq and
-// u_qk, gives every element — U_ii, z~ — bit for bit what the per-column
-// elimination gives, at one read-modify-write of the trailing matrix per
-// panel instead of per column.
-//   k_lu_panel  (one workgroup): steps j0 .. j0 + nb - 1 on the panel columns
-//               and z; l_iq kept in Lp[q - j0][i]; a row swap (GSL's pivot, the
-//               first row of maximal |a_iq| with NaNs never chosen, would not be
-//               row q) raises *flag and every later launch returns at once (the
-//               caller reruns the pivoting path from a fresh copy); a_qq == 0
-//               skips the step (GSL), marked in sk[q - j0].
-//               Then the panel's U rows on the trailing columns (row j0 + r
-//               takes steps j0 .. j0 + r - 1, one column per thread).
-//   k_lu_trail  the panel's nb updates on rows and columns >= j0 + nb,
-//               kTrRows rows per block (kTrRows / kTrGroups independent rows
-//               per thread), l from LDS.
-constexpr int kPanel = 16;
+// increasing q.  Any schedule that applies those updates in increasing q with
+// the same l_iq and u_qk gives every element — U_ii, z~ — bit for bit what the
+// per-column elimination gives.  Without pivoting the panel factorisation is
+// row-local once its nb x nb diagonal block D is factored: row i's panel
+// entries take l_iq = a_iq / u_qq and a_ic -= l_iq u_qc (c > q in the panel),
+// and column k's U entries take u_rk -= l_rq u_qk (q < r, l from D).  So one
+// launch per panel does everything (k_lu_tile), one 64 x 64 tile of the
+// trailing matrix per block:
+//   wave 0  the L chain of the tile's 64 rows (lane = row, the row's panel
+//           entries in registers, u_qq / u_qc broadcast from LDS), the swap
+//           check of those rows (GSL's pivot: the first row of maximal |a_iq|,
+//           NaNs never chosen — a row swap is needed iff some |a_iq| > |u_qq|,
+//           i > q; *flag is raised and the caller reruns the pivoting path
+//           from a fresh copy) and, in column-tile 0 blocks, z's forward solve;
+//   wave 1  the U-row solve of the tile's 64 columns (lane = column);
+//   all     the panel's nb delayed updates of the tile (16 rows per wave),
+//           whose loads were issued at the top of the kernel;
+//   block (0, 0) then factors the NEXT panel's diagonal block (the top-left
+//           corner of its own tile, already updated) in one wave's registers
+//           and publishes it (k_lu_diag for the first panel).
+// L and U of the panels are recomputed per tile (redundantly across tiles,
+// identically), never stored: the setup consumes U_ii and z~ only.  A ends with
+// every diagonal block factored in place (U_ii on the diagonal).  A zero u_qq
+// skips step q (GSL), as a bit in the block's skip mask.
+constexpr int kPanel = 16;     // panel width (k_lu_tile, k_lu_panel_piv)
 constexpr int kPanelThreads = 1024;
+constexpr int kTile = 64;      // trailing tile edge (k_lu_tile): lane = column
+constexpr int kTileWaves = 4;  // rows kTile / kTileWaves per wave in the update
 constexpr int kTrCols = 64;
 constexpr int kTrRows = 32;
 constexpr int kTrGroups = 4;  // row groups per trailing block (kTrRows / kTrGroups rows per thread)
-constexpr int kPanelLds = 152 * 1024;  // dynamic LDS budget of k_lu_panel_lds (160 KB per CU; 158 KB is refused)
+constexpr int kPanelLds = 152 * 1024;  // dynamic LDS budget of k_lu_panel_piv (160 KB per CU; 158 KB is refused)
 
-__global__ __launch_bounds__(kPanelThreads) void k_lu_panel(double* __restrict__ A, int n, int j0, int nb,
-                                                            double* __restrict__ Lp, double* __restrict__ sk,
-                                                            int* __restrict__ flag, double* __restrict__ z) {
-#pragma clang fp contract(off)
-    if (*flag) return;
-    const int t = threadIdx.x;
-    for (int q = j0; q < j0 + nb; q++) {
-        const double aqq = A[(size_t)q * n + q];
-        const double mq = fabs(aqq);
-        bool swap = false;
-        if (aqq == aqq)
-            for (int i = q + 1 + t; i < n; i += kPanelThreads) swap |= fabs(A[(size_t)i * n + q]) > mq;
-        if (__syncthreads_or(swap)) {
-            if (t == 0) *flag = 1;
-            return;
-        }
-        if (t == 0) sk[q - j0] = (aqq == 0.0) ? 1.0 : 0.0;
-        if (aqq == 0.0) continue;  // uniform
-        const double zq = z[q];
-        double* const lq = Lp + (size_t)(q - j0) * n;
-        for (int i = q + 1 + t; i < n; i += kPanelThreads) {  // one row per thread
-            const double l = A[(size_t)i * n + q] / aqq;
-            lq[i] = l;
-            const double prod = l * zq;
-            z[i] = z[i] - prod;
-            for (int k = q + 1; k < j0 + nb; k++) {  // panel columns right of q
-                const double pk = l * A[(size_t)q * n + k];
-                double* const p = A + (size_t)i * n + k;
-                *p = *p - pk;
-            }
-        }
-        __syncthreads();
-    }
-    __syncthreads();
-    // the panel's U rows on the trailing columns: row j0 + r takes steps j0 .. j0 + r - 1
-    for (int k = j0 + nb + t; k < n; k += kPanelThreads) {
-        double u[kPanel];
-#pragma unroll
-        for (int r = 0; r < kPanel; r++) {
-            if (r >= nb) break;
-            double v = A[(size_t)(j0 + r) * n + k];
-#pragma unroll
-            for (int q = 0; q < r; q++) {
-                if (sk[q] != 0.0) continue;
-                const double prod = Lp[(size_t)q * n + j0 + r] * u[q];
-                v = v - prod;
-            }
-            u[r] = v;
-            if (r > 0) A[(size_t)(j0 + r) * n + k] = v;
-        }
-    }
+// a published diagonal block: a[kPanel][kPanel] packed LU (row-major, l below
+// the diagonal, u on and above), z[kPanel] (final), skip mask (bit q: u_qq == 0)
+constexpr int kDblk = kPanel * kPanel + kPanel + 1;
+
+__device__ inline double rdlane(double v, int l) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 
-// k_lu_panel with the panel rows j0 .. n - 1 and z[j0 .. n - 1] held in LDS
-// (dynamic, (n - j0) x (nb + 2) doubles: rows padded to nb + 1, then z): the same operations on the same
-// values, one global round trip in and out instead of several per step.
-__global__ __launch_bounds__(kPanelThreads) void k_lu_panel_lds(double* __restrict__ A, int n, int j0, int nb,
-                                                                double* __restrict__ Lp, double* __restrict__ sk,
-                                                                int* __restrict__ flag, double* __restrict__ z,
-                                                                int check) {
+// Factor the nb x nb diagonal block at (j, j) held in one wave's registers
+// (lane r < nb: row j + r, v[c] = a_{j+r, j+c} after every earlier panel's
+// updates, zr = z_{j+r} likewise) with the per-column elimination's operations;
+// rows of the block below q are checked for a needed swap.  Writes the block
+// back to A (in place), the published copy to dblk, z to z.
+__device__ void factor_diag(double (&v)[kPanel], double zr, int j, int nb, double* __restrict__ A, int n,
+                            double* __restrict__ z, double* __restrict__ dblk, int check, int* __restrict__ flag) {
 #pragma clang fp contract(off)
-    __shared__ double sT[kPanel][kPanel];  // l of the panel's own rows (the U-row solve)
-    __shared__ double sSk[kPanel];
-    extern __shared__ double sP[];
-    if (*flag) return;
-    const int t = threadIdx.x;
-    const int R = n - j0;
-    const int ls = nb + 1;  // LDS row stride: odd in doubles, so a wave's rows spread over the banks
-    double* const sZ = sP + (size_t)R * ls;  // z[j0 .. n - 1]
-    for (int e = t; e < R * nb; e += kPanelThreads) sP[(e / nb) * ls + e % nb] = A[(size_t)(j0 + e / nb) * n + j0 + e % nb];
-    for (int r = t; r < R; r += kPanelThreads) sZ[r] = z[j0 + r];
-    __syncthreads();
-    for (int qq = 0; qq < nb; qq++) {
-        const double aqq = sP[qq * ls + qq];
-        const double mq = fabs(aqq);
-        bool swap = false;
-        if (check && aqq == aqq)
-            for (int r = qq + 1 + t; r < R; r += kPanelThreads) swap |= fabs(sP[r * ls + qq]) > mq;
-        if (__syncthreads_or(swap)) {
-            if (t == 0) *flag = 1;
-            return;
-        }
-        if (t == 0) sk[qq] = sSk[qq] = (aqq == 0.0) ? 1.0 : 0.0;
-        if (aqq == 0.0) continue;  // uniform
-        const double zq = sZ[qq];
-        double* const lq = Lp + (size_t)qq * n + j0;
-        for (int r = qq + 1 + t; r < R; r += kPanelThreads) {  // one row per thread
-            const double l = sP[r * ls + qq] / aqq;
-            lq[r] = l;
-            if (r < nb) sT[qq][r] = l;
-            const double prod = l * zq;
-            sZ[r] = sZ[r] - prod;
-            for (int c = qq + 1; c < nb; c++) {
-                const double pc = l * sP[qq * ls + c];
-                sP[r * ls + c] = sP[r * ls + c] - pc;
+    const int r = threadIdx.x & 63;
+    const bool row = r < nb;
+    unsigned long long skip = 0;
+    bool sw = false;
+#pragma unroll
+    for (int q = 0; q < kPanel; q++) {
+        const double uqq = rdlane(v[q], q);
+        if (q < nb) {  // uniform (nb < kPanel only for the last block)
+            if (check && uqq == uqq && row && r > q && fabs(v[q]) > fabs(uqq)) sw = true;
+            if (uqq == 0.0) {  // uniform: step q is skipped
+                skip |= 1ull << q;
+            } else {
+                const double zq = rdlane(zr, q);
+                double uq[kPanel];
+#pragma unroll
+                for (int c = q + 1; c < kPanel; c++) uq[c] = rdlane(v[c], q);
+                if (row && r > q) {
+                    const double l = v[q] / uqq;
+                    v[q] = l;
+                    const double pz = l * zq;
+                    zr = zr - pz;
+#pragma unroll
+                    for (int c = q + 1; c < kPanel; c++) {
+                        const double p = l * uq[c];
+                        v[c] = v[c] - p;
+                    }
+                }
             }
         }
-        __syncthreads();
+    }
+    if (check && __any(sw) && r == 0) *flag = 1;
+    if (row) {
+#pragma unroll
+        for (int c = 0; c < kPanel; c++)
+            if (c < nb) {
+                A[(size_t)(j + r) * n + j + c] = v[c];
+                dblk[r * kPanel + c] = v[c];
+            }
+        dblk[kPanel * kPanel + r] = zr;
+        if (z) z[j + r] = zr;
+    }
+    if (r == 0) dblk[kPanel * kPanel + kPanel] = __builtin_bit_cast(double, skip);
+}
+
+// the first panel's diagonal block (one wave)
+__global__ __launch_bounds__(64) void k_lu_diag(double* __restrict__ A, int n, int nb, double* __restrict__ z,
+                                                double* __restrict__ dblk, int check, int* __restrict__ flag) {
+    const int r = threadIdx.x;
+    double v[kPanel];
+#pragma unroll
+    for (int c = 0; c < kPanel; c++) v[c] = (r < nb && c < nb) ? A[(size_t)r * n + c] : 0.0;
+    const double zr = (z && r < nb) ? z[r] : 0.0;
+    factor_diag(v, zr, 0, nb, A, n, z, dblk, check, flag);
+}
+
+// One panel (columns j0 .. j0 + kPanel - 1, diagonal block factored in din) on the
+// trailing tile (rows i0 .. i0 + 63, columns k0 .. k0 + 63; i0, k0 >= j1 =
+// j0 + nb); block (0, 0) then factors the next panel's diagonal block (nbn
+// columns from j1) into dout.
+__global__ __launch_bounds__(kTile * kTileWaves) void k_lu_tile(double* __restrict__ A, int n, int j0, int nbn,
+                                                                double* __restrict__ z, const double* __restrict__ din,
+                                                                double* __restrict__ dout, int check,
+                                                                int* __restrict__ flag) {
+#pragma clang fp contract(off)
+    constexpr int kRows = kTile / kTileWaves;
+    __shared__ double sD[kPanel][kPanel + 1];  // D: l below, u on and above
+    __shared__ double sZ[kPanel];
+    __shared__ double sL[kTile][kPanel + 1];  // l of the tile's rows
+    __shared__ double sU[kPanel][kTile];      // u of the tile's columns
+    __shared__ double sN[kPanel][kPanel + 1];  // block (0, 0): the next diagonal block
+    if (check && *flag) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    constexpr int nb = kPanel;  // every panel with a trailing matrix is full width
+    const int j1 = j0 + nb;
+    const int i0 = j1 + blockIdx.y * kTile, k0 = j1 + blockIdx.x * kTile;
+    const int k = k0 + lane;
+    const bool corner = blockIdx.x == 0 && blockIdx.y == 0;
+    // the update's operands first: their latency hides behind the chains
+    double t[kRows];
+#pragma unroll
+    for (int m = 0; m < kRows; m++) {
+        const int i = i0 + w * kRows + m;
+        t[m] = (i < n && k < n) ? A[(size_t)i * n + k] : 0.0;
+    }
+    const unsigned long long skip = __builtin_bit_cast(unsigned long long, din[kPanel * kPanel + kPanel]);
+    double v[kPanel];  // wave 0: the row's panel entries; wave 1: the column's panel rows
+    const int i = i0 + lane;
+    double zi = 0.0;
+    if (w == 0) {
+#pragma unroll
+        for (int c = 0; c < kPanel; c++) v[c] = (i < n && c < nb) ? A[(size_t)i * n + j0 + c] : 0.0;
+        if (z && blockIdx.x == 0 && i < n) zi = z[i];
+    } else if (w == 1) {
+#pragma unroll
+        for (int c = 0; c < kPanel; c++) v[c] = (k < n && c < nb) ? A[(size_t)(j0 + c) * n + k] : 0.0;
+    } else {
+        for (int e = threadIdx.x - 128; e < kPanel * kPanel; e += 128) sD[e / kPanel][e % kPanel] = din[e];
+        if (threadIdx.x - 128 < kPanel) sZ[threadIdx.x - 128] = din[kPanel * kPanel + threadIdx.x - 128];
     }
     __syncthreads();
-    for (int e = t; e < R * nb; e += kPanelThreads) A[(size_t)(j0 + e / nb) * n + j0 + e % nb] = sP[(e / nb) * ls + e % nb];
-    for (int r = t; r < R; r += kPanelThreads) z[j0 + r] = sZ[r];
-    // the panel's U rows on the trailing columns (l and skip marks from LDS,
-    // the column's nb entries loaded before the triangular solve)
-    for (int k = j0 + nb + t; k < n; k += kPanelThreads) {
-        double u[kPanel];
+    if (w == 0) {  // L chain of row i (+ swap check, + z in column-tile 0)
+        bool sw = false;
 #pragma unroll
-        for (int r = 0; r < kPanel; r++) u[r] = r < nb ? A[(size_t)(j0 + r) * n + k] : 0.0;
+        for (int q = 0; q < kPanel; q++) {
+            const double uqq = sD[q][q];
+            if (check && uqq == uqq && i < n && fabs(v[q]) > fabs(uqq)) sw = true;
+            if ((skip >> q) & 1) {
+                sL[lane][q] = 0.0;
+                continue;
+            }
+            const double l = v[q] / uqq;
+            sL[lane][q] = l;
+            const double pz = l * sZ[q];
+            zi = zi - pz;
+#pragma unroll
+            for (int c = q + 1; c < kPanel; c++) {
+                const double p = l * sD[q][c];
+                v[c] = v[c] - p;
+            }
+        }
+        if (check && __any(sw) && lane == 0) *flag = 1;
+        // z of the rows the next diagonal block factors is written with it
+        if (z && blockIdx.x == 0 && i < n && !(corner && lane < nbn)) z[i] = zi;
+    } else if (w == 1) {  // U-row solve of column k
 #pragma unroll
         for (int r = 1; r < kPanel; r++) {
-            if (r >= nb) break;
 #pragma unroll
             for (int q = 0; q < r; q++) {
-                if (sSk[q] != 0.0) continue;
-                const double prod = sT[q][r] * u[q];
-                u[r] = u[r] - prod;
+                if ((skip >> q) & 1) continue;
+                const double p = sD[r][q] * v[q];
+                v[r] = v[r] - p;
             }
-            A[(size_t)(j0 + r) * n + k] = u[r];
+        }
+#pragma unroll
+        for (int q = 0; q < kPanel; q++) sU[q][lane] = v[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kPanel; q++) {
+        if ((skip >> q) & 1) continue;
+        const double uq = sU[q][lane];
+#pragma unroll
+        for (int m = 0; m < kRows; m++) {
+            const double p = sL[w * kRows + m][q] * uq;
+            t[m] = t[m] - p;
         }
     }
+#pragma unroll
+    for (int m = 0; m < kRows; m++) {
+        const int r = w * kRows + m;
+        const int ii = i0 + r;
+        if (ii >= n || k >= n) continue;
+        if (corner && r < nbn && lane < nbn)
+            sN[r][lane] = t[m];
+        else
+            A[(size_t)ii * n + k] = t[m];
+    }
+    if (!corner || nbn <= 0) return;
+    __syncthreads();
+    if (w != 0) return;
+    double d[kPanel];
+#pragma unroll
+    for (int c = 0; c < kPanel; c++) d[c] = (lane < nbn && c < nbn) ? sN[lane][c] : 0.0;
+    factor_diag(d, zi, j1, nbn, A, n, z, dout, check, flag);
 }
 
 // The partial-pivot elimination (GSL 2.5 gsl_linalg_LU_decomp), blocked the
@@ -467,41 +542,24 @@ int enqueue_lu(double* A, int n, int* dswp, hipStream_t st, std::string* err) {
     return chk(hipGetLastError(), "LU launch", err);
 }
 
-// enqueue the blocked swap-free elimination; *flag != 0 afterwards when some
-// column needed a row swap (A is then partly eliminated: recopy and pivot).
-// work: kPanel * n + kPanel doubles (panel multipliers, skipped-step marks)
-// Returns -1 with *err set when a launch failed (the HIP error is read once,
-// here), 1 when !check and the panel does not fit LDS (nothing enqueued).
+// enqueue the tiled swap-free elimination (k_lu_diag, then one k_lu_tile per
+// panel); with check, *flag != 0 afterwards when some column needed a row swap
+// (A is then partly eliminated: recopy and pivot).  work: 2 * kDblk doubles
+// (the diagonal blocks, double-buffered).  Returns -1 with *err set when a
+// launch failed (the HIP error is read once, here).
 int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipStream_t st, std::string* err,
                      bool check = true) {
     if (chk(hipMemsetAsync(flag, 0, sizeof(int), st), "memset", err)) return -1;
-    double* const sk = work + (size_t)kPanel * n;
-    // panel width: the widest (<= kPanel) whose n rows fit in LDS; the global-
-    // memory panel kernel beyond that.  The attribute is set on every call: it is
-    // per device (a process may drive several) and cheap.
-    int lds_cap = kPanelLds;
-    if (hipFuncSetAttribute((const void*)k_lu_panel_lds, hipFuncAttributeMaxDynamicSharedMemorySize, kPanelLds) !=
-        hipSuccess) {
-        (void)hipGetLastError();
-        lds_cap = 64 * 1024;
-    }
-    int pw = kPanel;
-    while (pw > 1 && (size_t)n * (pw + 2) * sizeof(double) > (size_t)lds_cap) pw--;
-    // PSX_LU_GLOBAL: the global-memory panel kernel at any size (tests)
-    const bool lds = (size_t)n * (pw + 2) * sizeof(double) <= (size_t)lds_cap && !std::getenv("PSX_LU_GLOBAL");
-    if (!check && !lds) return 1;  // no unchecked global-memory panel: the caller eliminates per column
-    if (!lds) pw = kPanel;
-    for (int j0 = 0; j0 < n - 1; j0 += pw) {
-        const int nb = std::min(pw, n - 1 - j0);
-        const int rest = n - j0 - nb;  // trailing columns (and rows), >= 1
-        if (lds)
-            hipLaunchKernelGGL(k_lu_panel_lds, dim3(1), dim3(kPanelThreads), (size_t)(n - j0) * (nb + 2) * sizeof(double), st,
-                               A, n, j0, nb, work, sk, flag, z, check ? 1 : 0);
-        else
-            hipLaunchKernelGGL(k_lu_panel, dim3(1), dim3(kPanelThreads), 0, st, A, n, j0, nb, work, sk, flag, z);
-        hipLaunchKernelGGL(k_lu_trail, dim3((rest + kTrCols - 1) / kTrCols, (rest + kTrRows - 1) / kTrRows),
-                           dim3(kTrCols, kTrGroups), 0, st, A, n, j0, nb, (const double*)work, (const double*)sk,
-                           (const int*)flag);
+    double* const dblk[2] = {work, work + kDblk};
+    hipLaunchKernelGGL(k_lu_diag, dim3(1), dim3(64), 0, st, A, n, std::min(kPanel, n), z, dblk[0], check ? 1 : 0,
+                       flag);
+    int p = 0;
+    for (int j0 = 0; j0 + kPanel < n; j0 += kPanel, p++) {
+        const int rest = n - j0 - kPanel;  // trailing rows (and columns), >= 1
+        const unsigned g = (unsigned)((rest + kTile - 1) / kTile);
+        hipLaunchKernelGGL(k_lu_tile, dim3(g, g), dim3(kTile * kTileWaves), 0, st, A, n, j0,
+                           std::min(kPanel, rest), z, (const double*)dblk[p & 1], dblk[(p + 1) & 1], check ? 1 : 0,
+                           flag);
     }
     return chk(hipGetLastError(), "LU launch", err);
 }
@@ -524,7 +582,7 @@ int lu_det_device(double* dA, int n, int* dswp, double* ddiag, hipStream_t st, d
     const size_t need = (size_t)n * (pw + 1) * sizeof(double);
     if (need <= (size_t)(attr ? kPanelLds : 64 * 1024) && !std::getenv("PSX_LU_UNBLOCKED")) {
         double* work = nullptr;
-        if (chk(hipMalloc(&work, ((size_t)kPanel * n + kPanel) * sizeof(double) + sizeof(int)), "LU work", err))
+        if (chk(psx::dmalloc(&work, ((size_t)kPanel * n + kPanel) * sizeof(double) + sizeof(int)), "LU work", err))
             return -1;
         double* const sk = work + (size_t)kPanel * n;
         int* const zflag = (int*)(sk + kPanel);
@@ -540,7 +598,7 @@ int lu_det_device(double* dA, int n, int* dswp, double* ddiag, hipStream_t st, d
         }
         if (!rc) rc = chk(hipGetLastError(), "LU launch", err);
         if (!rc) rc = chk(hipStreamSynchronize(st), "LU sync", err);
-        hipFree(work);
+        psx::dfree(work);
         if (rc) return rc;
     } else if (enqueue_lu(dA, n, dswp, st, err)) {
         return -1;
@@ -562,17 +620,50 @@ int lu_det_device(double* dA, int n, int* dswp, double* ddiag, hipStream_t st, d
     return 0;
 }
 
+int elim_device(const double* a, int n, const double* z, int check, double* piv, double* zt, int* swap,
+                std::string* err) {
+    if (n <= 0) return -1;
+    const size_t nn = (size_t)n * n;
+    double *dA = nullptr, *dz = nullptr, *dw = nullptr, *dd = nullptr;
+    int* dflag = nullptr;
+    int rc = 0;
+    if (chk(psx::dmalloc(&dA, nn * sizeof(double)), "alloc", err) || chk(psx::dmalloc(&dz, n * sizeof(double)), "alloc", err) ||
+        chk(psx::dmalloc(&dw, 2 * kDblk * sizeof(double)), "alloc", err) ||
+        chk(psx::dmalloc(&dd, n * sizeof(double)), "alloc", err) || chk(psx::dmalloc(&dflag, sizeof(int)), "alloc", err))
+        rc = -1;
+    if (!rc) rc = chk(hipMemcpy(dA, a, nn * sizeof(double), hipMemcpyHostToDevice), "upload", err);
+    if (!rc && z) rc = chk(hipMemcpy(dz, z, n * sizeof(double), hipMemcpyHostToDevice), "upload", err);
+    if (!rc) rc = enqueue_lu_fused(dA, n, dw, dflag, z ? dz : nullptr, nullptr, err, check != 0);
+    if (!rc) {
+        hipLaunchKernelGGL(k_get_diag, dim3((n + 255) / 256), dim3(256), 0, nullptr, dA, n, dd);
+        rc = chk(hipGetLastError(), "launch", err);
+    }
+    if (!rc) rc = chk(hipMemcpy(piv, dd, n * sizeof(double), hipMemcpyDeviceToHost), "copy", err);
+    if (!rc && z) rc = chk(hipMemcpy(zt, dz, n * sizeof(double), hipMemcpyDeviceToHost), "copy", err);
+    if (!rc) rc = chk(hipMemcpy(swap, dflag, sizeof(int), hipMemcpyDeviceToHost), "copy", err);
+    psx::dfree(dA); psx::dfree(dz); psx::dfree(dw); psx::dfree(dd); psx::dfree(dflag);
+    return rc;
+}
+
 int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, double* dS, double* dy,
                    LdStudyResult* res, std::string* err) {
     std::memset(res, 0, sizeof(*res));
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const clk::time_point t0 = clk::now();
+    clk::time_point t1 = t0, t2 = t0;
     const size_t nn = (size_t)M * M;
     double *dL = nullptr, *dA = nullptr, *dz = nullptr, *ddiag = nullptr, *dcol = nullptr;
     int* dswp = nullptr;
-    auto cleanup = [&]() { hipFree(dL); hipFree(dA); hipFree(dz); hipFree(ddiag); hipFree(dcol); hipFree(dswp); };
-    if (hipMalloc(&dL, nn * sizeof(double)) != hipSuccess || hipMalloc(&dA, nn * sizeof(double)) != hipSuccess ||
-        hipMalloc(&dz, M * sizeof(double)) != hipSuccess || hipMalloc(&ddiag, M * sizeof(double)) != hipSuccess ||
-        hipMalloc(&dcol, ((size_t)kPanel * M + kPanel) * sizeof(double)) != hipSuccess ||
-        hipMalloc(&dswp, (std::max(M, 1) + 2) * sizeof(int)) != hipSuccess) {
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(st);
+        psx::IdleScope idle;  // the scratch is used on st only
+        psx::dfree(dL); psx::dfree(dA); psx::dfree(dz); psx::dfree(ddiag); psx::dfree(dcol); psx::dfree(dswp);
+    };
+    if (psx::dmalloc(&dL, nn * sizeof(double)) != hipSuccess || psx::dmalloc(&dA, nn * sizeof(double)) != hipSuccess ||
+        psx::dmalloc(&dz, M * sizeof(double)) != hipSuccess || psx::dmalloc(&ddiag, M * sizeof(double)) != hipSuccess ||
+        psx::dmalloc(&dcol, std::max((size_t)kPanel * M + kPanel, (size_t)2 * kDblk) * sizeof(double)) != hipSuccess ||
+        psx::dmalloc(&dswp, (std::max(M, 1) + 2) * sizeof(int)) != hipSuccess) {
         cleanup();
         if (err) *err = "out of device memory (LD setup)";
         return -1;
@@ -588,6 +679,7 @@ int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, dou
     int rc = 0;
     do {
         if ((rc = chk(hipMemcpyAsync(dL, ld, nn * sizeof(double), hipMemcpyHostToDevice, st), "LD upload", err))) break;
+        t1 = clk::now();
         if ((rc = chk(hipMemsetAsync(dasym, 0, sizeof(int), st), "memset", err))) break;
         hipLaunchKernelGGL(k_sym_check, dim3(gb), dim3(cb), 0, st, dL, M, dasym);
         if ((rc = chk(hipMemcpyAsync(&hasym, dasym, sizeof(int), hipMemcpyDeviceToHost, st), "copy", err))) break;
@@ -630,6 +722,7 @@ int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, dou
             add += 0.01;
         }
         if (rc) break;
+        t2 = clk::now();
         res->added = add;
         res->psd_iterations = it + 1;
         // 2. Sigma' (lower triangle, symmetrised) -> dS; elimination without pivoting
@@ -647,16 +740,8 @@ int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, dou
                 break;
             if ((rc = chk(hipMemcpyAsync(dz, z, M * sizeof(double), hipMemcpyHostToDevice, st), "z upload", err)))
                 break;
-            // elimination without pivoting: the blocked panels with the pivot check off
-            // (per-column launches when the panel does not fit LDS)
-            const int lrc = enqueue_lu_fused(dA, M, dcol, dflag, dz, st, err, false);
-            if (lrc < 0) { rc = -1; break; }
-            if (lrc > 0)
-                for (int j = 0; j < M - 1; j++) {
-                    const int r = M - j - 1;
-                    hipLaunchKernelGGL(k_elim, dim3((r + kElimCols - 1) / kElimCols, (r + kElimRows - 1) / kElimRows),
-                                       dim3(kElimCols), 0, st, dA, M, j, dz);
-                }
+            // elimination without pivoting: the tiled panels with the pivot check off
+            if (enqueue_lu_fused(dA, M, dcol, dflag, dz, st, err, false)) { rc = -1; break; }
             hipLaunchKernelGGL(k_get_diag, dim3((M + 255) / 256), dim3(256), 0, st, dA, M, ddiag);
             if ((rc = chk(hipGetLastError(), "elimination launch", err))) break;
             hipMemcpyAsync(piv.data(), ddiag, M * sizeof(double), hipMemcpyDeviceToHost, st);
@@ -686,6 +771,10 @@ int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, dou
         if ((rc = chk(hipStreamSynchronize(st), "setup sync", err))) break;
     } while (false);
     cleanup();
+    const clk::time_point t3 = clk::now();
+    res->upload_ms = ms(t0, t1);
+    res->psd_ms = ms(t1, t2);
+    res->finish_ms = ms(t2, t3);
     return rc;
 }
 

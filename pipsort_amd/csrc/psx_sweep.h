@@ -19,7 +19,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <future>
 #include <map>
+#include <memory>
+#include <string>
 #include <tuple>
 #include <vector>
 
@@ -64,7 +67,7 @@ constexpr int kRecBufs = PSX_REC_BUFS;
 // One decomposition of a level into wave units, with its record CSR.
 struct SweepPlan {
     int k = 0, U = 0, ldg = 0, rank = 0, world = 1, ca = 0;
-    int n_units = 0, rec_stride = 0, n_rows = 0;
+    int n_units = 0, rec_stride = 0, pad = 0;  // pad: record keys in v = u + pad space (variant 1)
     uint64_t union_sets = 0;
     double alg_bytes = 0, flops = 0;
     int4* d_units = nullptr;     // {a0, a1, B, T}
@@ -72,15 +75,17 @@ struct SweepPlan {
     Acc5* d_rec_alt[kRecBufs - 1] = {};  // more record buffers (pipelined asynchronous passes)
     size_t rec_len = 0;          // records per buffer
     SetRec* d_srec = nullptr;    // [n_units]
-    int* d_csr = nullptr;        // ptr[n_rows+1], row_snp[n_rows], pos[n_units * rec_stride], dptr[U+1], gidx
+    int* d_csr = nullptr;        // pos[rec_len], dptr[U+1], gidx[rec_len] (psx_plan.hip)
     const int* d_pos = nullptr;  // record slot -> buffer position, -1: no SNP (inside d_csr)
     const int* d_dptr = nullptr; // [U+1] per-SNP runs of CSR positions (inside d_csr)
     const int* d_gidx = nullptr; // CSR position -> record slot (records are unit-major; the merges gather)
-    int csr_ptr_len = 0, csr_idx_len = 0;
     int variant = 0;             // 1: the k = 3 fast kernel's decomposition
     double fused_bytes = 0, fused_flops = 0;  // in-launch level-2 work of the last launch
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // kernel start/end, merges end
     bool ran = false;
+    // the unit list on the host until upload_plan (plans built ahead on a host thread)
+    std::vector<int4> h_units;
+    bool uploaded = false;
 };
 
 // Arguments of the k = 3 fast kernel (psx_sweep3.hip).  Sweep indices live in
@@ -129,8 +134,31 @@ int launch_bc3_colsum(int ntile, const double2* mu01, const int2* n, double2* sm
 // out[i] = (a[i], b[i])
 int launch_interleave2(const double* a, const double* b, size_t n, double2* out, hipStream_t st);
 
+// a level's plan built ahead on a host thread (plan_prefetch)
+struct PlanJob {
+    std::future<int> done;  // 0: P holds the plan (records not yet allocated)
+    SweepPlan P;
+    std::string err;
+};
+
+// device scratch of plan_csr_device (keys, sorted keys, slots, radix-sort temp)
+struct PlanScratch {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+// a plan's record CSR (pos | dptr | gidx) built on the device from its units
+int plan_csr_device(const int4* d_units, int n_units, int rec_stride, int k, int variant, int pad, int U, int* d_pos,
+                    int* d_dptr, int* d_gidx, PlanScratch& scratch, hipStream_t st);
+// GPU self-check: the device CSR of a plan equals the host restatement's
+int plan_csr_selftest(int U, const unsigned char* pres, int k, int rank, int world, int variant, long* mismatches,
+                      long* records);
+int warm_module_plan();
+
 struct SweepPlanCache {
     std::map<std::tuple<int, int, int, int, int>, SweepPlan> plans;  // (k, U, rank, world, variant)
+    std::map<std::tuple<int, int, int, int, int>, std::unique_ptr<PlanJob>> pending;  // plan_prefetch
+    std::vector<unsigned char> pres_host;    // presence bits by u (ldg), set by the engine at create
+    PlanScratch csr_scratch;
     double* d_skew[2] = {nullptr, nullptr};  // skewed Sigma~ tiles (B <= T), k = 2 and exact k = 3
     double* d_skewT[2] = {nullptr, nullptr}; // lane-owns-c tiles in v space (k = 3 fast kernel)
     double2* d_g01 = nullptr;                // skewT of both studies interleaved (k = 3 fast kernel)
@@ -156,9 +184,20 @@ bool sweep_supports(int k, int U);
 struct PlanUnit { int a0, a1, B, T; double work; int j0 = 0, j1 = 64; };
 int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* pres_host,
                std::vector<PlanUnit>& mine, int& ca, double& sets, double& configs, double& bytes);
+// plan-shaping knobs of the k = 3 decomposition (environment, read once)
+struct K3Knobs { double rounds, maskw, diagw, unitw, tail_frac, tail2; int diag_div; };
+const K3Knobs& k3_knobs();
+// hash of the knobs and the compiled plan constants (PlanTag: ranks must agree)
+uint64_t plan_knobs_hash();
 // k = 3 fast-kernel decomposition: units (a0, a1, K, C) in v space
 int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_host, std::vector<PlanUnit>& mine,
                  int& ca, double& sets, double& configs, double& bytes);
+// Build level k's plan for (rank, world) on a host thread (device `device`):
+// the unit decomposition, counts and record CSR, uploaded; sweep_prepare takes
+// it (and allocates its records) instead of building it.  Needs pres_host.
+// host-only diagnostics: build level k's plan (all SNPs in both studies) without the device
+int plan_host_ms(int U, int k, int rank, int world, double* ms, int* n_units, long* n_records);
+void plan_prefetch(SweepPlanCache& cache, int device, int k, int U, int ldg, int rank, int world, bool exact);
 int sweep_begin(SweepPlanCache& cache, hipStream_t stream);   // zero the EXACT flag
 int sweep_level(SweepPlanCache& cache, int k, int U, int ldg, int rank, int world, hipStream_t stream,
                 const SweepArgs& a, Acc5* acc, SetRec* sacc, bool exact);   // async enqueue

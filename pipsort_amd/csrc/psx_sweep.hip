@@ -21,6 +21,7 @@
 #include <cstdlib>
 
 #include <algorithm>
+#include <chrono>
 #include <array>
 #include <cmath>
 #include <cstring>
@@ -30,6 +31,7 @@
 #include "psx_sweep.h"
 #include "psx_sweep_dev.h"
 #include "psx_sweep_unit.h"
+#include "psx_mem.h"
 
 namespace psx {
 
@@ -118,21 +120,21 @@ __global__ __launch_bounds__(256) void k_merge_members(const Acc5* __restrict__ 
     }
 }
 
-// Row r's records are CSR positions [ptr[r], ptr[r+1]), each gathered from
-// record slot gidx[q] (unit-major record buffers; null: the position itself);
-// 256 threads fold them in a fixed order.
-__global__ __launch_bounds__(256) void k_merge_rows(const Acc5* __restrict__ rec, const int* __restrict__ ptr,
-                                                   const int* __restrict__ row_snp, const int* __restrict__ gidx,
-                                                   Acc5* __restrict__ acc) {
+// SNP u's records are CSR positions [dptr[u], dptr[u+1]) (none: the block
+// returns), each gathered from record slot gidx[q] (unit-major record
+// buffers); 256 threads fold them in a fixed order.
+__global__ __launch_bounds__(256) void k_merge_rows(const Acc5* __restrict__ rec, const int* __restrict__ dptr,
+                                                   const int* __restrict__ gidx, Acc5* __restrict__ acc) {
     __shared__ Acc5 sh[4];
-    const int row = blockIdx.x;
+    const int u = blockIdx.x;
+    const int q0 = dptr[u], q1 = dptr[u + 1];
+    if (q0 == q1) return;  // uniform
     Acc5 a = acc_zero();
-    for (int i = ptr[row] + (int)threadIdx.x; i < ptr[row + 1]; i += 256) fold_acc(a, rec[gidx ? gidx[i] : i]);
+    for (int i = q0 + (int)threadIdx.x; i < q1; i += 256) fold_acc(a, rec[gidx[i]]);
     wave_fold_acc(a);
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = a;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int u = row_snp[row];
         Acc5 g = acc[u];
         for (int w = 0; w < 4; w++) fold_acc(g, sh[w]);
         acc[u] = g;
@@ -317,6 +319,48 @@ constexpr double kDiagW = 0.65;   // per-a cost of a pipelined diagonal walk (PS
 constexpr double kUnitW = 0.04;   // fixed cost of a unit (PSX_K3_UNITW)
 constexpr double kMaskedDiagW = 0.65;  // per-a cost of a masked diagonal walk (PSX_K3_MASKW; 1.0 / 1.3 worse, r04aa; 0.65 with DIAGW 0.65 balances world 8 best, r04ae)
 
+// The plan-shaping knobs, read once per process.  PSX_K3_ROUNDS / PSX_K3_DIAG_DIV
+// (environment, tuning experiments) override the dispatch rounds the a-chunk is
+// sized for and divide the diagonal units' a-chunk; PSX_K3_MASKW / DIAGW /
+// UNITW the cost model of the shard split; PSX_K3_TAIL / TAIL2 the tail cuts.
+// Every rank of a job must cut the same plan: plan_knobs_hash() goes into each
+// rank's partial image (PlanTag) and the merge refuses images whose hashes differ.
+const K3Knobs& k3_knobs() {
+    static const K3Knobs k = [] {
+        K3Knobs r;
+        auto num = [](const char* name, double dflt, bool zero_ok) {
+            const char* e = std::getenv(name);
+            if (!e) return dflt;
+            const double v = std::atof(e);
+            return (zero_ok ? v >= 0 : v > 0) ? v : dflt;
+        };
+        r.rounds = num("PSX_K3_ROUNDS", (double)PSX_K3_ROUNDS, false);
+        r.diag_div = (int)num("PSX_K3_DIAG_DIV", 1.0, false);
+        r.maskw = num("PSX_K3_MASKW", kMaskedDiagW, false);
+        r.diagw = num("PSX_K3_DIAGW", kDiagW, false);
+        r.unitw = num("PSX_K3_UNITW", kUnitW, true);
+        const char* t = std::getenv("PSX_K3_TAIL");
+        r.tail_frac = t ? std::atof(t) : kTailFrac;
+        const char* t2 = std::getenv("PSX_K3_TAIL2");
+        r.tail2 = t2 ? std::atof(t2) : 0.0;
+        return r;
+    }();
+    return k;
+}
+
+uint64_t plan_knobs_hash() {
+    const K3Knobs& k = k3_knobs();
+    const double v[7] = {k.rounds, (double)k.diag_div, k.maskw, k.diagw, k.unitw, k.tail_frac, k.tail2};
+    uint64_t h = 1469598103934665603ull;  // FNV-1a over the values' bytes and the compiled constants
+    auto mix = [&](const void* p, size_t n) {
+        for (size_t i = 0; i < n; i++) h = (h ^ ((const unsigned char*)p)[i]) * 1099511628211ull;
+    };
+    mix(v, sizeof(v));
+    const int c[3] = {PSX_K3_WAVES, kMaxChunkA3, PSX_KMAX};
+    mix(c, sizeof(c));
+    return h;
+}
+
 int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_host, std::vector<PlanUnit>& mine,
                  int& ca, double& sets, double& configs, double& bytes) {
     const int nblk = ldg / 64, pad = ldg - U;
@@ -341,31 +385,9 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // for and divide the diagonal units' a-chunk (shorter units for the last
     // dispatch rounds).
     constexpr double kPlanCUs = 256.0;
-    static const double rounds = [] {
-        const char* e = std::getenv("PSX_K3_ROUNDS");
-        return e && std::atof(e) > 0 ? std::atof(e) : (double)PSX_K3_ROUNDS;
-    }();
-    static const int diag_div = [] {
-        const char* e = std::getenv("PSX_K3_DIAG_DIV");
-        return e && std::atoi(e) > 0 ? std::atoi(e) : 1;
-    }();
-    // per-a cost of a diagonal walk that runs the masked (unpipelined) step loop —
-    // a inside the block, or block 0 holding padding — relative to an
-    // off-diagonal walk (PSX_K3_MASKW)
-    static const double maskw = [] {
-        const char* e = std::getenv("PSX_K3_MASKW");
-        return e && std::atof(e) > 0 ? std::atof(e) : kMaskedDiagW;
-    }();
-    // per-a cost of a pipelined (folded) diagonal walk and the fixed cost of a
-    // unit, in off-diagonal a-walks (PSX_K3_DIAGW, PSX_K3_UNITW)
-    static const double diagw = [] {
-        const char* e = std::getenv("PSX_K3_DIAGW");
-        return e && std::atof(e) > 0 ? std::atof(e) : kDiagW;
-    }();
-    static const double unitw = [] {
-        const char* e = std::getenv("PSX_K3_UNITW");
-        return e && std::atof(e) >= 0 ? std::atof(e) : kUnitW;
-    }();
+    const K3Knobs& kn = k3_knobs();
+    const double rounds = kn.rounds, maskw = kn.maskw, diagw = kn.diagw, unitw = kn.unitw;
+    const int diag_div = kn.diag_div;
     const double kTarget = rounds * (4.0 * PSX_K3_WAVES * kPlanCUs);
     ca = (int)std::lround(total_a / (kTarget * world));
     ca = std::min(ca, kMaxChunkA3);  // (caps 6 / 8 with the tail split: +0.4 / +1.5 % at world 1, r04w)
@@ -466,10 +488,7 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // fraction of the shard's work, default kTailFrac) cuts the units at the end
     // of the order into single-a units, so the drain is made of the shortest
     // units.  Each (a, b, c) stays in the same shard, so the counts above hold.
-    static const double tail_frac = [] {
-        const char* e = std::getenv("PSX_K3_TAIL");
-        return e ? std::atof(e) : kTailFrac;
-    }();
+    const double tail_frac = kn.tail_frac;
     if (tail_frac > 0 && ca > 1) {
         double wtot = 0, wacc = 0;
         for (auto& u : mine) wtot += u.work;
@@ -492,10 +511,7 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
         // diagonal single-a units walk half their (folded) steps each, so the
         // final drain is made of half-length pieces; each pair of the block is
         // still visited once (steps 1..16 | 17..32)
-        static const double tail2 = [] {
-            const char* e = std::getenv("PSX_K3_TAIL2");
-            return e ? std::atof(e) : 0.0;
-        }();
+        const double tail2 = kn.tail2;
         if (tail2 > 0) {
             double w2 = 0;
             size_t c2 = tail.size();
@@ -527,11 +543,71 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     return 0;
 }
 
+// a plan's unit list to the device and its record CSR built there
+// (psx_plan.hip: pos | dptr | gidx in one block); the host unit list is dropped
+static int upload_plan(SweepPlan& P, SweepPlanCache& C, hipStream_t st) {
+    if (P.uploaded) return 0;
+    const size_t n = P.rec_len;
+    if (P.n_units > 0) {
+        SWCHK(psx::dmalloc(&P.d_units, sizeof(int4) * P.n_units));
+        SWCHK(hipMemcpyAsync(P.d_units, P.h_units.data(), sizeof(int4) * P.n_units, hipMemcpyHostToDevice, st));
+        SWCHK(psx::dmalloc(&P.d_srec, sizeof(SetRec) * (size_t)P.n_units));
+    }
+    SWCHK(psx::dmalloc(&P.d_csr, sizeof(int) * (2 * n + P.U + 1)));
+    P.d_pos = P.d_csr;
+    P.d_dptr = P.d_csr + n;
+    P.d_gidx = P.d_csr + n + P.U + 1;
+    if (plan_csr_device(P.d_units, P.n_units, P.rec_stride, P.k, P.variant, P.pad, P.U, const_cast<int*>(P.d_pos),
+                        const_cast<int*>(P.d_dptr), const_cast<int*>(P.d_gidx), C.csr_scratch, st)) {
+        g_sweep_err = "plan CSR on the device failed";
+        return -1;
+    }
+    SWCHK(hipStreamSynchronize(st));  // the host unit list is released below
+    std::vector<int4>().swap(P.h_units);
+    P.uploaded = true;
+    return 0;
+}
+
+// The record CSR restated on the host (the pre-r05 builder): tests compare the
+// device build against it (plan_csr_selftest).
+static void host_plan_csr(const SweepPlan& P, const std::vector<int4>& hu, std::vector<int>& pos,
+                          std::vector<int>& dptr, std::vector<int>& gidx) {
+    const int U = P.U, pad = P.pad;
+    std::vector<int> key((size_t)P.n_units * P.rec_stride, -1);
+    for (int i = 0; i < P.n_units; i++) {
+        const int B = hu[i].z & 0xffff, T = hu[i].w & 0xffff;
+        int* kk = key.data() + (size_t)i * P.rec_stride;
+        const bool one = P.variant && P.k == 3 && B == T;
+        for (int t = 0; t < 64; t++) {
+            int c = 64 * T + t - pad;
+            if (c >= 0 && c < U) kk[t] = c;
+            int b = 64 * B + t - pad;
+            if (!one && b >= 0 && b < U) kk[64 + t] = b;
+        }
+        if (P.k == 3)
+            for (int a = hu[i].x; a < hu[i].y; a++) kk[128 + (a - hu[i].x)] = a - pad;
+    }
+    std::vector<int> cnt(U + 1, 0);
+    for (int v : key) if (v >= 0) cnt[v]++;
+    dptr.assign(U + 1, 0);
+    for (int u = 0; u < U; u++) dptr[u + 1] = dptr[u] + cnt[u];
+    gidx.assign(dptr[U], 0);
+    std::vector<int> fill(dptr.begin(), dptr.end() - 1);
+    pos.assign(key.size(), -1);
+    for (size_t i = 0; i < key.size(); i++)
+        if (key[i] >= 0) {
+            gidx[fill[key[i]]++] = (int)i;
+            pos[i] = (int)i;
+        }
+}
+
 // variant 1: the k = 3 fast kernel's decomposition (plan_units3c, v space);
-// variant 0: plan_units (k = 2, and the exact k = 3 rerun)
+// variant 0: plan_units (k = 2, and the exact k = 3 rerun).  Host only: the unit
+// list and the plan's counts (upload_plan puts it on the device).
 static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, const unsigned char* pres_host,
                       int variant) {
     P.k = k; P.U = U; P.ldg = ldg; P.rank = rank; P.world = world;
+    P.variant = variant;
     std::vector<PlanUnit> mine;
     int ca = 0;
     double sets = 0, configs = 0, bytes = 0;
@@ -559,77 +635,44 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
     // counters of its own build cannot overstate the FP64 rate; k = 2 by the
     // round-1 ratio of VALU work per set.  bench.py reports it only as a model.
     P.flops = sets * (k == 3 ? 131.0 : 110.0);
-    const int pad = variant ? ldg - U : 0;  // record keys of variant 1 are in v space
-    // device buffers
-    std::vector<int4> hu(P.n_units);
+    P.pad = variant ? ldg - U : 0;  // record keys of variant 1 are in v space
     // variant 1 packs the b-walk step range of (half) units into the high bits
+    P.h_units.resize(P.n_units);
     for (int i = 0; i < P.n_units; i++)
-        hu[i] = variant ? make_int4(mine[i].a0, mine[i].a1, mine[i].B | (mine[i].j0 << 16), mine[i].T | (mine[i].j1 << 16))
-                        : make_int4(mine[i].a0, mine[i].a1, mine[i].B, mine[i].T);
-    if (P.n_units > 0) {
-        SWCHK(hipMalloc(&P.d_units, sizeof(int4) * P.n_units));
-        SWCHK(hipMemcpy(P.d_units, hu.data(), sizeof(int4) * P.n_units, hipMemcpyHostToDevice));
-
-        SWCHK(hipMalloc(&P.d_srec, sizeof(SetRec) * (size_t)P.n_units));
-    }
-    // CSR: record -> SNP, grouped by SNP in record order (deterministic folds)
-    std::vector<int> key((size_t)P.n_units * P.rec_stride, -1);
-    for (int i = 0; i < P.n_units; i++) {
-        const PlanUnit& u = mine[i];
-        int* kk = key.data() + (size_t)i * P.rec_stride;
-        // the k = 3 fast kernel writes a diagonal tile's c and b-slot records of one
-        // SNP as one (c) record
-        const bool one = variant && k == 3 && u.B == u.T;
-        for (int t = 0; t < 64; t++) {
-            int c = 64 * u.T + t - pad;
-            if (c >= 0 && c < U) kk[t] = c;
-            int b = 64 * u.B + t - pad;
-            if (!one && b >= 0 && b < U) kk[64 + t] = b;
-        }
-        if (k == 3)
-            for (int a = u.a0; a < u.a1; a++) kk[128 + (a - u.a0)] = a - pad;
-    }
-    std::vector<int> cnt(U, 0);
-    for (int v : key) if (v >= 0) cnt[v]++;
-    std::vector<int> ptr(1, 0), rows, start(U, -1);
-    int acc = 0;
-    for (int u = 0; u < U; u++)
-        if (cnt[u]) { start[u] = acc; rows.push_back(u); acc += cnt[u]; ptr.push_back(acc); }
-    std::vector<int> idx(acc), fill(U, 0);
-    for (size_t i = 0; i < key.size(); i++)
-        if (key[i] >= 0) idx[start[key[i]] + fill[key[i]]++] = (int)i;
-    P.n_rows = (int)rows.size();
-    P.csr_ptr_len = (int)ptr.size();
-    P.csr_idx_len = (int)idx.size();
+        P.h_units[i] = variant ? make_int4(mine[i].a0, mine[i].a1, mine[i].B | (mine[i].j0 << 16),
+                                           mine[i].T | (mine[i].j1 << 16))
+                               : make_int4(mine[i].a0, mine[i].a1, mine[i].B, mine[i].T);
     // Records are unit-major: the kernels write record slot i at position i
     // (pos[i] = -1: no SNP), so a unit's 64 c (b) records are contiguous and the
-    // stores coalesce; the merges gather each SNP's records through idx, in
+    // stores coalesce; the merges gather each SNP's records through gidx, in
     // record order (same fold order as a per-SNP layout; same-box A/B against
     // writing each record at its CSR position: world 1 -0.4 %, world 8 -1 %)
-    std::vector<int> pos(key.size(), -1);
-    for (size_t i = 0; i < key.size(); i++) pos[i] = key[i] >= 0 ? (int)i : -1;
-    // dense per-SNP pointers (rows are in increasing SNP order): SNP u's run is
-    // [dptr[u], dptr[u+1]), empty when u has no record
-    std::vector<int> dptr(U + 1, 0);
-    for (int u = 0, r = 0; u <= U; u++) {
-        while (r < (int)rows.size() && rows[r] < u) r++;
-        dptr[u] = r < (int)rows.size() ? ptr[r] : acc;
-    }
-    std::vector<int> packed;
-    packed.insert(packed.end(), ptr.begin(), ptr.end());
-    packed.insert(packed.end(), rows.begin(), rows.end());
-    packed.insert(packed.end(), pos.begin(), pos.end());
-    packed.insert(packed.end(), dptr.begin(), dptr.end());
-    packed.insert(packed.end(), idx.begin(), idx.end());
-    P.rec_len = key.size();
-    if (P.rec_len) SWCHK(hipMalloc(&P.d_rec, sizeof(Acc5) * P.rec_len));
-    if (!packed.empty()) {
-        SWCHK(hipMalloc(&P.d_csr, sizeof(int) * packed.size()));
-        SWCHK(hipMemcpy(P.d_csr, packed.data(), sizeof(int) * packed.size(), hipMemcpyHostToDevice));
-        P.d_pos = P.d_csr + ptr.size() + rows.size();
-        P.d_dptr = P.d_pos + pos.size();
-        P.d_gidx = P.d_dptr + dptr.size();
-    }
+    P.rec_len = (size_t)P.n_units * P.rec_stride;
+    return 0;
+}
+
+int plan_csr_selftest(int U, const unsigned char* pres, int k, int rank, int world, int variant, long* mismatches,
+                      long* records) {
+    const int ldg = (U + 63) / 64 * 64;
+    SweepPlan P;
+    SweepPlanCache C;
+    if (build_plan(P, k, U, ldg, rank, world, pres, variant)) return -1;
+    const std::vector<int4> hu = P.h_units;
+    std::vector<int> pos, dptr, gidx;
+    host_plan_csr(P, hu, pos, dptr, gidx);
+    hipStream_t st = nullptr;
+    if (upload_plan(P, C, st)) return -1;
+    std::vector<int> dpos(P.rec_len), ddptr(U + 1), dgidx(P.rec_len);
+    SWCHK(hipMemcpy(dpos.data(), P.d_pos, sizeof(int) * P.rec_len, hipMemcpyDeviceToHost));
+    SWCHK(hipMemcpy(ddptr.data(), P.d_dptr, sizeof(int) * (U + 1), hipMemcpyDeviceToHost));
+    SWCHK(hipMemcpy(dgidx.data(), P.d_gidx, sizeof(int) * P.rec_len, hipMemcpyDeviceToHost));
+    long bad = 0;
+    for (size_t i = 0; i < P.rec_len; i++) bad += dpos[i] != pos[i];
+    for (int u = 0; u <= U; u++) bad += ddptr[u] != dptr[u];
+    for (size_t q = 0; q < gidx.size(); q++) bad += dgidx[q] != gidx[q];
+    *mismatches = bad;
+    *records = (long)gidx.size();
+    psx::dfree(P.d_units); psx::dfree(P.d_srec); psx::dfree(P.d_csr); psx::dfree(C.csr_scratch.p);
     return 0;
 }
 
@@ -662,16 +705,16 @@ static Sweep3Args sweep3_args(const SweepPlanCache& C, const SweepArgs& a, int U
 
 static void free_k3(SweepPlanCache& C) {
     for (int s = 0; s < 2; s++) {
-        hipFree(C.d_skewT[s]); C.d_skewT[s] = nullptr;
-        hipFree(C.d_ys[s]); C.d_ys[s] = nullptr;
+        psx::dfree(C.d_skewT[s]); C.d_skewT[s] = nullptr;
+        psx::dfree(C.d_ys[s]); C.d_ys[s] = nullptr;
     }
-    hipFree(C.d_bcn); C.d_bcn = nullptr;
-    hipFree(C.d_bcsm); C.d_bcsm = nullptr;
-    hipFree(C.d_bcsn); C.d_bcsn = nullptr;
-    hipFree(C.d_bccm); C.d_bccm = nullptr;
-    hipFree(C.d_bccn); C.d_bccn = nullptr;
-    hipFree(C.d_g01); C.d_g01 = nullptr;
-    hipFree(C.d_mu01); C.d_mu01 = nullptr;
+    psx::dfree(C.d_bcn); C.d_bcn = nullptr;
+    psx::dfree(C.d_bcsm); C.d_bcsm = nullptr;
+    psx::dfree(C.d_bcsn); C.d_bcsn = nullptr;
+    psx::dfree(C.d_bccm); C.d_bccm = nullptr;
+    psx::dfree(C.d_bccn); C.d_bccn = nullptr;
+    psx::dfree(C.d_g01); C.d_g01 = nullptr;
+    psx::dfree(C.d_mu01); C.d_mu01 = nullptr;
 }
 
 // the layouts every tiled level reads (skewed Sigma~ tiles, singleton weights,
@@ -680,16 +723,16 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
     if (C.d_skew[0] && C.skew_ldg == ldg && C.skew_src[0] == a.G0 && C.skew_src[1] == a.G1) return 0;
     free_k3(C);
     for (int s = 0; s < 2; s++) {
-        hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
-        hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
-        hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
+        psx::dfree(C.d_skew[s]); C.d_skew[s] = nullptr;
+        psx::dfree(C.d_muS[s]); C.d_muS[s] = nullptr;
+        psx::dfree(C.d_nS[s]); C.d_nS[s] = nullptr;
     }
-    hipFree(C.d_tab); C.d_tab = nullptr;
+    psx::dfree(C.d_tab); C.d_tab = nullptr;
     {
         // 2^(i/256) correctly rounded (long double on the host)
         double tab[256];
         for (int i = 0; i < 256; i++) tab[i] = (double)exp2l((long double)i / 256.0L);
-        SWCHK(hipMalloc(&C.d_tab, sizeof(tab)));
+        SWCHK(psx::dmalloc(&C.d_tab, sizeof(tab)));
         SWCHK(hipMemcpyAsync(C.d_tab, tab, sizeof(tab), hipMemcpyHostToDevice, st));
         std::vector<unsigned char> pres(ldg);
         SWCHK(hipMemcpyAsync(pres.data(), a.pres, ldg, hipMemcpyDeviceToHost, st));
@@ -698,8 +741,8 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
         for (int u = 0; u < U; u++) C.allpres = C.allpres && pres[u] == 3;
     }
     for (int s = 0; s < 2; s++) {
-        SWCHK(hipMalloc(&C.d_muS[s], sizeof(double) * ldg));
-        SWCHK(hipMalloc(&C.d_nS[s], sizeof(int) * ldg));
+        SWCHK(psx::dmalloc(&C.d_muS[s], sizeof(double) * ldg));
+        SWCHK(psx::dmalloc(&C.d_nS[s], sizeof(int) * ldg));
         hipLaunchKernelGGL(k_build_singles, dim3((ldg + 255) / 256), dim3(256), 0, st, s ? a.Ad1 : a.Ad0,
                            s ? a.y1 : a.y0, 1.0 / std::sqrt(s ? a.d1 : a.d0), ldg, C.d_muS[s], C.d_nS[s]);
         SWCHK(hipGetLastError());
@@ -707,12 +750,12 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
     const int nblk = ldg / 64;
     const int ntile = nblk * (nblk + 1) / 2;
     for (int s = 0; s < 2; s++) {
-        SWCHK(hipMalloc(&C.d_skew[s], sizeof(double) * (size_t)ntile * 4096));
+        SWCHK(psx::dmalloc(&C.d_skew[s], sizeof(double) * (size_t)ntile * 4096));
         hipLaunchKernelGGL(k_build_skew, dim3(ntile, 64), dim3(64), 0, st, s ? a.G1 : a.G0, ldg, nblk, C.d_skew[s]);
         SWCHK(hipGetLastError());
     }
     if (!C.d_redo) {
-        SWCHK(hipMalloc(&C.d_redo, sizeof(int)));
+        SWCHK(psx::dmalloc(&C.d_redo, sizeof(int)));
         SWCHK(hipMemsetAsync(C.d_redo, 0, sizeof(int), st));
     }
     C.skew_ldg = ldg;
@@ -729,9 +772,9 @@ static int ensure_k3(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hipS
     const int nblk = ldg / 64;
     const int ntile = nblk * (nblk + 1) / 2;
     for (int s = 0; s < 2; s++) {
-        SWCHK(hipMalloc(&C.d_ys[s], sizeof(double) * ldg));
+        SWCHK(psx::dmalloc(&C.d_ys[s], sizeof(double) * ldg));
         if (launch_scale_y(s ? a.y1 : a.y0, ldg, C.d_ys[s], st)) SWCHK(hipGetLastError());
-        SWCHK(hipMalloc(&C.d_skewT[s], sizeof(double) * (size_t)ntile * 4096));
+        SWCHK(psx::dmalloc(&C.d_skewT[s], sizeof(double) * (size_t)ntile * 4096));
         if (launch_build_skewT(s ? a.G1 : a.G0, ldg, ldg - U, C.d_skewT[s], st)) SWCHK(hipGetLastError());
     }
     {  // the a-independent {b, c} weights of every k = 3 step
@@ -739,26 +782,55 @@ static int ensure_k3(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hipS
         // kTileRowPad rows past the last tile: the pipelined b-walk loads up to
         // three steps ahead without clamping (rows it never uses)
         const size_t nrow = (size_t)ntile * 4096, npad = (size_t)kTileRowPad * 64;
-        SWCHK(hipMalloc(&C.d_mu01, sizeof(double2) * (nrow + npad)));
-        SWCHK(hipMalloc(&C.d_bcn, sizeof(int2) * (nrow + npad)));
-        SWCHK(hipMalloc(&C.d_g01, sizeof(double2) * (nrow + npad)));
+        SWCHK(psx::dmalloc(&C.d_mu01, sizeof(double2) * (nrow + npad)));
+        SWCHK(psx::dmalloc(&C.d_bcn, sizeof(int2) * (nrow + npad)));
+        SWCHK(psx::dmalloc(&C.d_g01, sizeof(double2) * (nrow + npad)));
         SWCHK(hipMemsetAsync(C.d_mu01 + nrow, 0, sizeof(double2) * npad, st));
         SWCHK(hipMemsetAsync(C.d_bcn + nrow, 0, sizeof(int2) * npad, st));
         SWCHK(hipMemsetAsync(C.d_g01 + nrow, 0, sizeof(double2) * npad, st));
         if (launch_build_bc3(S3, ntile, C.d_mu01, C.d_bcn, st)) SWCHK(hipGetLastError());
-        SWCHK(hipMalloc(&C.d_bcsm, sizeof(double2) * (size_t)ntile * 64));
-        SWCHK(hipMalloc(&C.d_bcsn, sizeof(int2) * (size_t)ntile * 64));
+        SWCHK(psx::dmalloc(&C.d_bcsm, sizeof(double2) * (size_t)ntile * 64));
+        SWCHK(psx::dmalloc(&C.d_bcsn, sizeof(int2) * (size_t)ntile * 64));
         if (launch_bc3_rowsum(ntile, C.d_mu01, C.d_bcn, C.d_bcsm, C.d_bcsn, st)) SWCHK(hipGetLastError());
-        SWCHK(hipMalloc(&C.d_bccm, sizeof(double2) * (size_t)ntile * 64));
-        SWCHK(hipMalloc(&C.d_bccn, sizeof(int2) * (size_t)ntile * 64));
+        SWCHK(psx::dmalloc(&C.d_bccm, sizeof(double2) * (size_t)ntile * 64));
+        SWCHK(psx::dmalloc(&C.d_bccn, sizeof(int2) * (size_t)ntile * 64));
         if (launch_bc3_colsum(ntile, C.d_mu01, C.d_bcn, C.d_bccm, C.d_bccn, st)) SWCHK(hipGetLastError());
         if (launch_interleave2(C.d_skewT[0], C.d_skewT[1], (size_t)ntile * 4096, C.d_g01, st)) SWCHK(hipGetLastError());
     }
     return 0;
 }
 
+int plan_host_ms(int U, int k, int rank, int world, double* ms, int* n_units, long* n_records) {
+    const int ldg = (U + 63) / 64 * 64;
+    std::vector<unsigned char> pres(ldg, 0);
+    for (int u = 0; u < U; u++) pres[u] = 3;
+    SweepPlan P;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = build_plan(P, k, U, ldg, rank, world, pres.data(), k == 3 ? 1 : 0);
+    *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    *n_units = P.n_units;
+    *n_records = (long)P.rec_len;
+    return rc;
+}
+
+void plan_prefetch(SweepPlanCache& C, int device, int k, int U, int ldg, int rank, int world, bool exact) {
+    const int variant = (k == 3 && !exact) ? 1 : 0;
+    auto key = std::make_tuple(k, U, rank, world, variant);
+    if ((int)C.pres_host.size() != ldg || C.plans.count(key) || C.pending.count(key)) return;
+    std::unique_ptr<PlanJob> job(new PlanJob());
+    PlanJob* J = job.get();
+    std::vector<unsigned char> pres(C.pres_host);
+    J->done = std::async(std::launch::async, [=]() {
+        (void)device;  // host work only: the device part runs at the first pass
+        const int rc = build_plan(J->P, k, U, ldg, rank, world, pres.data(), variant);
+        if (rc) J->err = g_sweep_err;
+        return rc;
+    });
+    C.pending.emplace(key, std::move(job));
+}
+
 int sweep_begin(SweepPlanCache& C, hipStream_t st) {
-    if (!C.d_flag) SWCHK(hipMalloc(&C.d_flag, sizeof(int)));
+    if (!C.d_flag) SWCHK(psx::dmalloc(&C.d_flag, sizeof(int)));
     SWCHK(hipMemsetAsync(C.d_flag, 0, sizeof(int), st));
     return 0;
 }
@@ -785,11 +857,28 @@ int sweep_prepare(SweepPlanCache& C, int k, int U, int ldg, int rank, int world,
     auto key = std::make_tuple(k, U, rank, world, variant);
     auto it = C.plans.find(key);
     if (it == C.plans.end()) {
-        std::vector<unsigned char> pres(ldg);
-        SWCHK(hipStreamSynchronize(st));
-        SWCHK(hipMemcpy(pres.data(), a.pres, ldg, hipMemcpyDeviceToHost));
         SweepPlan P;
-        if (build_plan(P, k, U, ldg, rank, world, pres.data(), variant)) return -1;
+        auto pj = C.pending.find(key);
+        if (pj != C.pending.end()) {  // built ahead (plan_prefetch)
+            const int rc = pj->second->done.get();
+            P = pj->second->P;
+            const std::string err = pj->second->err;
+            C.pending.erase(pj);
+            if (rc) {
+                g_sweep_err = err;
+                return -1;
+            }
+        } else {
+            std::vector<unsigned char> pres(C.pres_host);
+            if ((int)pres.size() != ldg) {
+                pres.assign(ldg, 0);
+                SWCHK(hipStreamSynchronize(st));
+                SWCHK(hipMemcpy(pres.data(), a.pres, ldg, hipMemcpyDeviceToHost));
+            }
+            if (build_plan(P, k, U, ldg, rank, world, pres.data(), variant)) return -1;
+        }
+        if (upload_plan(P, C, st)) return -1;
+        if (P.rec_len && !P.d_rec) SWCHK(psx::dmalloc(&P.d_rec, sizeof(Acc5) * P.rec_len));
         P.variant = variant;
         for (int i = 0; i < 3; i++) SWCHK(hipEventCreate(&P.ev[i]));
         it = C.plans.emplace(key, P).first;
@@ -806,11 +895,8 @@ int sweep_level(SweepPlanCache& C, int k, int U, int ldg, int rank, int world, h
     if (sweep_kernel(C, *PP, st, a, nullptr, exact, nullptr, nullptr)) return -1;
     SweepPlan& P = *PP;
     if (P.n_units == 0) return 0;
-    if (P.n_rows > 0) {
-        hipLaunchKernelGGL(k_merge_rows, dim3(P.n_rows), dim3(256), 0, st, P.d_rec, P.d_csr,
-                           P.d_csr + P.csr_ptr_len, P.d_gidx, acc);
-        SWCHK(hipGetLastError());
-    }
+    hipLaunchKernelGGL(k_merge_rows, dim3(P.U), dim3(256), 0, st, P.d_rec, P.d_dptr, P.d_gidx, acc);
+    SWCHK(hipGetLastError());
     SetRec none = set_zero();
     if (launch_merge_sets(P.d_srec, P.n_units, none, sacc, st)) return -1;
     SWCHK(hipEventRecord(P.ev[2], st));
@@ -849,7 +935,7 @@ Acc5* plan_records(SweepPlan& P, int parity) {
         return nullptr;
     }
     Acc5*& r = P.d_rec_alt[parity - 1];
-    if (!r && P.rec_len > 0 && hipMalloc(&r, sizeof(Acc5) * P.rec_len) != hipSuccess) {
+    if (!r && P.rec_len > 0 && psx::dmalloc(&r, sizeof(Acc5) * P.rec_len) != hipSuccess) {
         r = nullptr;
         g_sweep_err = "out of device memory (record buffer)";
     }
@@ -888,7 +974,7 @@ int sweep_kernel(SweepPlanCache& C, SweepPlan& P, hipStream_t st, const SweepArg
             P.fused_flops = l2->flops;
         }
         static const char* trace_path = std::getenv("PSX_UNIT_TRACE");  // diagnostics: unit timeline dump
-        if (trace_path) SWCHK(hipMalloc(&S3.trace, sizeof(unsigned long long) * kTraceWords * (size_t)P.n_units));
+        if (trace_path) SWCHK(psx::dmalloc(&S3.trace, sizeof(unsigned long long) * kTraceWords * (size_t)P.n_units));
         if (trace_path) SWCHK(hipMemsetAsync(S3.trace, 0, sizeof(unsigned long long) * kTraceWords * (size_t)P.n_units, st));
         if (launch_sweep3(C.allpres, S3, P.n_units, P.d_units, rec, srec, P.rec_stride, flag, P.d_pos, st,
                           ride ? &b : nullptr, ev0, ev1))
@@ -897,7 +983,7 @@ int sweep_kernel(SweepPlanCache& C, SweepPlan& P, hipStream_t st, const SweepArg
             std::vector<unsigned long long> h(kTraceWords * (size_t)P.n_units);
             SWCHK(hipStreamSynchronize(st));
             SWCHK(hipMemcpy(h.data(), S3.trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
-            SWCHK(hipFree(S3.trace));
+            SWCHK(psx::dfree(S3.trace));
             if (FILE* f = std::fopen(trace_path, "wb")) {
                 std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
                 std::fclose(f);
@@ -946,23 +1032,31 @@ int sweep_stats_plan(SweepPlan& P, int k, SweepStats* stats) {
 }
 
 void sweep_free(SweepPlanCache& C) {
+    psx::dfree(C.csr_scratch.p);
+    C.csr_scratch = PlanScratch();
+    for (auto& kv : C.pending) {  // plans built ahead and never used
+        kv.second->done.wait();
+        SweepPlan& P = kv.second->P;
+        psx::dfree(P.d_units); psx::dfree(P.d_srec); psx::dfree(P.d_csr);
+    }
+    C.pending.clear();
     for (auto& kv : C.plans) {
         SweepPlan& P = kv.second;
-        hipFree(P.d_units); hipFree(P.d_rec); hipFree(P.d_srec);
-        hipFree(P.d_csr);
-        for (Acc5* r : P.d_rec_alt) hipFree(r);
+        psx::dfree(P.d_units); psx::dfree(P.d_rec); psx::dfree(P.d_srec);
+        psx::dfree(P.d_csr);
+        for (Acc5* r : P.d_rec_alt) psx::dfree(r);
         for (int i = 0; i < 3; i++) if (P.ev[i]) hipEventDestroy(P.ev[i]);
     }
     C.plans.clear();
     free_k3(C);
     for (int s = 0; s < 2; s++) {
-        hipFree(C.d_skew[s]); C.d_skew[s] = nullptr;
-        hipFree(C.d_muS[s]); C.d_muS[s] = nullptr;
-        hipFree(C.d_nS[s]); C.d_nS[s] = nullptr;
+        psx::dfree(C.d_skew[s]); C.d_skew[s] = nullptr;
+        psx::dfree(C.d_muS[s]); C.d_muS[s] = nullptr;
+        psx::dfree(C.d_nS[s]); C.d_nS[s] = nullptr;
     }
-    hipFree(C.d_tab); C.d_tab = nullptr;
-    hipFree(C.d_redo); C.d_redo = nullptr;
-    if (C.own_flag) hipFree(C.d_flag);
+    psx::dfree(C.d_tab); C.d_tab = nullptr;
+    psx::dfree(C.d_redo); C.d_redo = nullptr;
+    if (C.own_flag) psx::dfree(C.d_flag);
     C.d_flag = nullptr;
 }
 

@@ -35,9 +35,9 @@ EXPORTED = [
     "psx_set_shard", "psx_run_exhaustive", "psx_run_configs", "psx_run_sss",
     "psx_eval_union_batch", "psx_reset", "psx_get_accum", "psx_partials_bytes",
     "psx_export_partials", "psx_merge_partials", "psx_get_timing", "psx_count_configs",
-    "psx_fold_partials_host", "psx_shard_stats", "psx_plan_units_k3", "psx_set_stream",
+    "psx_fold_partials_host", "psx_plan_hash", "psx_plan_build_ms", "psx_plan_csr_selftest", "psx_shard_stats", "psx_plan_units_k3", "psx_set_stream",
     "psx_psd_shift", "psx_lowrank_study", "psx_sym_eigen", "psx_lu_det",
-    "psx_create_from_ld", "psx_psd_shift_gpu", "psx_lu_det_gpu",
+    "psx_create_from_ld", "psx_psd_shift_gpu", "psx_lu_det_gpu", "psx_elim_gpu",
     "psx_run_exhaustive_async", "psx_sync", "psx_run_sss_sharded",
     "psx_multi_create", "psx_multi_create_from_ld", "psx_multi_run_exhaustive", "psx_multi_run_configs",
     "psx_multi_run_sss", "psx_multi_get_accum", "psx_multi_get_timing", "psx_multi_count",
@@ -96,10 +96,20 @@ class SetupInfo(ctypes.Structure):
         ("min_pivot_ratio", ctypes.c_double * 2),
         ("setup_ms", ctypes.c_double),
         ("spsq", ctypes.c_double * 2),
+        ("alloc_ms", ctypes.c_double),
+        ("studies_ms", ctypes.c_double),
+        ("tail_ms", ctypes.c_double),
+        ("study_upload_ms", ctypes.c_double * 2),
+        ("study_psd_ms", ctypes.c_double * 2),
+        ("study_finish_ms", ctypes.c_double * 2),
     ]
 
     def as_dict(self):
-        return {f: (list(getattr(self, f)) if f != "setup_ms" else self.setup_ms) for f, _ in self._fields_}
+        d = {}
+        for f, _ in self._fields_:
+            v = getattr(self, f)
+            d[f] = v if isinstance(v, float) else list(v)
+        return d
 
 
 class _Accum(ctypes.Structure):
@@ -127,6 +137,8 @@ class Timing(ctypes.Structure):
         ("exact_rerun", ctypes.c_int32),
         ("robust_units", ctypes.c_int32),
         ("span_ms", ctypes.c_double),
+        ("prepare_ms", ctypes.c_double),
+        ("run_ms", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -169,6 +181,10 @@ def load_library(path: str = LIB_PATH):
         "psx_get_timing": (c_int, [vp, P(Timing)]),
         "psx_count_configs": (c_u64, [P(_Problem)]),
         "psx_fold_partials_host": (c_int, [vp, c_i32, c_i64, vp]),
+        "psx_plan_hash": (c_int, [vp, P(ctypes.c_uint64)]),
+        "psx_plan_build_ms": (c_int, [c_i32, c_i32, c_i32, c_i32, P(dbl), P(c_i32), P(c_i64)]),
+        "psx_plan_csr_selftest": (c_int, [c_i32, P(ctypes.c_uint8), c_i32, c_i32, c_i32, c_i32, c_int, P(c_i64),
+                                          P(c_i64)]),
         "psx_set_stream": (c_int, [vp, vp]),
         "psx_shard_stats": (c_int, [P(_Problem), c_i32, c_i32, c_i32, P(c_u64), P(dbl)]),
         "psx_plan_units_k3": (c_int, [c_i32, c_i32, c_i32, P(c_i32), c_i32]),
@@ -179,6 +195,7 @@ def load_library(path: str = LIB_PATH):
         "psx_create_from_ld": (c_int, [P(_LdProblem), c_int, P(vp), P(SetupInfo)]),
         "psx_psd_shift_gpu": (c_int, [P(dbl), c_i32, P(dbl), c_int]),
         "psx_lu_det_gpu": (c_int, [P(dbl), c_i32, c_int, P(dbl)]),
+        "psx_elim_gpu": (c_int, [P(dbl), c_i32, P(dbl), c_i32, P(dbl), P(dbl), P(c_i32), c_int]),
         "psx_run_exhaustive_async": (c_int, [vp]),
         "psx_sync": (c_int, [vp, P(c_i32)]),
         "psx_run_sss_sharded": (c_int, [vp, ALLGATHER_FN, vp, P(c_i32)]),
@@ -202,8 +219,8 @@ def load_library(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.psx_abi_version() != 2 and os.environ.get("PSX_AB") != "1":
-        raise EngineError(PSX_ENODEV, f"{path}: ABI version {lib.psx_abi_version()}, this module needs 2")
+    if lib.psx_abi_version() != 3 and os.environ.get("PSX_AB") != "1":
+        raise EngineError(PSX_ENODEV, f"{path}: ABI version {lib.psx_abi_version()}, this module needs 3")
     _lib = lib
     return lib
 
@@ -244,6 +261,22 @@ def lu_det(a: np.ndarray, gpu: bool = False, device: int = 0) -> float:
     else:
         _check(lib.psx_lu_det(_ptr(aa, ctypes.c_double), aa.shape[0], ctypes.byref(d)))
     return d.value
+
+
+def elim_gpu(a: np.ndarray, z=None, check: bool = True, device: int = 0):
+    """The setup's swap-free elimination on the GPU (psx_elim_gpu): returns
+    (pivots U_ii, L^-1 z or None, swap_needed)."""
+    aa = np.ascontiguousarray(a, dtype=np.float64)
+    n = aa.shape[0]
+    piv = np.empty(n)
+    zz = None if z is None else np.ascontiguousarray(z, dtype=np.float64)
+    zt = None if z is None else np.empty(n)
+    sw = ctypes.c_int32(0)
+    _check(load_library().psx_elim_gpu(_ptr(aa, ctypes.c_double), n,
+                                       None if zz is None else _ptr(zz, ctypes.c_double), int(check),
+                                       _ptr(piv, ctypes.c_double), None if zt is None else _ptr(zt, ctypes.c_double),
+                                       ctypes.byref(sw), int(device)))
+    return piv, zt, bool(sw.value)
 
 
 def psd_shift_gpu(sigma: np.ndarray, device: int = 0):
@@ -395,11 +428,18 @@ class ModelInputs:
         return p
 
     def _ld_struct(self):
-        self._keep_ld = [self.m, np.concatenate([x.ravel() for x in self.ld]), np.concatenate(self.z),
+        # the ABI takes the studies' LDs concatenated; built once per ModelInputs
+        # (a 2 x 32 MB copy at M = 2000 is ~10 ms of host time per create)
+        key = tuple(id(x) for x in self.ld) + tuple(id(x) for x in self.z)
+        if getattr(self, "_ld_key", None) != key:
+            self._ld_key = key
+            self._ld_cat = np.concatenate([np.asarray(x, dtype=np.float64).ravel() for x in self.ld])
+            self._z_cat = np.concatenate([np.asarray(x, dtype=np.float64) for x in self.z])
+        self._keep_ld = [self.m, self._ld_cat, self._z_cat,
                          np.ascontiguousarray(self.union_to_local, dtype=np.int32),
                          np.ascontiguousarray(self.sample_sizes, dtype=np.int32)]
         m, ld, z, u2l, n = self._keep_ld
-        q = _LdProblem()
+        q = _LdProblem()  # (ld / z are read-only to the engine: the cached copies stay valid)
         q.n_studies = 2
         q.m = _ptr(m, ctypes.c_int32)
         q.ld = _ptr(ld, ctypes.c_double)
@@ -432,6 +472,27 @@ def fold_partials_host(images: np.ndarray) -> np.ndarray:
     return out
 
 
+def plan_build_ms(n_union: int, k: int = 3, rank: int = 0, world: int = 1):
+    """Host time of building a level's unit plan + record CSR (psx_plan_build_ms):
+    (ms, units, records)."""
+    ms, nu, nr = ctypes.c_double(0), ctypes.c_int32(0), ctypes.c_int64(0)
+    _check(load_library().psx_plan_build_ms(n_union, k, rank, world, ctypes.byref(ms), ctypes.byref(nu),
+                                            ctypes.byref(nr)))
+    return ms.value, nu.value, nr.value
+
+
+def plan_csr_selftest(n_union: int, k: int, rank: int, world: int, variant: int, presence=None, device: int = 0):
+    """GPU: (mismatches, records) of a plan's device-built record CSR against the
+    host restatement (psx_plan_csr_selftest)."""
+    bad, nrec = ctypes.c_int64(0), ctypes.c_int64(0)
+    pr = None
+    if presence is not None:
+        pr = np.ascontiguousarray(presence, dtype=np.uint8)
+    _check(load_library().psx_plan_csr_selftest(n_union, None if pr is None else _ptr(pr, ctypes.c_uint8), k, rank,
+                                                world, variant, int(device), ctypes.byref(bad), ctypes.byref(nrec)))
+    return bad.value, nrec.value
+
+
 def plan_units_k3(n_union: int, rank: int = 0, world: int = 1) -> np.ndarray:
     """The k = 3 fast sweep's work units of one shard (host-only diagnostics):
     int32 [n, 4] rows {a0, a1, K | j0 << 16, C | j1 << 16} in dispatch order."""
@@ -448,6 +509,17 @@ ACC5_DTYPE = np.dtype([("mP", "<i4"), ("mS", "<i4"), ("mN", "<i4"), ("pad", "<i4
                        ("post1", "<f8"), ("shared", "<f8"), ("sll", "<f8"), ("nsll", "<f8")])
 SETREC_DTYPE = np.dtype([("m", "<i4"), ("m0", "<i4"), ("m1", "<i4"), ("pad", "<i4"), ("tot", "<f8"),
                          ("nc0", "<f8"), ("nc1", "<f8"), ("score", "<f8"), ("npat", "<f8")])
+# last slot of an image: which shard of which plan (psx_math.h PlanTag)
+PLANTAG_DTYPE = np.dtype([("magic", "<i4"), ("world", "<i4"), ("rank", "<i4"), ("U", "<i4"), ("hash", "<u8"),
+                          ("pad", "<u8", (4,))])
+PLAN_MAGIC = 0x54585350
+
+
+def plan_tag(rank: int, world: int, U: int, hash_: int) -> bytes:
+    """The PlanTag slot of a partial image (for images built on the host)."""
+    t = np.zeros(1, dtype=PLANTAG_DTYPE)
+    t["magic"], t["world"], t["rank"], t["U"], t["hash"] = PLAN_MAGIC, world, rank, U, hash_
+    return t.tobytes()
 
 
 @dataclass
@@ -575,6 +647,12 @@ class PostCal:
 
     def set_shard(self, rank: int, world: int):
         _check(self.lib.psx_set_shard(self.h, rank, world))
+
+    def plan_hash(self) -> int:
+        """The shard plan's hash (psx_plan_hash): equal on every rank of a job."""
+        h = ctypes.c_uint64(0)
+        _check(self.lib.psx_plan_hash(self.h, ctypes.byref(h)))
+        return int(h.value)
 
     def run_exhaustive(self):
         """postcal.cpp:716 computeTotalLikelihood."""

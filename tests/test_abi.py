@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
     for name in decl:
         assert re.search(rf"\bT {name}\b", dyn), name
         assert getattr(lib, name)
-    assert lib.psx_abi_version() == 2  # 2: psx_timing.span_ms
+    assert lib.psx_abi_version() == 3  # 3: psx_timing.prepare_ms / run_ms, setup phases, partial-image PlanTag
 
 
 def test_no_cpu_fallback():
@@ -97,25 +97,33 @@ def test_k3_block_pattern_plan_counts(U, world):
     assert abs(cfg - 27 * math.comb(U, 3)) < 0.5
 
 
+def _tagged(raw, rank, world, U=100, h=0x1234):
+    """An image with its PlanTag slot (the last 56 bytes) set."""
+    return np.frombuffer(bytes(raw[:-56]) + E.plan_tag(rank, world, U, h), dtype=np.uint8)
+
+
 def test_partial_fold_is_associative_and_order_fixed():
     rng = np.random.default_rng(0)
     ldg = 128
     imgs = []
     for r in range(4):
-        a = np.zeros(ldg + 1, dtype=E.ACC5_DTYPE)
+        a = np.zeros(ldg + 2, dtype=E.ACC5_DTYPE)
         for f in ("mP", "mS", "mN"):
-            a[f] = rng.integers(-3000, 3000, ldg + 1)
+            a[f] = rng.integers(-3000, 3000, ldg + 2)
         for f in ("post0", "post1", "shared", "sll", "nsll"):
-            a[f] = rng.random(ldg + 1) * (rng.random(ldg + 1) > 0.2)
+            a[f] = rng.random(ldg + 2) * (rng.random(ldg + 2) > 0.2)
         s = np.zeros(1, dtype=E.SETREC_DTYPE)
         s["m"], s["m0"], s["m1"] = rng.integers(-50, 50), -70, 3
         s["tot"], s["nc0"], s["nc1"], s["score"], s["npat"] = 1.5, 0.5, 0.25, -3.0, 7
         raw = a.tobytes()
-        raw = raw[: ldg * 56] + s.tobytes()
+        raw = raw[: ldg * 56] + s.tobytes() + E.plan_tag(r, 4, 100, 0x1234)
         imgs.append(np.frombuffer(raw, dtype=np.uint8))
     imgs = np.stack(imgs)
     full = E.fold_partials_host(imgs)
-    left = E.fold_partials_host(np.stack([E.fold_partials_host(imgs[:2]), E.fold_partials_host(imgs[2:])]))
+    # a fold is a world-1 image: the halves are re-tagged as shards 0 / 1 of 2
+    pair = [np.stack([_tagged(imgs[i], 0, 2), _tagged(imgs[i + 1], 1, 2)]) for i in (0, 2)]
+    halves = [_tagged(E.fold_partials_host(pair[0]), 0, 2), _tagged(E.fold_partials_host(pair[1]), 1, 2)]
+    left = E.fold_partials_host(np.stack(halves))
     A = np.frombuffer(full[: ldg * 56].tobytes(), dtype=E.ACC5_DTYPE)
     B = np.frombuffer(left[: ldg * 56].tobytes(), dtype=E.ACC5_DTYPE)
 
@@ -125,6 +133,27 @@ def test_partial_fold_is_associative_and_order_fixed():
         np.testing.assert_allclose(val(A, m, s), val(B, m, s), rtol=0, atol=1e-12)
     sa = np.frombuffer(full[ldg * 56: ldg * 56 + 56].tobytes(), dtype=E.SETREC_DTYPE)[0]
     assert sa["npat"] == 28 and sa["score"] == -3.0
+    tag = np.frombuffer(full[-56:].tobytes(), dtype=E.PLANTAG_DTYPE)[0]
+    assert (tag["magic"], tag["world"], tag["rank"], tag["hash"]) == (E.PLAN_MAGIC, 1, 0, 0x1234)
+
+
+def test_mismatched_plan_images_are_refused():
+    """Images of ranks that cut different plans (another hash: other PSX_K3_*
+    knobs or build), out of rank order, of another world size, or without a
+    tag are refused by the fold (the device merge checks the same tags)."""
+    ldg = 64
+    base = np.zeros((ldg + 2) * 56, dtype=np.uint8)
+    good = [_tagged(base, r, 3) for r in range(3)]
+    E.fold_partials_host(np.stack(good))
+    bad_cases = {
+        "hash": [good[0], good[1], _tagged(base, 2, 3, h=0x1235)],
+        "order": [good[1], good[0], good[2]],
+        "world": [good[0], good[1], _tagged(base, 2, 4)],
+        "untagged": [good[0], good[1], base],
+    }
+    for name, imgs in bad_cases.items():
+        with pytest.raises(E.EngineError, match="one plan"):
+            E.fold_partials_host(np.stack(imgs))
 
 
 def test_model_inputs_shape_helpers_without_gpu():

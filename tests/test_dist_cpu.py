@@ -24,18 +24,19 @@ def _port():
     return p
 
 
-def _image(rank, ldg=256):
+def _image(rank, world=2, ldg=256):
     rng = np.random.default_rng(100 + rank)
-    a = np.zeros(ldg + 1, dtype=E.ACC5_DTYPE)
+    a = np.zeros(ldg + 2, dtype=E.ACC5_DTYPE)
     for f in ("mP", "mS", "mN"):
-        a[f] = rng.integers(-2000, 2000, ldg + 1)
+        a[f] = rng.integers(-2000, 2000, ldg + 2)
     for f in ("post0", "post1", "shared", "sll", "nsll"):
-        a[f] = rng.random(ldg + 1) * (rng.random(ldg + 1) > 0.3)
+        a[f] = rng.random(ldg + 2) * (rng.random(ldg + 2) > 0.3)
     raw = bytearray(a.tobytes())
     s = np.zeros(1, dtype=E.SETREC_DTYPE)
     s["m"], s["m0"], s["m1"] = rank * 3, -rank, 2 * rank
     s["tot"], s["nc0"], s["nc1"], s["score"], s["npat"] = 1.0 + rank, 0.5, 0.25, -rank, 10 + rank
     raw[ldg * 56: ldg * 56 + s.itemsize] = s.tobytes()
+    raw[(ldg + 1) * 56:] = E.plan_tag(rank, world, 200, 0xABC)
     return np.frombuffer(bytes(raw), dtype=np.uint8)
 
 

@@ -289,16 +289,78 @@ def _elim_spsq(a, z):
     return q
 
 
-@pytest.mark.parametrize("M,glob", [(1, 0), (2, 0), (15, 0), (16, 0), (17, 0), (33, 0), (300, 0), (1000, 0),
-                                    (2000, 0), (17, 1), (300, 1)])
-def test_blocked_swap_free_elimination_bit_identical(gpu, M, glob, monkeypatch):
-    """The blocked (panel + delayed trailing update) swap-free elimination of
-    psx_setup.hip gives the per-column elimination's pivots bit for bit:
-    the setup's min pivot ratio equals the host restatement's exactly, on
-    sizes around the 16-column panel and on the SYN-v1 LDs (M = 2000: 8-column
-    panels in LDS); glob = 1 forces the global-memory panel kernel."""
-    if glob:
-        monkeypatch.setenv("PSX_LU_GLOBAL", "1")
+def _elim(a, z, check=True):
+    """Host restatement of the tiled kernels' contract (psx_elim_gpu): the
+    per-column elimination without pivoting (a zero pivot skips its step, as
+    GSL does), z's forward solve riding along, and whether GSL's pivot search
+    would have swapped some row (some |a_ij| > |a_jj| below the diagonal, NaNs
+    never chosen)."""
+    a = np.array(a, dtype=np.float64, copy=True)
+    z = np.array(z, dtype=np.float64, copy=True)
+    n = a.shape[0]
+    swap = False
+    for j in range(n - 1):
+        if check and a[j, j] == a[j, j] and (np.abs(a[j + 1:, j]) > abs(a[j, j])).any():
+            swap = True
+        if a[j, j] == 0.0:
+            continue
+        l = a[j + 1:, j] / a[j, j]
+        a[j + 1:, j + 1:] -= np.outer(l, a[j, j + 1:])
+        z[j + 1:] -= l * z[j]
+    return np.diag(a).copy(), z, swap
+
+
+def _tiled_cases():
+    cases = []
+    for n in (1, 2, 15, 16, 17, 31, 32, 33, 63, 64, 65, 79, 80, 81, 96, 97, 129, 200, 333):
+        idx = np.arange(n)
+        rng = np.random.default_rng(n)
+        a = 0.9 ** np.abs(idx[:, None] - idx[None, :]) + 0.01 * rng.standard_normal((n, n))
+        a[idx, idx] += 0.5
+        cases.append((f"ld{n}", a))
+    # zero pivots (steps skipped, no swap needed: the column below is zero too)
+    n = 70
+    a = np.eye(n) * 2.0 + 0.1 * np.random.default_rng(7).standard_normal((n, n))
+    for j in (3, 16, 17, 40, 69):
+        a[j, :] = 0.0
+        a[:, j] = 0.0
+    cases.append(("zero-pivots", a))
+    # a row swap needed in a diagonal block, and one below it (check mode flags both)
+    b = cases[13][1].copy()  # n = 81
+    b[5, 2] = 10.0
+    cases.append(("swap-in-block", b))
+    c = cases[13][1].copy()
+    c[70, 20] = 10.0
+    cases.append(("swap-below-block", c))
+    return cases
+
+
+@pytest.mark.parametrize("name,a", _tiled_cases(), ids=[c[0] for c in _tiled_cases()])
+def test_tiled_elimination_bit_identical(gpu, name, a):
+    """The tiled swap-free elimination (k_lu_diag + one k_lu_tile per 16-column
+    panel, every tile recomputing its rows' L chains and columns' U solves from
+    the published diagonal block) gives every pivot U_ii and every z~_i of the
+    per-column elimination bit for bit, on sizes around the panel / tile edges,
+    with skipped (zero) pivots, and raises the swap flag exactly when GSL's
+    pivot search would swap; with the check off (the setup's step 2) the
+    pivots are the unpivoted elimination's."""
+    z = np.random.default_rng(11).standard_normal(a.shape[0])
+    for check in (True, False):
+        piv, zt, sw = E.elim_gpu(a, z, check=check)
+        hp, hz, hs = _elim(a, z, check=check)
+        assert sw == hs, (name, check, sw, hs)
+        if sw:
+            continue
+        assert np.array_equal(piv.view(np.uint64), hp.view(np.uint64)), (name, check, np.flatnonzero(piv != hp)[:5])
+        assert np.array_equal(zt.view(np.uint64), hz.view(np.uint64)), (name, check, np.flatnonzero(zt != hz)[:5])
+
+
+@pytest.mark.parametrize("M", [1, 2, 15, 16, 17, 33, 300, 1000, 2000])
+def test_blocked_swap_free_elimination_bit_identical(gpu, M):
+    """The tiled swap-free elimination of psx_setup.hip gives the per-column
+    elimination's pivots bit for bit inside the setup: the setup's min pivot
+    ratio equals the host restatement's exactly, on sizes around the 16-column
+    panel and on the SYN-v1 LDs."""
     if M >= 1000:
         ld, z, _, _, u2l = synth.syn_v1(M)
     else:
