@@ -10,28 +10,25 @@
 // Q|W|Q^T, z and z^T Q|W|^-1 Q^T z, so whenever Sigma' is positive definite
 // they are exactly Sigma', z and z^T Sigma'^-1 z: no eigendecomposition.
 //
-//  * Step 1 runs here as a right-looking elimination, blocked (an LDS panel
-//    of <= kPanel columns, trailing updates delayed; swap-free LDs without
-//    pivot search, others with GSL's pivot and the swaps replayed on the
-//    trailing columns; per-column launches past the LDS budget), with the
-//    reference's operation
-//    order and IEEE rounding (division correctly rounded, multiply and
-//    subtract not fused), so the per-element update sequence — and hence
+//  * Step 1 runs here as a right-looking elimination with the reference's
+//    operation order and IEEE rounding (division correctly rounded, multiply
+//    and subtract not fused), so the per-element update sequence — and hence
 //    every U_ii and the index-order determinant product — is bit-identical to
 //    the host restatement psx_psd_shift (model.cpp), the oracle of this step.
+//    Swap-free LDs (every SYN-v1 locus) take the tiled kernels: one launch
+//    per 16-column panel, each block factoring the panel's diagonal block with
+//    its tile's rows and applying the delayed updates to its tile (k_lu_step,
+//    ~5-12 us per panel; M = 2000 in 2.7 ms).  An LD that needs a row swap
+//    takes GSL's pivot search in LDS panels (k_lu_panel_piv + k_lu_trail).
 //  * Positive definiteness and z^T Sigma'^-1 z come from one elimination
 //    without pivoting of the symmetrised Sigma' (its pivots are the D of
 //    L D L^T) with the forward solve of z fused in.  When some pivot is not
 //    comfortably positive (ratio to the largest diagonal < kPdRatio) the
-//    caller falls back to the reference's eigen route (host restatement).
-//
-// The trailing update is an HBM/L2 streaming kernel (one read-modify-write of
-// the trailing matrix per panel); the matrix (32 MB at M = 2000) stays
-// L2/MALL resident.  The panel kernel is one workgroup on one CU (its LDS
-// throughput bounds it); launch latency dominates below a few hundred rows.
+//    caller falls back to the reference's eigen route (rocSOLVER, psx_eigen.hip).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -137,40 +134,24 @@ __global__ __launch_bounds__(kElimCols) void k_elim(double* __restrict__ A, int 
 // min(i, k), a_ik <- a_ik - l_iq * u_qk (multiply and subtract not fused), in
 // increasing q.  Any schedule that applies those updates in increasing q with
 // the same l_iq and u_qk gives every element — U_ii, z~ — bit for bit what the
-// per-column elimination gives.  Without pivoting the panel factorisation is
-// row-local once its nb x nb diagonal block D is factored: row i's panel
+// per-column elimination gives.  Without pivoting a panel's factorisation is
+// row-local once its 16 x 16 diagonal block D is factored: row i's panel
 // entries take l_iq = a_iq / u_qq and a_ic -= l_iq u_qc (c > q in the panel),
-// and column k's U entries take u_rk -= l_rq u_qk (q < r, l from D).  So one
-// launch per panel does everything (k_lu_tile), one 64 x 64 tile of the
-// trailing matrix per block:
-//   wave 0  the L chain of the tile's 64 rows (lane = row, the row's panel
-//           entries in registers, u_qq / u_qc broadcast from LDS), the swap
-//           check of those rows (GSL's pivot: the first row of maximal |a_iq|,
-//           NaNs never chosen — a row swap is needed iff some |a_iq| > |u_qq|,
-//           i > q; *flag is raised and the caller reruns the pivoting path
-//           from a fresh copy) and, in column-tile 0 blocks, z's forward solve;
-//   wave 1  the U-row solve of the tile's 64 columns (lane = column);
-//   all     the panel's nb delayed updates of the tile (16 rows per wave),
-//           whose loads were issued at the top of the kernel;
-//   block (0, 0) then factors the NEXT panel's diagonal block (the top-left
-//           corner of its own tile, already updated) in one wave's registers
-//           and publishes it (k_lu_diag for the first panel).
-// L and U of the panels are recomputed per tile (redundantly across tiles,
-// identically), never stored: the setup consumes U_ii and z~ only.  A ends with
-// every diagonal block factored in place (U_ii on the diagonal).  A zero u_qq
-// skips step q (GSL), as a bit in the block's skip mask.
-constexpr int kPanel = 16;     // panel width (k_lu_tile, k_lu_panel_piv)
+// column k's U entries take u_rk -= l_rq u_qk (q < r, l from D).  So one
+// launch per panel (k_lu_step, below) does a panel: every block factors D and
+// its tile rows' L chains in one pass, solves its tile columns' U rows and
+// applies the delayed updates to its tile; L and U are recomputed per tile
+// (identically), never stored — the setup consumes U_ii and z~ only.  The
+// swap check (GSL's pivot: the first row of maximal |a_iq|, NaNs never chosen,
+// so a swap is needed iff some |a_iq| > |u_qq|, i > q) raises *flag, and the
+// caller reruns the pivoting path from a fresh copy.  A zero u_qq skips step q
+// (GSL).
+constexpr int kPanel = 16;     // panel width (k_lu_step, k_lu_panel_piv)
 constexpr int kPanelThreads = 1024;
-constexpr int kTile = 64;      // trailing tile edge (k_lu_tile): lane = column
-constexpr int kTileWaves = 4;  // rows kTile / kTileWaves per wave in the update
 constexpr int kTrCols = 64;
 constexpr int kTrRows = 32;
 constexpr int kTrGroups = 4;  // row groups per trailing block (kTrRows / kTrGroups rows per thread)
 constexpr int kPanelLds = 152 * 1024;  // dynamic LDS budget of k_lu_panel_piv (160 KB per CU; 158 KB is refused)
-
-// a published diagonal block: a[kPanel][kPanel] packed LU (row-major, l below
-// the diagonal, u on and above), z[kPanel] (final), skip mask (bit q: u_qq == 0)
-constexpr int kDblk = kPanel * kPanel + kPanel + 1;
 
 __device__ inline double rdlane(double v, int l) {
     const long long b = __builtin_bit_cast(long long, v);
@@ -183,37 +164,32 @@ __device__ inline double rdlane(double v, int l) {
 // (lane r < nb: row j + r, v[c] = a_{j+r, j+c} after every earlier panel's
 // updates, zr = z_{j+r} likewise) with the per-column elimination's operations;
 // rows of the block below q are checked for a needed swap.  Writes the block
-// back to A (in place), the published copy to dblk, z to z.
+// back to A (in place) and z to z.
 __device__ void factor_diag(double (&v)[kPanel], double zr, int j, int nb, double* __restrict__ A, int n,
-                            double* __restrict__ z, double* __restrict__ dblk, int check, int* __restrict__ flag) {
+                            double* __restrict__ z, int check, int* __restrict__ flag) {
 #pragma clang fp contract(off)
     const int r = threadIdx.x & 63;
     const bool row = r < nb;
-    unsigned long long skip = 0;
     bool sw = false;
 #pragma unroll
     for (int q = 0; q < kPanel; q++) {
         const double uqq = rdlane(v[q], q);
-        if (q < nb) {  // uniform (nb < kPanel only for the last block)
-            if (check && uqq == uqq && row && r > q && fabs(v[q]) > fabs(uqq)) sw = true;
-            if (uqq == 0.0) {  // uniform: step q is skipped
-                skip |= 1ull << q;
-            } else {
-                const double zq = rdlane(zr, q);
-                double uq[kPanel];
+        const bool step = q < nb;  // uniform (nb < kPanel only for the last block)
+        if (check && step && uqq == uqq && row && r > q && fabs(v[q]) > fabs(uqq)) sw = true;
+        // u_qq == 0 skips step q (GSL): a lane predicate below, no branch
+        const double zq = rdlane(zr, q);
+        double uq[kPanel];
 #pragma unroll
-                for (int c = q + 1; c < kPanel; c++) uq[c] = rdlane(v[c], q);
-                if (row && r > q) {
-                    const double l = v[q] / uqq;
-                    v[q] = l;
-                    const double pz = l * zq;
-                    zr = zr - pz;
+        for (int c = q + 1; c < kPanel; c++) uq[c] = rdlane(v[c], q);
+        if (step && row && r > q && uqq != 0.0) {
+            const double l = v[q] / uqq;
+            v[q] = l;
+            const double pz = l * zq;
+            zr = zr - pz;
 #pragma unroll
-                    for (int c = q + 1; c < kPanel; c++) {
-                        const double p = l * uq[c];
-                        v[c] = v[c] - p;
-                    }
-                }
+            for (int c = q + 1; c < kPanel; c++) {
+                const double p = l * uq[c];
+                v[c] = v[c] - p;
             }
         }
     }
@@ -221,96 +197,150 @@ __device__ void factor_diag(double (&v)[kPanel], double zr, int j, int nb, doubl
     if (row) {
 #pragma unroll
         for (int c = 0; c < kPanel; c++)
-            if (c < nb) {
-                A[(size_t)(j + r) * n + j + c] = v[c];
-                dblk[r * kPanel + c] = v[c];
-            }
-        dblk[kPanel * kPanel + r] = zr;
+            if (c < nb) A[(size_t)(j + r) * n + j + c] = v[c];
         if (z) z[j + r] = zr;
     }
-    if (r == 0) dblk[kPanel * kPanel + kPanel] = __builtin_bit_cast(double, skip);
 }
 
-// the first panel's diagonal block (one wave)
-__global__ __launch_bounds__(64) void k_lu_diag(double* __restrict__ A, int n, int nb, double* __restrict__ z,
-                                                double* __restrict__ dblk, int check, int* __restrict__ flag) {
-    const int r = threadIdx.x;
+// the diagonal block at (j, j) of n - j <= kPanel rows, factored in place (the
+// last one, after k_lu_step's panels); then the earlier panels' U_ii and final
+// z (dg / zf, kept aside by k_lu_step) go to A's diagonal and z
+__global__ __launch_bounds__(64) void k_lu_diag_at(double* __restrict__ A, int n, int j, double* __restrict__ z,
+                                                   int check, int* __restrict__ flag, const double* __restrict__ dg,
+                                                   const double* __restrict__ zf) {
+    const int r = threadIdx.x, nb = n - j;
     double v[kPanel];
 #pragma unroll
-    for (int c = 0; c < kPanel; c++) v[c] = (r < nb && c < nb) ? A[(size_t)r * n + c] : 0.0;
-    const double zr = (z && r < nb) ? z[r] : 0.0;
-    factor_diag(v, zr, 0, nb, A, n, z, dblk, check, flag);
+    for (int c = 0; c < kPanel; c++) v[c] = (r < nb && c < nb) ? A[(size_t)(j + r) * n + j + c] : 0.0;
+    const double zr = (z && r < nb) ? z[j + r] : 0.0;
+    factor_diag(v, zr, j, nb, A, n, z, check, flag);
+    for (int i = r; i < j; i += 64) {
+        A[(size_t)i * n + i] = dg[i];
+        if (z) z[i] = zf[i];
+    }
 }
 
-// One panel (columns j0 .. j0 + kPanel - 1, diagonal block factored in din) on the
-// trailing tile (rows i0 .. i0 + 63, columns k0 .. k0 + 63; i0, k0 >= j1 =
-// j0 + nb); block (0, 0) then factors the next panel's diagonal block (nbn
-// columns from j1) into dout.
-__global__ __launch_bounds__(kTile * kTileWaves) void k_lu_tile(double* __restrict__ A, int n, int j0, int nbn,
-                                                                double* __restrict__ z, const double* __restrict__ din,
-                                                                double* __restrict__ dout, int check,
-                                                                int* __restrict__ flag) {
+// One launch per panel, v2 (k_lu_step): no published diagonal block.  Every
+// block factors the panel's diagonal block D itself, merged with its tile rows'
+// L chains into one right-looking pass over a 64-row panel per "row wave"
+// (lanes 0 .. 15: D's rows j0 .. j0 + 15, lanes 16 .. 63: 48 tile rows): at
+// step q lane q holds the pivot row, broadcast by readlane, and every lane
+// below it takes l = a_q / u_qq and its updates — the per-column elimination's
+// operations on these elements, in its order.  Then CW "column waves" solve the
+// tile's 64 CW columns' U rows with D's l (LDS), and all 16 waves apply the
+// panel's delayed updates to the (48 RW) x (64 CW) tile.  The tile shape is
+// picked per panel so that one round of blocks (one 1024-thread block per CU)
+// covers the trailing matrix.  Block (0, 0) keeps D's U_ii and final z aside
+// (every block of the launch reads D's rows from A), and k_lu_diag_at factors
+// the last diagonal block and writes them all back.
+constexpr int kStepRows = 48;   // tile rows per row wave (it holds them with D's 16)
+constexpr int kStepWaves = 16;  // waves per block
+static_assert(kStepRows + kPanel == 64, "a row wave holds D and its tile rows");
+
+template <int RW, int CW>
+__global__ __launch_bounds__(64 * kStepWaves) void k_lu_step(double* __restrict__ A, int n, int j0,
+                                                               double* __restrict__ z, int check,
+                                                               int* __restrict__ flag, double* __restrict__ dg,
+                                                               double* __restrict__ zf,
+                                                               unsigned long long* __restrict__ tr) {
 #pragma clang fp contract(off)
-    constexpr int kRows = kTile / kTileWaves;
-    __shared__ double sD[kPanel][kPanel + 1];  // D: l below, u on and above
-    __shared__ double sZ[kPanel];
-    __shared__ double sL[kTile][kPanel + 1];  // l of the tile's rows
-    __shared__ double sU[kPanel][kTile];      // u of the tile's columns
-    __shared__ double sN[kPanel][kPanel + 1];  // block (0, 0): the next diagonal block
+    constexpr int nb = kPanel;
+    constexpr int TR = kStepRows * RW, TC = 64 * CW;
+    constexpr int kSets = kStepWaves / CW;     // row sets in the update (wave w: column group w % CW)
+    constexpr int kRows = TR / kSets;          // rows per wave in the update
+    static_assert(RW + CW <= kStepWaves && TR % kSets == 0, "tile shape");
+    __shared__ double sD[kPanel][kPanel + 1];  // D factored: l below, u on and above
+    __shared__ double sL[TR][kPanel + 1];      // l of the tile's rows
+    __shared__ double sU[kPanel][TC];          // u of the tile's columns
+    __shared__ unsigned long long sSkip;
+    const int tb = (blockIdx.x == 0 && blockIdx.y == 0) ? 0 : (blockIdx.x == 1 && blockIdx.y == 1) ? 1 : -1;
+    auto stamp = [&](int i) {
+        if (tr && tb >= 0 && threadIdx.x == 0) tr[tb * 8 + i] = wall_clock64();
+    };
+    stamp(0);
     if (check && *flag) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    constexpr int nb = kPanel;  // every panel with a trailing matrix is full width
     const int j1 = j0 + nb;
-    const int i0 = j1 + blockIdx.y * kTile, k0 = j1 + blockIdx.x * kTile;
-    const int k = k0 + lane;
+    const int i0 = j1 + blockIdx.y * TR, k0 = j1 + blockIdx.x * TC;
     const bool corner = blockIdx.x == 0 && blockIdx.y == 0;
-    // the update's operands first: their latency hides behind the chains
-    double t[kRows];
+    // the update's operands first (its first chunk of rows): their latency hides
+    // behind the panel pass
+    const int cg = w % CW, rs = w / CW;  // this wave's column group and row set
+    const int k = k0 + 64 * cg + lane;
+    constexpr int kChunk = kRows < 6 ? kRows : 6;  // rows in registers at a time (more spill)
+    static_assert(kRows % kChunk == 0, "update chunks");
+    double t[kChunk];
+    auto load_chunk = [&](int c0) {
 #pragma unroll
-    for (int m = 0; m < kRows; m++) {
-        const int i = i0 + w * kRows + m;
-        t[m] = (i < n && k < n) ? A[(size_t)i * n + k] : 0.0;
-    }
-    const unsigned long long skip = __builtin_bit_cast(unsigned long long, din[kPanel * kPanel + kPanel]);
-    double v[kPanel];  // wave 0: the row's panel entries; wave 1: the column's panel rows
-    const int i = i0 + lane;
-    double zi = 0.0;
-    if (w == 0) {
+        for (int m = 0; m < kChunk; m++) {
+            const int i = i0 + rs * kRows + c0 + m;
+            t[m] = (i < n && k < n) ? A[(size_t)i * n + k] : 0.0;
+        }
+    };
+    load_chunk(0);
+    double v[kPanel];
+    if (w < RW) {
+        // lane r < 16: D's row j0 + r; lane r >= 16: tile row i0 + 48 w + r - 16
+        const int row = lane < nb ? j0 + lane : i0 + kStepRows * w + lane - nb;
+        const bool live = row < n;
 #pragma unroll
-        for (int c = 0; c < kPanel; c++) v[c] = (i < n && c < nb) ? A[(size_t)i * n + j0 + c] : 0.0;
-        if (z && blockIdx.x == 0 && i < n) zi = z[i];
-    } else if (w == 1) {
-#pragma unroll
-        for (int c = 0; c < kPanel; c++) v[c] = (k < n && c < nb) ? A[(size_t)(j0 + c) * n + k] : 0.0;
-    } else {
-        for (int e = threadIdx.x - 128; e < kPanel * kPanel; e += 128) sD[e / kPanel][e % kPanel] = din[e];
-        if (threadIdx.x - 128 < kPanel) sZ[threadIdx.x - 128] = din[kPanel * kPanel + threadIdx.x - 128];
-    }
-    __syncthreads();
-    if (w == 0) {  // L chain of row i (+ swap check, + z in column-tile 0)
+        for (int c = 0; c < kPanel; c++) v[c] = live ? A[(size_t)row * n + j0 + c] : 0.0;
+        double zr = (z && live && (lane < nb || blockIdx.x == 0)) ? z[row] : 0.0;
+        unsigned long long skip = 0;
         bool sw = false;
 #pragma unroll
         for (int q = 0; q < kPanel; q++) {
-            const double uqq = sD[q][q];
-            if (check && uqq == uqq && i < n && fabs(v[q]) > fabs(uqq)) sw = true;
-            if ((skip >> q) & 1) {
-                sL[lane][q] = 0.0;
-                continue;
-            }
-            const double l = v[q] / uqq;
-            sL[lane][q] = l;
-            const double pz = l * sZ[q];
-            zi = zi - pz;
+            const double uqq = rdlane(v[q], q);
+            const bool below = lane > q && live;  // D rows below the pivot, every tile row
+            if (check && uqq == uqq && below && fabs(v[q]) > fabs(uqq)) sw = true;
+            // u_qq == 0 skips step q (GSL): folded into the lane predicate, no
+            // uniform branch (one made the compiler copy the whole row per step)
+            if (uqq == 0.0) skip |= 1ull << q;
+            const double zq = rdlane(zr, q);
+            double uq[kPanel];
 #pragma unroll
-            for (int c = q + 1; c < kPanel; c++) {
-                const double p = l * sD[q][c];
-                v[c] = v[c] - p;
+            for (int c = q + 1; c < kPanel; c++) uq[c] = rdlane(v[c], q);
+            if (below && uqq != 0.0) {
+                const double l = v[q] / uqq;
+                v[q] = l;
+                const double pz = l * zq;
+                zr = zr - pz;
+#pragma unroll
+                for (int c = q + 1; c < kPanel; c++) {
+                    const double p = l * uq[c];
+                    v[c] = v[c] - p;
+                }
             }
         }
         if (check && __any(sw) && lane == 0) *flag = 1;
-        // z of the rows the next diagonal block factors is written with it
-        if (z && blockIdx.x == 0 && i < n && !(corner && lane < nbn)) z[i] = zi;
-    } else if (w == 1) {  // U-row solve of column k
+        if (lane < nb) {
+            if (w == 0) {
+#pragma unroll
+                for (int c = 0; c < kPanel; c++) sD[lane][c] = v[c];
+                // D's U_ii and final z to the side arrays: every block of this launch
+                // reads D's rows and z from A / z, so nothing is written back there
+                if (corner) {
+#pragma unroll
+                    for (int c = 0; c < kPanel; c++)
+                        if (c == lane) dg[j0 + lane] = v[c];
+                    zf[j0 + lane] = zr;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < kPanel; c++) sL[kStepRows * w + lane - nb][c] = v[c];
+            if (z && blockIdx.x == 0 && live) z[row] = zr;
+        }
+        if (w == 0 && lane == 0) sSkip = skip;
+    } else if (w < RW + CW) {
+        const int kc = k0 + 64 * (w - RW) + lane;
+#pragma unroll
+        for (int c = 0; c < kPanel; c++) v[c] = (kc < n) ? A[(size_t)(j0 + c) * n + kc] : 0.0;
+    }
+    __syncthreads();
+    stamp(1);
+    const unsigned long long skip = sSkip;
+    if (w >= RW && w < RW + CW) {  // U-row solve of column k0 + 64 (w - RW) + lane with D's l
 #pragma unroll
         for (int r = 1; r < kPanel; r++) {
 #pragma unroll
@@ -321,36 +351,53 @@ __global__ __launch_bounds__(kTile * kTileWaves) void k_lu_tile(double* __restri
             }
         }
 #pragma unroll
-        for (int q = 0; q < kPanel; q++) sU[q][lane] = v[q];
+        for (int q = 0; q < kPanel; q++) sU[q][64 * (w - RW) + lane] = v[q];
     }
     __syncthreads();
+    stamp(2);
+    double uc[kPanel];  // this lane's column of the panel's U rows
 #pragma unroll
-    for (int q = 0; q < kPanel; q++) {
-        if ((skip >> q) & 1) continue;
-        const double uq = sU[q][lane];
+    for (int q = 0; q < kPanel; q++) uc[q] = sU[q][64 * cg + lane];
 #pragma unroll
-        for (int m = 0; m < kRows; m++) {
-            const double p = sL[w * kRows + m][q] * uq;
-            t[m] = t[m] - p;
+    for (int c0 = 0; c0 < kRows; c0 += kChunk) {
+        if (c0 > 0) load_chunk(c0);
+#pragma unroll
+        for (int q = 0; q < kPanel; q++) {
+            if ((skip >> q) & 1) continue;
+#pragma unroll
+            for (int m = 0; m < kChunk; m++) {
+                const double p = sL[rs * kRows + c0 + m][q] * uc[q];
+                t[m] = t[m] - p;
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < kChunk; m++) {
+            const int ii = i0 + rs * kRows + c0 + m;
+            if (ii < n && k < n) A[(size_t)ii * n + k] = t[m];
         }
     }
-#pragma unroll
-    for (int m = 0; m < kRows; m++) {
-        const int r = w * kRows + m;
-        const int ii = i0 + r;
-        if (ii >= n || k >= n) continue;
-        if (corner && r < nbn && lane < nbn)
-            sN[r][lane] = t[m];
-        else
-            A[(size_t)ii * n + k] = t[m];
-    }
-    if (!corner || nbn <= 0) return;
-    __syncthreads();
-    if (w != 0) return;
-    double d[kPanel];
-#pragma unroll
-    for (int c = 0; c < kPanel; c++) d[c] = (lane < nbn && c < nbn) ? sN[lane][c] : 0.0;
-    factor_diag(d, zi, j1, nbn, A, n, z, dout, check, flag);
+    stamp(3);
+}
+
+// one panel's k_lu_step: the smallest tile whose grid fits one round of blocks
+// (one 1024-thread block per CU), else the largest
+void launch_lu_step(double* A, int n, int j0, double* z, int check, int* flag, double* dg, double* zf,
+                    unsigned long long* tr, hipStream_t st) {
+    const int rest = n - j0 - kPanel;
+    auto blocks = [&](int rw, int cw) {
+        return (long)((rest + kStepRows * rw - 1) / (kStepRows * rw)) * ((rest + 64 * cw - 1) / (64 * cw));
+    };
+    constexpr long kRound = 256;
+    const dim3 b(64 * kStepWaves);
+#define PSX_LU_STEP(RW, CW)                                                                                         \
+    hipLaunchKernelGGL((k_lu_step<RW, CW>), dim3((rest + 64 * CW - 1) / (64 * CW),                                  \
+                                                 (rest + kStepRows * RW - 1) / (kStepRows * RW)),                   \
+                       b, 0, st, A, n, j0, z, check, flag, dg, zf, tr)
+    if (blocks(1, 1) <= kRound) PSX_LU_STEP(1, 1);
+    else if (blocks(1, 2) <= kRound) PSX_LU_STEP(1, 2);
+    else if (blocks(2, 2) <= kRound) PSX_LU_STEP(2, 2);
+    else PSX_LU_STEP(2, 4);
+#undef PSX_LU_STEP
 }
 
 // The partial-pivot elimination (GSL 2.5 gsl_linalg_LU_decomp), blocked the
@@ -542,24 +589,47 @@ int enqueue_lu(double* A, int n, int* dswp, hipStream_t st, std::string* err) {
     return chk(hipGetLastError(), "LU launch", err);
 }
 
-// enqueue the tiled swap-free elimination (k_lu_diag, then one k_lu_tile per
-// panel); with check, *flag != 0 afterwards when some column needed a row swap
-// (A is then partly eliminated: recopy and pivot).  work: 2 * kDblk doubles
-// (the diagonal blocks, double-buffered).  Returns -1 with *err set when a
+// enqueue the tiled swap-free elimination (one k_lu_step per panel, then
+// k_lu_diag_at); with check, *flag != 0 afterwards when some column needed a
+// row swap (A is then partly eliminated: recopy and pivot).  Afterwards A's
+// diagonal holds U_ii and z holds z~.  work: 2 n doubles (U_ii / z kept aside).  Returns -1 with *err set when a
 // launch failed (the HIP error is read once, here).
 int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipStream_t st, std::string* err,
                      bool check = true) {
     if (chk(hipMemsetAsync(flag, 0, sizeof(int), st), "memset", err)) return -1;
-    double* const dblk[2] = {work, work + kDblk};
-    hipLaunchKernelGGL(k_lu_diag, dim3(1), dim3(64), 0, st, A, n, std::min(kPanel, n), z, dblk[0], check ? 1 : 0,
-                       flag);
-    int p = 0;
-    for (int j0 = 0; j0 + kPanel < n; j0 += kPanel, p++) {
-        const int rest = n - j0 - kPanel;  // trailing rows (and columns), >= 1
-        const unsigned g = (unsigned)((rest + kTile - 1) / kTile);
-        hipLaunchKernelGGL(k_lu_tile, dim3(g, g), dim3(kTile * kTileWaves), 0, st, A, n, j0,
-                           std::min(kPanel, rest), z, (const double*)dblk[p & 1], dblk[(p + 1) & 1], check ? 1 : 0,
-                           flag);
+    // PSX_LU_TRACE (diagnostics): per-panel phase clocks of two tiles, averaged on stderr
+    static const bool trace = std::getenv("PSX_LU_TRACE") != nullptr;
+    const int npan = std::max(0, (n - 1) / kPanel);
+    unsigned long long* tr = nullptr;
+    if (trace && npan > 0) {
+        if (chk(psx::dmalloc(&tr, sizeof(unsigned long long) * 16 * npan), "trace", err)) return -1;
+        (void)hipMemsetAsync(tr, 0, sizeof(unsigned long long) * 16 * npan, st);
+    }
+    int p = 0, j0 = 0;
+    for (; j0 + kPanel < n; j0 += kPanel, p++)
+        launch_lu_step(A, n, j0, z, check ? 1 : 0, flag, work, work + n, tr ? tr + 16 * p : nullptr, st);
+    // the last diagonal block (n - j0 <= kPanel rows), then U_ii / z of the others
+    hipLaunchKernelGGL(k_lu_diag_at, dim3(1), dim3(64), 0, st, A, n, j0, z, check ? 1 : 0, flag, (const double*)work,
+                       (const double*)(work + n));
+    if (tr) {
+        std::vector<unsigned long long> h(16 * (size_t)npan);
+        (void)hipMemcpyAsync(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost, st);
+        (void)hipStreamSynchronize(st);
+        double ph[2][4] = {{0}}, cnt[2] = {0, 0};
+        for (int q = 0; q < npan; q++)
+            for (int b = 0; b < 2; b++) {
+                const unsigned long long* t = h.data() + 16 * q + 8 * b;
+                if (!t[0] || !t[3]) continue;
+                cnt[b]++;
+                for (int i = 0; i < 3; i++) ph[b][i] += (double)(t[i + 1] - t[i]) * 0.01;  // 100 MHz -> us
+                if (b == 0 && t[4]) ph[b][3] += (double)(t[4] - t[3]) * 0.01;
+            }
+        fprintf(stderr, "psx-lu-trace n=%d panels=%d block(0,0): %.2f %.2f %.2f us; block(1,1): %.2f %.2f %.2f us "
+                        "(loads + D + L pass | U solve | update)\n",
+                n, npan, ph[0][0] / std::max(1.0, cnt[0]), ph[0][1] / std::max(1.0, cnt[0]),
+                ph[0][2] / std::max(1.0, cnt[0]), ph[1][0] / std::max(1.0, cnt[1]),
+                ph[1][1] / std::max(1.0, cnt[1]), ph[1][2] / std::max(1.0, cnt[1]));
+        psx::dfree(tr);
     }
     return chk(hipGetLastError(), "LU launch", err);
 }
@@ -628,7 +698,7 @@ int elim_device(const double* a, int n, const double* z, int check, double* piv,
     int* dflag = nullptr;
     int rc = 0;
     if (chk(psx::dmalloc(&dA, nn * sizeof(double)), "alloc", err) || chk(psx::dmalloc(&dz, n * sizeof(double)), "alloc", err) ||
-        chk(psx::dmalloc(&dw, 2 * kDblk * sizeof(double)), "alloc", err) ||
+        chk(psx::dmalloc(&dw, 2 * (size_t)n * sizeof(double)), "alloc", err) ||
         chk(psx::dmalloc(&dd, n * sizeof(double)), "alloc", err) || chk(psx::dmalloc(&dflag, sizeof(int)), "alloc", err))
         rc = -1;
     if (!rc) rc = chk(hipMemcpy(dA, a, nn * sizeof(double), hipMemcpyHostToDevice), "upload", err);
@@ -662,7 +732,7 @@ int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, dou
     };
     if (psx::dmalloc(&dL, nn * sizeof(double)) != hipSuccess || psx::dmalloc(&dA, nn * sizeof(double)) != hipSuccess ||
         psx::dmalloc(&dz, M * sizeof(double)) != hipSuccess || psx::dmalloc(&ddiag, M * sizeof(double)) != hipSuccess ||
-        psx::dmalloc(&dcol, std::max((size_t)kPanel * M + kPanel, (size_t)2 * kDblk) * sizeof(double)) != hipSuccess ||
+        psx::dmalloc(&dcol, ((size_t)kPanel * M + kPanel) * sizeof(double)) != hipSuccess ||
         psx::dmalloc(&dswp, (std::max(M, 1) + 2) * sizeof(int)) != hipSuccess) {
         cleanup();
         if (err) *err = "out of device memory (LD setup)";

@@ -767,8 +767,23 @@ static int ensure_skew(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hi
 // what only the fast k = 3 kernel reads (scaled y, transposed tiles, the
 // a-independent {b, c} weights and their sums), built on the first k = 3 pass
 // of a locus: a c <= 2 run never loads the k = 3 code object
+static int ensure_k3_build(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hipStream_t st);
+
+// d_g01 marks a complete build: a build that failed part way is released
+// (d_g01 back to null), so a retry starts from nothing (no orphaned buffers)
 static int ensure_k3(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hipStream_t st) {
     if (C.d_g01) return 0;
+    free_k3(C);
+    if (ensure_k3_build(C, a, ldg, U, st)) {
+        const std::string err = g_sweep_err;
+        free_k3(C);
+        g_sweep_err = err;
+        return -1;
+    }
+    return 0;
+}
+
+static int ensure_k3_build(SweepPlanCache& C, const SweepArgs& a, int ldg, int U, hipStream_t st) {
     const int nblk = ldg / 64;
     const int ntile = nblk * (nblk + 1) / 2;
     for (int s = 0; s < 2; s++) {

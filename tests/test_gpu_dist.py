@@ -95,3 +95,69 @@ def test_bench_gpus_more_than_visible_fails(gpu):
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and r.stdout == ""
     assert f"--gpus {n} but only" in r.stderr
+
+
+def test_bench_gpus2_rccl(gpu):
+    """`bench.py --gpus 2` over RCCL, one GPU per rank: runs on a box with two
+    or more GPUs (the driver's node), skipped on a one-GPU box.  The line
+    reports the 2-rank RCCL world, the merged count and one plan hash."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one device visible")
+    env = dict(os.environ)
+    env.pop("PSX_DIST_BACKEND", None)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--workload", "syn200c2", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["rccl_world"] == 2 and "RCCL" in out["config"]["parallelism"]
+    assert out["configs_checked"] == out["config"]["configs_per_step"] == 179_701
+    assert len(out["plan_hash"]) == 16
+
+
+def test_merge_refuses_mismatched_plans(gpu):
+    """psx_merge_partials checks every image's PlanTag on the device: images of
+    shards of different worlds, out of rank order, or of another locus are
+    refused with an error (never folded into a wrong total)."""
+    import torch
+    sys.path.insert(0, ROOT)
+    from pipsort_amd import engine as E
+    from pipsort_amd import synth
+    ld, z, _, _, u2l = synth.syn_v1(120)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=2, sharing_param=0.25)
+    ld2, z2, _, _, u2l2 = synth.syn_v1(125)  # same image size (ldg 128), another locus
+    other = E.seam_from_arrays(ld2, z2, u2l2, (10000, 8000), max_causal=2, sharing_param=0.25)
+    h = [E.PostCal(seam), E.PostCal(seam), E.PostCal(other)]
+    nb = h[0].partials_bytes()
+    buf = torch.empty(2 * max(nb, h[2].partials_bytes()), dtype=torch.uint8, device="cuda")
+
+    def merge(a, ra, wa, b, rb, wb):
+        a.set_shard(ra, wa)
+        b.set_shard(rb, wb)
+        a.run_exhaustive()
+        b.run_exhaustive()
+        a.export_partials(buf.data_ptr())
+        b.export_partials(buf.data_ptr() + nb)
+        torch.cuda.synchronize()
+        m = E.PostCal(seam)
+        try:
+            m.merge_partials(buf.data_ptr(), 2)
+            return m.accum().n_configs
+        finally:
+            m.close()
+
+    assert merge(h[0], 0, 2, h[1], 1, 2) == seam.count_configs()  # the good case
+    for args in ((h[0], 0, 2, h[1], 1, 3),    # another world
+                 (h[0], 1, 2, h[1], 0, 2)):   # out of rank order
+        with pytest.raises(E.EngineError, match="one plan"):
+            merge(*args)
+    if h[2].partials_bytes() == nb:  # another locus of the same image size: another hash
+        with pytest.raises(E.EngineError, match="one plan"):
+            merge(h[0], 0, 2, h[2], 1, 2)
+    for x in h:
+        x.close()

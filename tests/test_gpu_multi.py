@@ -143,21 +143,69 @@ def test_multi_exact_rerun_matches_single_sync(gpu):
     many.close()
 
 
+def _bitwise(a, b):
+    """Every accumulator bit for bit (the 0-sentinel entries included)."""
+    assert a.n_configs == b.n_configs
+    for f in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+        x, y = np.asarray(getattr(a, f)), np.asarray(getattr(b, f))
+        assert np.array_equal(x.view(np.uint64), y.view(np.uint64)), f
+    assert np.float64(a.total).view(np.uint64) == np.float64(b.total).view(np.uint64)
+
+
+def _device_lists(n_dev):
+    """Device lists the multi-device tests run: both orders of two devices, every
+    device in order and reversed, and a repeated-device mix."""
+    out = [[0, 1], [1, 0], list(range(min(n_dev, 8))), list(reversed(range(min(n_dev, 8)))), [1, 0, 1, 0]]
+    uniq = []
+    for d in out:
+        if d not in uniq:
+            uniq.append(d)
+    return uniq
+
+
 def test_multi_distinct_devices(gpu):
-    """Shards on two distinct devices (peer copies of the partial image into
-    device 0's gather buffer over xGMI): equal to one handle.  Runs where the
-    box has two or more GPUs (the driver's node), skipped on a one-GPU box."""
+    """Shards on distinct devices (peer copies of the partial images into
+    device 0's gather buffer over xGMI) give, for every device list, the SAME
+    BITS as the same number of shards on one device (same plan, same rank-order
+    fold: the result may not depend on which device ran a shard), and one
+    handle's results to rounding.  Runs where the box has two or more GPUs (the
+    driver's node); skipped on a one-GPU box, so this path is unverified until a
+    multi-GPU run records it passing."""
     if E.device_count() < 2:
         pytest.skip("one device visible")
     ld, z, _, _, u2l = synth.syn_v1(300)
     seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
     one = E.PostCal(seam)
     one.run_exhaustive()
-    for devs in ([0, 1], [1, 0], list(range(min(E.device_count(), 8)))):
+    ref = {}
+    for devs in _device_lists(E.device_count()):
+        n = len(devs)
+        if n not in ref:
+            same = E.MultiPostCal(seam, [0] * n)
+            same.run_exhaustive()
+            ref[n] = same.accum()
+            same.close()
         many = E.MultiPostCal(seam, devs)
         many.run_exhaustive()
         g = many.accum()
+        _bitwise(g, ref[n])
         _same(g, one.accum())
         assert many.timing()["configs"] == g.n_configs
         many.close()
     one.close()
+
+
+def test_multi_device_lists_fold_identically_on_one_gpu(gpu):
+    """The bitwise claim of test_multi_distinct_devices on a one-GPU box: two
+    multi-handles with the same shard count fold to the same bits (the fold is
+    deterministic, whatever ran first)."""
+    ld, z, _, _, u2l = synth.syn_v1(200)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    a = E.MultiPostCal(seam, [0, 0, 0])
+    a.run_exhaustive()
+    b = E.MultiPostCal(seam, [0, 0, 0])
+    b.run_exhaustive()
+    b.run_exhaustive()
+    _bitwise(a.accum(), b.accum())
+    a.close()
+    b.close()

@@ -383,6 +383,10 @@ def test_blocked_swap_free_elimination_bit_identical(gpu, M):
         piv = _elim_pivots(a)
         dmax = np.abs(np.diag(a)).max()
         assert info["min_pivot_ratio"][s] == piv.min() / dmax, (s, info["min_pivot_ratio"][s], piv.min() / dmax)
+        # the tiled kernels alone: no swap flagged (more tiles than resident blocks
+        # at M >= 1000) and every pivot bit for bit
+        gp, _, sw = E.elim_gpu(a)
+        assert not sw and np.array_equal(gp.view(np.uint64), piv.view(np.uint64)), (s, sw)
         if M <= 300:  # z's forward solve (it feeds K = -||S'||^2 / 2): bit-identical too
             assert _bits(info["spsq"][s]) == _bits(_elim_spsq(a, z[s])), (s, info["spsq"][s], _elim_spsq(a, z[s]))
     pc.close()
