@@ -289,6 +289,22 @@ def cpu_baseline_example(threads=None):
                       f"expected_study*_post.txt (6 digits)"}
 
 
+def sss_batch(M):
+    """The SSS neighbourhood of the 4-SNP configuration {M/4 - 1, M/4, 3M/4,
+    3M/4 + 1} (sss_postcal.cpp:20-99): 4 x (M - 4) swaps, 4 removals, M - 4
+    additions, -1 padded to 5; and its pattern count."""
+    cur = [M // 4 - 1, M // 4, 3 * M // 4, 3 * M // 4 + 1]
+    rest = [u for u in range(M) if u not in cur]
+    sets = []
+    for i in range(4):  # swaps (nbdzero)
+        keep = [c for j, c in enumerate(cur) if j != i]
+        sets += [sorted(keep + [u]) + [-1] for u in rest]
+    sets += [sorted([c for j, c in enumerate(cur) if j != i]) + [-1, -1] for i in range(4)]  # nbdminus
+    sets += [sorted(cur + [u]) for u in rest]  # nbdplus
+    arr = np.array(sets, dtype=np.int32)
+    return arr, int(sum(3 ** int((r >= 0).sum()) for r in arr))
+
+
 def sss_probe(reps=20):
     """BASELINE configs[4]: the SSS path (sss_postcal.cpp:102-380) on SYN-v1
     M = 2000, -c 5 — the walk itself, and the throughput of one SSS proposal
@@ -304,29 +320,55 @@ def sss_probe(reps=20):
     iters = pc.run_sss()
     walk_ms = (time.perf_counter() - t0) * 1e3
     walk_configs = pc.accum().n_configs
-    cur = [M // 4 - 1, M // 4, 3 * M // 4, 3 * M // 4 + 1]
-    rest = [u for u in range(M) if u not in cur]
-    sets = []
-    for i in range(4):  # swaps (nbdzero)
-        keep = [c for j, c in enumerate(cur) if j != i]
-        sets += [sorted(keep + [u]) + [-1] for u in rest]
-    sets += [sorted([c for j, c in enumerate(cur) if j != i]) + [-1, -1] for i in range(4)]  # nbdminus
-    sets += [sorted(cur + [u]) for u in rest]  # nbdplus
-    arr = np.array(sets, dtype=np.int32)
-    npat = int(sum(3 ** int((r >= 0).sum()) for r in arr))
+    arr, npat = sss_batch(M)
+    sets = arr
     pc.eval_union_batch(arr, accumulate=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    kms = []
     for _ in range(reps):
         pc.eval_union_batch(arr, accumulate=True)
+        kms.append(pc.timing()["kernel_ms"])  # the batch's k_eval_sets launch (HIP events)
     batch_ms = (time.perf_counter() - t0) * 1e3 / reps
     pc.close()
+    roof = sss_roofline(len(sets), npat, sum(kms) / len(kms))
     return {"workload": "SYN-v1 2-study locus, M=2000 SNPs, -c 5 -p 0.25 -n 10000,8000 (BASELINE configs[4])",
             "gpu_model_setup_and_create_ms": setup_ms, "walk_iterations": iters, "walk_configs": walk_configs,
             "walk_ms": walk_ms, "batch_sets": len(sets), "batch_configs": npat, "batch_ms": batch_ms,
-            "batch_configs_per_s": npat / (batch_ms / 1e3), "long_walks": sss_long_walks(),
+            "batch_configs_per_s": npat / (batch_ms / 1e3), "roofline": roof, "long_walks": sss_long_walks(),
             "multi_gpu": "sharded under --gpus N (psx_run_sss_sharded: every iteration's batch split over the "
                          "ranks, one all-gather of scores per iteration); this N = 1 line times one GPU"}
+
+
+def sss_roofline(n_sets, npat, kernel_ms):
+    """The batch's dominant kernel, k_eval_sets (a wave per union set: 2^k
+    subset LDL^T per study, then the 3^k assignments), is FP64 VALU work:
+    achieved = FP64 operations of one launch (PMC SQ_INSTS_VALU_FLOPS_FP64 x 64
+    of this very build and batch shape, profiles/pmc_latest.json "sss_eval") /
+    its launch duration measured here (HIP events around the launch)."""
+    out = {"bound": "valu_fp64", "kernel": "k_eval_sets", "kernel_ms": kernel_ms, "peak": FP64_PEAK_TFLOPS,
+           "unit": "TFLOP/s", "kernel_configs_per_s": npat / (kernel_ms / 1e3) if kernel_ms > 0 else None,
+           "duration_source": "HIP events around the launch on the engine stream (psx_get_timing), mean of reps",
+           "achieved": None, "frac": None, "eval_src_sha": eval_src_sha()}
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        ev = json.load(open(p)).get("sss_eval") or {}
+    except Exception:
+        ev = {}
+    if (ev.get("eval_src_sha") == out["eval_src_sha"] and ev.get("grid_size") == 64 * n_sets
+            and ev.get("fp64_flop_insts_per_launch") and kernel_ms > 0):
+        flops = ev["fp64_flop_insts_per_launch"] * 64.0
+        out.update(achieved=flops / (kernel_ms / 1e3) / 1e12, flops_per_launch=flops,
+                   flops_source="PMC SQ_INSTS_VALU_FLOPS_FP64 x 64 (profiles/pmc_latest.json sss_eval, same build)")
+        out["frac"] = out["achieved"] / FP64_PEAK_TFLOPS
+        c = ev.get("counters_per_dispatch", {})
+        if c.get("SQ_INSTS_VALU"):
+            out["fp64_valu_share"] = sum(c.get(k, 0.0) for k in (
+                "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
+                "SQ_INSTS_VALU_TRANS_F64")) / c["SQ_INSTS_VALU"]
+    else:
+        out["flops_source"] = "no PMC counters of this build / batch shape (profiles/pmc_latest.json sss_eval)"
+    return out
 
 
 def sss_long_walks(reps=3):
@@ -539,6 +581,19 @@ def kernel_src_sha():
     import hashlib
     h = hashlib.sha256()
     for f in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, "pipsort_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+EVAL_SOURCES = ("psx_engine.hip", "psx_wave.h", "psx_math.h", "psx_sweep_dev.h")
+
+
+def eval_src_sha():
+    """Hash of the sources k_eval_sets (the SSS batch evaluator) is built from."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in EVAL_SOURCES:
         with open(os.path.join(ROOT, "pipsort_amd", "csrc", f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]

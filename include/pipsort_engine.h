@@ -74,7 +74,10 @@ typedef struct {
     uint64_t union_sets;    /* union subsets evaluated by the dominant kernel              */
     double alg_bytes;       /* algorithmic bytes of the dominant kernel      */
     double flops;           /* FP64 operation estimate of the dominant kernel              */
-    int32_t exact_rerun;    /* 1 if the sweep was redone with the exact notSharedLL variant */
+    int32_t exact_rerun;    /* nonzero if the sweep was redone with the exact notSharedLL
+                               variant; the checks that fired: bit 0 a set's / an a or c
+                               slot's notSharedLL group (k = 3) or the k = 2 window, bit 1
+                               an off-diagonal unit's b-slot notSharedLL total (k = 3) */
     int32_t robust_units;   /* k = 3 units redone by the robust variant (cumulative since create) */
     double span_ms;         /* asynchronous passes: first sweep's start to the last one's end,
                                per pass (consecutive sweeps may overlap: kernel_ms double-counts) */
@@ -219,7 +222,9 @@ int psx_run_sss_sharded(psx_engine *e, psx_allgather_fn allgather, void *ctx, in
 /* PostCal::expand_and_compute_lkl (sss_postcal.cpp:447-685), batched: evaluate
  * n_sets union sets (ascending union indices, -1 padded to `stride`), return the
  * SSS score (pattern L with largest |L|, sss_postcal.cpp:624-626) per set and,
- * if accumulate != 0, add every pattern into the accumulators. */
+ * if accumulate != 0, add every pattern into the accumulators.  Padding may sit
+ * anywhere in a row; an all -1 row is the null configuration.  psx_get_timing
+ * then reports the batch's evaluation kernel (kernel_ms, union_sets). */
 int psx_eval_union_batch(psx_engine *e, const int32_t *sets, int32_t stride, int32_t n_sets,
                          int accumulate, double *score_out);
 

@@ -28,6 +28,9 @@
 #include "psx_sweep.h"
 #include "psx_sweep_dev.h"
 #include "psx_mem.h"
+#include "psx_wave.h"
+
+extern "C" __device__ __attribute__((const)) double __ockl_wfred_min_f64(double);
 
 using psx::Acc5;
 using psx::kPlanMagic;
@@ -144,41 +147,121 @@ __global__ void k_to_union(const double* __restrict__ S, int M, const int* __res
 // One union set S (stride entries, -1 padded) by the calling wave: its set
 // record (*so), its member records (mo[0 .. k), if mo) and its SSS score (*sc,
 // if sc); fpair = (C0 mask, C1 mask) restricts the set to one pattern.
-__device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride, const int* __restrict__ fpair,
-                         SetRec* __restrict__ so, Acc5* __restrict__ mo, double* __restrict__ sc) {
-    constexpr int KM = PSX_KMAX;
-    __shared__ double s_g[2][KM][KM];
-    __shared__ double s_ad[2][KM], s_y[2][KM];
-    __shared__ double s_mu[2][64];
-    __shared__ double s_f[2][64];
-    __shared__ int s_n[2][64];
-    __shared__ int s_mem[KM];
-    const int lane = threadIdx.x;
-    const int v = lane < stride && lane < KM ? S[lane] : -1;
-    const unsigned long long bal = __ballot(v >= 0);
-    const int k = __popcll(bal);
-    if (v >= 0) s_mem[__popcll(bal & ((1ull << lane) - 1ull))] = v;
-    __syncthreads();
-    for (int e = lane; e < 2 * KM * KM; e += 64) {
-        const int s = e / (KM * KM), i = (e / KM) % KM, j = e % KM;
-        if (i < k && j < i) s_g[s][i][j] = P.G[s][(size_t)s_mem[i] * P.ldg + s_mem[j]];
-    }
-    if (lane < 2 * KM) {
-        const int s = lane / KM, i = lane % KM;
-        if (i < k) {
-            s_ad[s][i] = P.Ad[s][s_mem[i]];
-            s_y[s][i] = P.y[s][s_mem[i]];
+// the 3^KMAX assignments as (c0, c1) member masks: assignment p gives member j
+// digit j of p (base 3): study 0 only / study 1 only / both (postcal.cpp:928-943's
+// mask order restated); a set of k < KMAX members takes the first 3^k entries,
+// masked to its k members
+struct PatTab {
+    unsigned short v[729];
+};
+constexpr PatTab make_pat() {
+    PatTab t{};
+    for (int p = 0; p < 729; p++) {
+        int r = p, c0 = 0, c1 = 0;
+        for (int j = 0; j < 6; j++) {
+            const int x = r % 3 + 1;
+            r /= 3;
+            if (x & 1) c0 |= 1 << j;
+            if (x & 2) c1 |= 1 << j;
         }
+        t.v[p] = (unsigned short)(c0 | (c1 << 8));
     }
-    int pmask[2] = {0, 0};
+    return t;
+}
+static_assert(PSX_KMAX == 6, "the assignment table covers 3^6");
+__constant__ PatTab kPat = make_pat();
+
+// A set's operands (its members' Sigma~ sub-blocks, A_d, y and presence), staged
+// in two halves so that a caller can put other loads between them
+// (k_sss_eval's map probe): eval_gather issues the global loads into
+// registers, eval_stage waits for them and writes LDS.
+struct EvalShm {
+    double g[2][PSX_KMAX][PSX_KMAX];
+    double ad[2][PSX_KMAX], y[2][PSX_KMAX];
+    double mu[2][64], f[2][64];
+    int n[2][64];
+    int mem[PSX_KMAX];
+};
+struct EvalOps {
+    double g[2];     // this lane's (<= 2) lower-triangle Sigma~ entries: e = lane, lane + 64
+    double ad, y;    // lanes < 2 KMAX: (study lane / KMAX, member lane % KMAX)
+    unsigned pr;     // lanes < KMAX: presence bits of member lane
+    int k;
+};
+__device__ __forceinline__ EvalOps eval_gather(const DevProb& P, const int* __restrict__ S, int stride,
+                                               EvalShm& sh) {
+    constexpr int KM = PSX_KMAX;
+    const int lane = threadIdx.x;
+    EvalOps o;
+    int mem[KM];  // the members (S's non-negative entries, in order)
+    int k = 0;
 #pragma unroll
     for (int j = 0; j < KM; j++) {
-        if (j < k) {
-            const unsigned char pr = P.pres[s_mem[j]];
-            if (pr & 1) pmask[0] |= 1 << j;
-            if (pr & 2) pmask[1] |= 1 << j;
-        }
+        mem[j] = -1;
+        const int v = j < stride ? S[j] : -1;
+#pragma unroll
+        for (int c = 0; c <= j; c++)
+            if (v >= 0 && c == k) mem[c] = v;
+        k += v >= 0;
     }
+    o.k = k;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int e = lane + 64 * h;
+        const int s = e / (KM * KM), i = (e / KM) % KM, j = e % KM;
+        int mi = -1, mj = -1;
+#pragma unroll
+        for (int c = 0; c < KM; c++) {
+            mi = c == i ? mem[c] : mi;
+            mj = c == j ? mem[c] : mj;
+        }
+        o.g[h] = (e < 2 * KM * KM && i < k && j < i) ? P.G[s][(size_t)mi * P.ldg + mj] : 0.0;
+    }
+    {
+        const int s = lane / KM, i = lane % KM;
+        int mi = -1;
+#pragma unroll
+        for (int c = 0; c < KM; c++) mi = c == i ? mem[c] : mi;
+        const bool ok = lane < 2 * KM && i < k;
+        o.ad = ok ? P.Ad[s][mi] : 0.0;
+        o.y = ok ? P.y[s][mi] : 0.0;
+        o.pr = (lane < KM && lane < k) ? P.pres[mi] : 0u;
+        if (lane < KM) sh.mem[lane] = mi;
+    }
+    return o;
+}
+__device__ __forceinline__ void eval_stage(const EvalOps& o, EvalShm& sh) {
+    constexpr int KM = PSX_KMAX;
+    const int lane = threadIdx.x;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int e = lane + 64 * h;
+        const int s = e / (KM * KM), i = (e / KM) % KM, j = e % KM;
+        if (e < 2 * KM * KM && i < o.k && j < i) sh.g[s][i][j] = o.g[h];
+    }
+    if (lane < 2 * KM && lane % KM < o.k) {
+        sh.ad[lane / KM][lane % KM] = o.ad;
+        sh.y[lane / KM][lane % KM] = o.y;
+    }
+}
+
+// the set's 2^k subset weights per study and its 3^k assignments (after
+// eval_gather / eval_stage): set record, member records, score
+__device__ void eval_compute(const DevProb& P, const EvalOps& o, EvalShm& shm, const int* __restrict__ fpair,
+                             SetRec* __restrict__ so, Acc5* __restrict__ mo, double* __restrict__ sc,
+                             unsigned long long* tr = nullptr) {
+    constexpr int KM = PSX_KMAX;
+    double (&s_g)[2][KM][KM] = shm.g;
+    double (&s_ad)[2][KM] = shm.ad;
+    double (&s_y)[2][KM] = shm.y;
+    double (&s_mu)[2][64] = shm.mu;
+    double (&s_f)[2][64] = shm.f;
+    int (&s_n)[2][64] = shm.n;
+    const int lane = threadIdx.x;
+    const int k = o.k;
+    int pmask[2];
+    pmask[0] = (int)(__ballot(o.pr & 1u) & 0x3f);
+    pmask[1] = (int)(__ballot(o.pr & 2u) & 0x3f);
     __syncthreads();
     const int nsub = 1 << k;
     // one (study, subset) per lane: 2^k subsets of both studies (one pass for
@@ -229,6 +312,7 @@ __device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride
         }
     }
     __syncthreads();
+    if (tr) tr[3] = wall_clock64();
     const int S0 = pmask[0], S1 = pmask[1];
     const int Gll = s_n[0][S0] + s_n[1][S1] + 2;
     int GN[KM];
@@ -260,19 +344,13 @@ __device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride
     double p0[KM], p1[KM], sh[KM], sl[KM], ns[KM];
 #pragma unroll
     for (int j = 0; j < KM; j++) p0[j] = p1[j] = sh[j] = sl[j] = ns[j] = 0.0;
+    const int full = (1 << k) - 1;
     for (int p = lane; p < npat; p += 64) {
-        int c0 = 0, c1 = 0, x[KM];
-        int r = p;
+        const unsigned pt = kPat.v[p];
+        const int c0 = (int)(pt & 0xffu) & full, c1 = (int)(pt >> 8) & full;
+        int x[KM];
 #pragma unroll
-        for (int j = 0; j < KM; j++) {
-            x[j] = 0;
-            if (j < k) {
-                x[j] = r % 3 + 1;
-                r /= 3;
-                if (x[j] & 1) c0 |= 1 << j;
-                if (x[j] & 2) c1 |= 1 << j;
-            }
-        }
+        for (int j = 0; j < KM; j++) x[j] = ((c0 >> j) & 1) | (((c1 >> j) & 1) << 1);
         if ((c0 & ~S0) || (c1 & ~S1)) continue;  // (study, SNP) pair not present: no mask bit
         if (fc0 >= 0 && (c0 != fc0 || c1 != fc1)) continue;
         const int nsh = __popc(c0 & c1);
@@ -302,20 +380,30 @@ __device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride
             }
         }
     }
-    tot = wave_sum(tot);
-    nc0 = wave_sum(nc0);
-    nc1 = wave_sum(nc1);
-    npatv = wave_sum(npatv);
-    smin = wave_min(smin);
-    double vp0 = 0, vp1 = 0, vsh = 0, vsl = 0, vns = 0;
+    if (tr) tr[4] = wall_clock64();
+    // every sum in one transposed batch (~7 instructions per value instead of
+    // six dependent LDS shuffles each); the score's minimum by DPP
+    static_assert(4 + 5 * KM <= 36, "reduction batch");
+    double red[36];
+    red[0] = tot; red[1] = nc0; red[2] = nc1; red[3] = npatv;
 #pragma unroll
     for (int j = 0; j < KM; j++) {
-        if (j < k) {
-            const double a0 = wave_sum(p0[j]), a1 = wave_sum(p1[j]), a2 = wave_sum(sh[j]), a3 = wave_sum(sl[j]),
-                         a4 = wave_sum(ns[j]);
-            if (j == lane) { vp0 = a0; vp1 = a1; vsh = a2; vsl = a3; vns = a4; }
-        }
+        red[4 + 5 * j] = p0[j]; red[5 + 5 * j] = p1[j]; red[6 + 5 * j] = sh[j];
+        red[7 + 5 * j] = sl[j]; red[8 + 5 * j] = ns[j];
     }
+#pragma unroll
+    for (int i = 4 + 5 * KM; i < 36; i++) red[i] = 0.0;
+    psx::wave_sum_t(red);
+    tot = red[0]; nc0 = red[1]; nc1 = red[2]; npatv = red[3];
+    smin = __ockl_wfred_min_f64(smin);
+    if (tr) tr[5] = wall_clock64();
+    double vp0 = 0, vp1 = 0, vsh = 0, vsl = 0, vns = 0;
+#pragma unroll
+    for (int j = 0; j < KM; j++)
+        if (j == lane) {
+            vp0 = red[4 + 5 * j]; vp1 = red[5 + 5 * j]; vsh = red[6 + 5 * j];
+            vsl = red[7 + 5 * j]; vns = red[8 + 5 * j];
+        }
     if (lane == 0) {
         SetRec rr = psx::set_zero();
         rr.m = GS;
@@ -345,8 +433,18 @@ __device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride
         a.nsll = vns;
         mo[lane] = a;
     }
+    if (tr) tr[6] = wall_clock64();
 }
 
+
+// one set (sorted members, -1 padded, in global or LDS memory): gather, stage, compute
+__device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride, const int* __restrict__ fpair,
+                         SetRec* __restrict__ so, Acc5* __restrict__ mo, double* __restrict__ sc) {
+    __shared__ EvalShm shm;
+    const EvalOps o = eval_gather(P, S, stride, shm);
+    eval_stage(o, shm);
+    eval_compute(P, o, shm, fpair, so, mo, sc);
+}
 
 // span (optional, device [lo, hi)): block b evaluates set lo + b of `sets`, the
 // blocks past hi - lo exit (a batch whose size the device decided); outputs
@@ -363,85 +461,6 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
     }
     eval_set(P, sets + (size_t)(base + set) * stride, stride, forced ? forced + 2 * set : nullptr, srec + set,
              mrec ? mrec + (size_t)set * stride : nullptr, score ? score + set : nullptr);
-}
-
-// Configs rows (psx_run_configs, postcal.cpp:400-714): every row is one union
-// set with ONE forced assignment (c0, c1), so a lane per row factors just the
-// two forced subsets (psx::ldlt_terms: the same eliminations k_eval_sets runs
-// with the other members zeroed out) instead of a wave per row factoring all
-// 2^k subsets.  Same records as k_eval_sets with the forced filter: the values
-// are equal, the shifts are taken at the assignment's own exponent np (where
-// k_eval_sets uses the full-set exponents) — the same (shift, sum) numbers.
-__global__ __launch_bounds__(64) void k_eval_rows(DevProb P, const int* __restrict__ sets, int stride,
-                                                  const int* __restrict__ forced, long nsets,
-                                                  SetRec* __restrict__ srec, Acc5* __restrict__ mrec) {
-    constexpr int KM = PSX_KMAX;
-    const long set = (long)blockIdx.x * 64 + threadIdx.x;
-    if (set >= nsets) return;
-    const int* S = sets + (size_t)set * stride;
-    int mem[KM];
-    int k = 0;
-    for (int j = 0; j < stride && j < KM; j++)
-        if (S[j] >= 0) mem[k++] = S[j];
-    int S0 = 0, S1 = 0;
-    for (int j = 0; j < k; j++) {
-        const unsigned pr = P.pres[mem[j]];
-        if (pr & 1u) S0 |= 1 << j;
-        if (pr & 2u) S1 |= 1 << j;
-    }
-    const int c0 = forced[2 * set], c1 = forced[2 * set + 1];
-    const int Ck = P.Ck[k];
-    SetRec rr = psx::set_zero();
-    Acc5 a = psx::acc_zero();
-    double wll = 0.0, w = 0.0;
-    int G = 0;
-    // the forced assignment is one of k_eval_sets' 3^k (every member in a study
-    // where it is present) or the row adds nothing
-    const bool valid = k > 0 && ((c0 | c1) == (1 << k) - 1) && !(c0 & ~S0) && !(c1 & ~S1);
-    if (valid) {
-        double mu[2], f[2];
-        int n[2];
-        for (int s = 0; s < 2; s++) {
-            const int cs = s ? c1 : c0;
-            int idx[KM];
-            int t = 0;
-            for (int j = 0; j < k; j++)
-                if ((cs >> j) & 1) idx[t++] = mem[j];
-            double q, Pd;
-            psx::ldlt_terms(P.G[s], P.ldg, P.Ad[s], P.y[s], P.dval[s], idx, t, q, Pd);
-            psx::split_exp(0.5 * q * PSX_LOG2E, 1.0 / sqrt(Pd), n[s], mu[s]);
-            f[s] = 0.5 * q - 0.5 * log(Pd);
-        }
-        const int nsh = __popc(c0 & c1);
-        const double mup = mu[0] * mu[1];
-        const int np = n[0] + n[1];
-        G = np + 2;  // k_eval_sets' "+ 2" headroom, at this assignment's exponent
-        wll = ldexp(mup, -2);
-        w = wll * P.pit[k][nsh];
-        rr.m = G + Ck;
-        rr.tot = w;
-        rr.m0 = rr.m1 = np + Ck;
-        rr.nc0 = c0 == 0 ? mup * P.pit[k][0] : 0.0;
-        rr.nc1 = c1 == 0 ? mup * P.pit[k][0] : 0.0;
-        rr.score = f[0] + f[1] + P.prior[k][nsh];
-        rr.npat = 1.0;
-        a.mP = G + Ck;
-        a.mS = G;
-        a.mN = G;
-    }
-    srec[set] = rr;
-    for (int j = 0; j < k; j++) {
-        Acc5 r = a;
-        if (valid) {
-            const int x = ((c0 >> j) & 1) | (((c1 >> j) & 1) << 1);
-            r.post0 = (x & 1) ? w : 0.0;
-            r.post1 = (x & 2) ? w : 0.0;
-            r.shared = x == 3 ? w : 0.0;
-            r.sll = x == 3 ? wll : 0.0;
-            r.nsll = x == 3 ? 0.0 : wll;  // notSharedLL: 2^{np - (np + 2)} mup
-        }
-        mrec[(size_t)set * stride + j] = r;
-    }
 }
 
 // merge `count` concatenated partial images (rank order) into acc / sacc.
@@ -690,9 +709,15 @@ struct psx_engine {
     // sweep workspace (tiled kernel)
     psx::SweepPlanCache plans;
     // generic workspace
-    // sets | forced | CSR of one batch, uploaded with one copy from pinned staging
+    // the sets of one batch, uploaded with one copy from pinned staging; their
+    // member records' CSR (dptr[U + 1] | gidx), built on the device
     int* dgen = nullptr;
     size_t cap_gen = 0;
+    int* dgcsr = nullptr;
+    size_t cap_gcsr = 0;
+    psx::PlanScratch gscratch;
+    unsigned char* dbm = nullptr;  // chunked batch merge scratch (psx::launch_merge_batch)
+    size_t cap_bm = 0;
     int* hstage = nullptr;
     size_t cap_stage = 0;
     hipEvent_t stage_ev = nullptr;  // last upload out of hstage (reuse waits on it)
@@ -769,7 +794,7 @@ psx_engine::~psx_engine() {
     if (stage_ev) { hipEventSynchronize(stage_ev); hipEventDestroy(stage_ev); }
     if (hstage) psx::hfree(hstage);
     if (hscore) psx::hfree(hscore);
-    psx::dfree(dgen); psx::dfree(dscore); psx::dfree(dsrec); psx::dfree(dmrec); psx::dfree(dpass);
+    psx::dfree(dgen); psx::dfree(dgcsr); psx::dfree(dbm); psx::dfree(gscratch.p); psx::dfree(dscore); psx::dfree(dsrec); psx::dfree(dmrec); psx::dfree(dpass);
     psx::sweep_free(plans);
     psx::configs_free(cfg);
     psx::dfree(d_cfg_maps);
@@ -860,52 +885,55 @@ void build_csr(const std::vector<int>& sets, int stride, size_t nsets, int U, st
     }
 }
 
-// Evaluate a batch of union sets with the generic kernel; optionally fold all
-// patterns into the accumulators and/or return SSS scores.
-// k_eval_sets over n sets staged in e->hstage as [sets (n * stride) | forced
-// (n * 2, optional) | CSR ptr | idx | rows (accumulate)]: one upload, the
-// kernel, the deterministic record merges.
-// Wait for an eval_generic_staged(..., finish = false) batch: scores out, kernel time.
-int finish_generic(psx_engine* e, size_t nsets, double* scores, double* kernel_ms) {
-    HIPCHK(hipStreamSynchronize(e->stream));
-    if (scores)
-        for (size_t i = 0; i < nsets; i++) scores[i] = e->K + e->hscore[i];
-    if (kernel_ms) {
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
-        *kernel_ms += ms;
-    }
+// The pinned staging buffer, n ints, once its previous upload is done.
+int stage_acquire(psx_engine* e, size_t n, int** out) {
+    if (e->stage_rec) HIPCHK(hipEventSynchronize(e->stage_ev));
+    int rc = ensure_host(e->hstage, e->cap_stage, n);
+    if (rc) return rc;
+    *out = e->hstage;
     return 0;
 }
 
-int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool has_forced, size_t n_ptr, size_t n_idx,
-                        size_t n_rows, bool accumulate, double* scores, double* kernel_ms, bool finish = true) {
+// Evaluate nsets union sets staged in e->hstage ([set][stride], members first,
+// -1 after them) with the generic kernel: one upload, k_eval_sets, then
+// (accumulate) the deterministic merges of its member and set records; scores
+// (SSS) copied back.  Batches of up to kBatchChunks chunks (an SSS
+// neighbourhood) merge in two launches (psx::launch_merge_batch); larger ones
+// (generic exhaustive levels) through the records' CSR, built by a device radix
+// sort (psx::csr_from_keys_device).
+constexpr int kBatchChunks = 64;
+
+int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool accumulate, double* scores, double* kernel_ms) {
+    if (nsets == 0) return 0;
+    if (stride > PSX_KMAX) return fail(PSX_ERANGE, "union set larger than PSX_KMAX");
     int rc;
-    const size_t n_sets = nsets * stride, n_forced = has_forced ? nsets * 2 : 0;
-    const size_t total = n_sets + n_forced + n_ptr + n_idx + n_rows;
-    if ((rc = ensure(e->dgen, e->cap_gen, total))) return rc;
+    const size_t n_sets = nsets * stride;
+    const bool chunked = accumulate && psx::batch_merge_chunks((long)nsets, stride) <= kBatchChunks && e->U <= 131072;
+    if ((rc = ensure(e->dgen, e->cap_gen, n_sets))) return rc;
     if ((rc = ensure(e->dsrec, e->cap_srec, nsets))) return rc;
-    if ((rc = ensure(e->dmrec, e->cap_mrec, nsets * stride))) return rc;
+    if ((rc = ensure(e->dmrec, e->cap_mrec, n_sets))) return rc;
     if (scores && (rc = ensure(e->dscore, e->cap_score, nsets))) return rc;
-    HIPCHK(hipMemcpyAsync(e->dgen, e->hstage, total * sizeof(int), hipMemcpyHostToDevice, e->stream));
+    if (chunked && (rc = ensure(e->dbm, e->cap_bm, psx::batch_merge_bytes((long)nsets, stride, e->U)))) return rc;
+    if (accumulate && !chunked && (rc = ensure(e->dgcsr, e->cap_gcsr, (size_t)e->U + 1 + n_sets))) return rc;
+    HIPCHK(hipMemcpyAsync(e->dgen, e->hstage, n_sets * sizeof(int), hipMemcpyHostToDevice, e->stream));
     if (!e->stage_ev) HIPCHK(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
     HIPCHK(hipEventRecord(e->stage_ev, e->stream));
     e->stage_rec = true;
-    const int* dsets = e->dgen;
-    const int* dforced = has_forced ? e->dgen + n_sets : nullptr;
-    const int* dcsr = e->dgen + n_sets + n_forced;
     if (kernel_ms) HIPCHK(hipEventRecord(e->ev[2], e->stream));
-    if (has_forced && !scores)  // configs rows: one forced assignment per set, a lane per set
-        hipLaunchKernelGGL(k_eval_rows, dim3((unsigned)((nsets + 63) / 64)), dim3(64), 0, e->stream, e->dp, dsets,
-                           stride, dforced, (long)nsets, e->dsrec, e->dmrec);
-    else
-        hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)nsets), dim3(64), 0, e->stream, e->dp, dsets, stride, dforced,
-                           e->dsrec, e->dmrec, scores ? e->dscore : nullptr);
+    hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)nsets), dim3(64), 0, e->stream, e->dp, e->dgen, stride, nullptr,
+                       e->dsrec, e->dmrec, scores ? e->dscore : nullptr);
     HIPCHK(hipGetLastError());
     if (kernel_ms) HIPCHK(hipEventRecord(e->ev[3], e->stream));
-    if (accumulate) {
-        if (psx::launch_merge_members(e->dmrec, dcsr, dcsr + n_ptr, dcsr + n_ptr + n_idx, (int)n_rows, e->dacc,
-                                      e->stream))
+    if (chunked) {
+        if (psx::launch_merge_batch(e->dgen, stride, (long)nsets, e->U, e->dmrec, e->dsrec, e->dbm, e->dacc,
+                                    e->dsacc, e->stream))
+            return fail(PSX_EHIP, "set-batch merge failed");
+    } else if (accumulate) {
+        int* dptr = e->dgcsr;
+        int* gidx = e->dgcsr + e->U + 1;
+        if (psx::csr_from_keys_device(e->dgen, (long)n_sets, e->U, dptr, gidx, e->gscratch, e->stream))
+            return fail(PSX_EHIP, "device CSR of a set batch failed");
+        if (psx::launch_merge_dptr(e->dmrec, dptr, gidx, e->U, e->dacc, e->stream))
             return fail(PSX_EHIP, psx::sweep_error());
         SetRec none = psx::set_zero();
         if (psx::launch_merge_sets(e->dsrec, (long)nsets, none, e->dsacc, e->stream))
@@ -915,33 +943,16 @@ int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool has_forced
         if ((rc = ensure_host(e->hscore, e->cap_hscore, nsets))) return rc;
         HIPCHK(hipMemcpyAsync(e->hscore, e->dscore, nsets * sizeof(double), hipMemcpyDeviceToHost, e->stream));
     }
-    if (!finish || (!scores && !kernel_ms)) return 0;
-    return finish_generic(e, nsets, scores, kernel_ms);
-}
-
-int eval_generic(psx_engine* e, const std::vector<int>& sets, int stride, size_t nsets, const int* forced,
-                 bool accumulate, double* scores, double* kernel_ms) {
-    if (nsets == 0) return 0;
-    if (stride > PSX_KMAX) return fail(PSX_ERANGE, "union set larger than PSX_KMAX");
-    int rc;
-    std::vector<int> ptr, idx, rows;
-    if (accumulate) build_csr(sets, stride, nsets, e->U, ptr, idx, rows);
-    const size_t n_sets = nsets * stride, n_forced = forced ? nsets * 2 : 0;
-    const size_t total = n_sets + n_forced + ptr.size() + idx.size() + rows.size();
-    // the staging buffer is reused once its previous upload is done
-    if (e->stage_rec) HIPCHK(hipEventSynchronize(e->stage_ev));
-    if ((rc = ensure_host(e->hstage, e->cap_stage, total))) return rc;
-    int* h = e->hstage;
-    std::memcpy(h, sets.data(), n_sets * sizeof(int));
-    if (forced) std::memcpy(h + n_sets, forced, n_forced * sizeof(int));
-    int* hc = h + n_sets + n_forced;
-    if (accumulate) {
-        std::memcpy(hc, ptr.data(), ptr.size() * sizeof(int));
-        std::memcpy(hc + ptr.size(), idx.data(), idx.size() * sizeof(int));
-        std::memcpy(hc + ptr.size() + idx.size(), rows.data(), rows.size() * sizeof(int));
+    if (!scores && !kernel_ms) return 0;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (scores)
+        for (size_t i = 0; i < nsets; i++) scores[i] = e->K + e->hscore[i];
+    if (kernel_ms) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+        *kernel_ms += ms;
     }
-    return eval_generic_staged(e, stride, nsets, forced != nullptr, ptr.size(), idx.size(), rows.size(), accumulate,
-                               scores, kernel_ms);
+    return 0;
 }
 
 // `count` null configurations (postcal.cpp:793-822) as a set record
@@ -1009,16 +1020,16 @@ int run_level_generic(psx_engine* e, int k, double* kms) {
     std::vector<int> c(k);
     unrank_lex(lo, e->U, k, c.data());
     uint64_t r = lo;
-    std::vector<int> sets;
     while (r < hi) {
         uint64_t n = std::min<uint64_t>(CH, hi - r);
-        sets.resize(n * k);
+        int* h = nullptr;
+        int rc = stage_acquire(e, n * k, &h);
+        if (rc) return rc;
         for (uint64_t i = 0; i < n; i++) {
-            std::copy(c.begin(), c.end(), sets.begin() + i * k);
+            std::copy(c.begin(), c.end(), h + i * k);
             next_lex(c.data(), e->U, k);
         }
-        int rc = eval_generic(e, sets, k, n, nullptr, true, nullptr, kms);
-        if (rc) return rc;
+        if ((rc = eval_generic_staged(e, k, n, true, nullptr, kms))) return rc;
         r += n;
     }
     return 0;
@@ -1965,36 +1976,60 @@ extern "C" {
 int psx_eval_union_batch(psx_engine* e, const int32_t* sets, int32_t stride, int32_t n_sets, int accumulate,
                          double* score_out) {
     HIPCHK(hipSetDevice(e->dev));
+    const auto t0 = std::chrono::steady_clock::now();
     if (stride < 1 || stride > PSX_KMAX) return fail(PSX_ERANGE, "stride outside [1, 6]");
-    // the empty set is the null configuration (sss_postcal.cpp:463-499): host side
-    std::vector<int> v;
-    std::vector<size_t> where;
-    v.reserve((size_t)n_sets * stride);
+    // the empty set is the null configuration (sss_postcal.cpp:463-499): host
+    // side.  The other sets are validated and written compacted (members first,
+    // -1 after them: record j of a set is its j-th member) straight into the
+    // pinned staging buffer, in one pass.
+    int rc;
+    int* h = nullptr;
+    if (n_sets > 0 && (rc = stage_acquire(e, (size_t)n_sets * stride, &h))) return rc;
+    std::vector<int> where;  // batch position -> row (only when some row is empty)
+    size_t nb = 0;
     double nulls = 0;
     for (int i = 0; i < n_sets; i++) {
         const int* s = sets + (size_t)i * stride;
+        int* o = h + nb * stride;
         int prev = -1, k = 0;
         for (int j = 0; j < stride; j++) {
-            if (s[j] < 0) continue;
-            if (s[j] <= prev || s[j] >= e->U) return fail(PSX_EINVAL, "sets must be ascending union indices");
-            prev = s[j];
-            k++;
+            const int v = s[j];
+            if (v < 0) continue;
+            if (v <= prev || v >= e->U) return fail(PSX_EINVAL, "sets must be ascending union indices");
+            prev = o[k++] = v;
         }
         if (k == 0) {
+            if (where.empty())
+                for (size_t q = 0; q < nb; q++) where.push_back((int)q);
             nulls += 1;
             if (score_out) score_out[i] = e->K + e->L0;
             continue;
         }
-        where.push_back(i);
-        v.insert(v.end(), s, s + stride);
+        for (int j = k; j < stride; j++) o[j] = -1;
+        if (nulls > 0) where.push_back(i);
+        nb++;
     }
-    std::vector<double> sc(where.size());
-    int rc = eval_generic(e, v, stride, where.size(), nullptr, accumulate != 0, score_out ? sc.data() : nullptr, nullptr);
-    if (rc) return rc;
-    if (score_out)
-        for (size_t i = 0; i < where.size(); i++) score_out[where[i]] = sc[i];
+    const auto t1 = std::chrono::steady_clock::now();
+    if (nb > 0) {
+        // scores straight into score_out when no row was empty
+        std::vector<double> sc(score_out && nulls > 0 ? nb : 0);
+        double* so = score_out ? (nulls > 0 ? sc.data() : score_out) : nullptr;
+        double kms = 0;
+        if ((rc = eval_generic_staged(e, stride, nb, accumulate != 0, so, &kms))) return rc;
+        if (score_out && nulls > 0)
+            for (size_t i = 0; i < nb; i++) score_out[where[i]] = sc[i];
+        // the batch's k_eval_sets launch (HIP events around it on e->stream)
+        std::memset(&e->timing, 0, sizeof(e->timing));
+        e->timing.kernel_ms = kms;
+        e->timing.kernel_launches = 1;
+        e->timing.union_sets = nb;
+    }
     if (accumulate && nulls > 0 && (rc = fold_null(e, nulls))) return rc;
     HIPCHK(hipStreamSynchronize(e->stream));
+    // host walls: validation + staging, the whole call
+    using ms = std::chrono::duration<double, std::milli>;
+    e->timing.prepare_ms = ms(t1 - t0).count();
+    e->timing.run_ms = ms(std::chrono::steady_clock::now() - t0).count();
     return 0;
 }
 
@@ -2151,6 +2186,7 @@ struct SssIter {
     int cur[PSX_KMAX];
     int k, U, stride, num_zero, num_minus, num_plus, n_nbd, rank, world;
     double null_score;  // K + L0: a null configuration's L (postcal.cpp:797-803)
+    unsigned long long* trace;  // PSX_SSS_TRACE: item 1's phase clocks (null: none)
 };
 
 // neighbour i (0 .. n_nbd) or, for i == -1, the current configuration: its
@@ -2207,14 +2243,20 @@ __global__ __launch_bounds__(64) void k_sss_eval(DevProb P, SssIter it, const Ma
                                                  double* __restrict__ lk_host, SetRec* __restrict__ srec,
                                                  Acc5* __restrict__ mrec, double* __restrict__ score,
                                                  int* __restrict__ mark_host) {
-    __shared__ int srow[PSX_KMAX];
+    __shared__ EvalShm shm;
     const int p = blockIdx.x, i = p - 1, lane = threadIdx.x;
+    unsigned long long* const tr = (it.trace && p == 1 && lane == 0) ? it.trace : nullptr;
+    if (tr) tr[0] = wall_clock64();
     int row[PSX_KMAX];
     const int n = nbd_row(it, i, row);
+    // the set's operands are requested before the map probe and consumed after
+    // it: one global round trip less for an unseen set (a seen one drops them)
+    const EvalOps ops = eval_gather(P, row, it.stride, shm);
     double v = 0.0;
     unsigned long long klo, khi;
     pack_key(row, n, klo, khi);
     const int seen = map_find_wave(T, mask, klo, khi, v) ? 1 : 0;
+    if (tr) tr[1] = wall_clock64();
     if (lane == 0) {
         if (i >= 0) {
             const int mk = seen ? -1 : (n == 0 ? -2 : p);
@@ -2229,33 +2271,25 @@ __global__ __launch_bounds__(64) void k_sss_eval(DevProb P, SssIter it, const Ma
             cnt[kCurNull] = (!seen && n == 0) ? 1 : 0;
         }
     }
-    if (seen || n == 0 || p < lo || p >= hi) return;
+    if (p < lo || p >= hi) return;  // another rank's item
+    if (seen || n == 0) {
+        // zero records (a fold of a zero record is exactly a no-op): the post folds
+        // every item of the slice without looking at marks or rows
+        if (lane < it.stride) mrec[(size_t)p * it.stride + lane] = psx::acc_zero();
+        if (lane == 0) srec[p] = psx::set_zero();
+        return;
+    }
 #ifdef PSX_SSS_ABLATE
     if (PSX_SSS_ABLATE == 1) return;
 #endif
 #pragma unroll
     for (int j = 0; j < PSX_KMAX; j++)
-        if (j < it.stride && lane == j) {
-            srow[j] = row[j];
-            rows[(size_t)p * it.stride + j] = row[j];
-        }
-    __syncthreads();
-    eval_set(P, srow, it.stride, nullptr, srec + p, mrec + (size_t)p * it.stride, score + p);
+        if (j < it.stride && lane == j) rows[(size_t)p * it.stride + j] = row[j];
+    eval_stage(ops, shm);
+    if (tr) tr[2] = wall_clock64();
+    eval_compute(P, ops, shm, nullptr, srec + p, mrec + (size_t)p * it.stride, score + p, tr);
     if (mark_host && lane == 0 && i >= 0) lk_host[i] = score[p];  // the lane that wrote it
-}
-
-// member position of u in a sorted, -1 padded batch row (or -1)
-__device__ inline int member_of(const int* row, int stride, int u) {
-    int j = -1;
-    for (int q = 0; q < stride; q++)
-        if (row[q] == u) j = q;
-    return j;
-}
-
-// item p evaluated by this rank (its records exist)
-__device__ inline bool evaluated(const int* __restrict__ mark, const int* __restrict__ cnt, int p, int lo, int hi) {
-    if (p < lo || p >= hi) return false;
-    return p == 0 ? cnt[kCurPos] == 0 : mark[p - 1] == p;
+    if (tr) tr[7] = wall_clock64();
 }
 
 // blocks [0, U): per-SNP record folds; block U: the scalars; blocks > U: the
@@ -2271,18 +2305,54 @@ __global__ __launch_bounds__(256) void k_sss_post(SssIter it, int lo, int hi, co
                                                   double* __restrict__ lk_host) {
     const int b = blockIdx.x, t = threadIdx.x;
     if (mode == 2 && b <= it.U) return;
+    // Every item p of the slice [lo, hi) has records at mrec[p * stride + j]
+    // (zero records where k_sss_eval did not evaluate it), and a member's
+    // position j in item p's row follows from the iteration geometry
+    // (nbd_row), so the folds below issue their record loads without waiting
+    // for marks or rows.
+    const int k = it.k;
     if (b < it.U) {
         const int u = b;
-        bool in_cur = false;
-        for (int j = 0; j < it.k; j++) in_cur |= it.cur[j] == u;
+        int ju = -1, less = 0;  // u's slot in cur (or -1); members of cur below u
+        for (int j = 0; j < k; j++) {
+            ju = it.cur[j] == u ? j : ju;
+            less += it.cur[j] < u;
+        }
         Acc5 a = psx::acc_zero();
-        if (in_cur) {
-            // in (nearly) every item: the slice's evaluated items in item order
-            for (int p = lo + t; p < hi; p += 256)
-                if (evaluated(mark, cnt, p, lo, hi)) {
-                    const int j = member_of(rows + (size_t)p * it.stride, it.stride, u);
-                    if (j >= 0) psx::fold_acc(a, mrec[(size_t)p * it.stride + j]);
+        if (ju >= 0) {
+            // in (nearly) every item: the slice's items in item order
+            constexpr int kR = 8;  // record loads in flight per thread
+            for (int p0 = lo + t; p0 < hi; p0 += 256 * kR) {
+                Acc5 r[kR];
+#pragma unroll
+                for (int q = 0; q < kR; q++) {
+                    const int p = p0 + 256 * q;
+                    int j = -1;
+                    if (p < hi) {
+                        const int i = p - 1;
+                        if (i < 0) {
+                            j = ju;
+                        } else if (i < it.num_zero + it.num_minus) {  // swap / minus: slot v dropped
+                            const int v = i < it.num_zero ? i % k : i - it.num_zero;
+                            if (v != ju) {
+                                j = ju - (v < ju);
+                                if (i < it.num_zero) {  // + the (i / k)-th SNP outside cur
+                                    int x = i / k;
+                                    for (int c = 0; c < k; c++) x += it.cur[c] <= x;
+                                    j += x < u;
+                                }
+                            }
+                        } else {  // plus: + the x-th SNP outside cur
+                            int x = i - it.num_zero - it.num_minus;
+                            for (int c = 0; c < k; c++) x += it.cur[c] <= x;
+                            j = ju + (x < u);
+                        }
+                    }
+                    r[q] = j >= 0 ? mrec[(size_t)p * it.stride + j] : psx::acc_zero();
                 }
+#pragma unroll
+                for (int q = 0; q < kR; q++) psx::fold_acc(a, r[q]);
+            }
             __shared__ Acc5 sh[4];
             psx::wave_fold_acc(a);
             if ((t & 63) == 0) sh[t >> 6] = a;
@@ -2295,23 +2365,28 @@ __global__ __launch_bounds__(256) void k_sss_post(SssIter it, int lo, int hi, co
             return;
         }
         if (t != 0) return;
-        // u is the ri-th SNP outside cur: neighbours ri * k + v, then its plus set
-        int ri = u;
-        for (int j = 0; j < it.k; j++) ri -= it.cur[j] < u;
-        bool any = false;
-        for (int v = 0; v <= it.k; v++) {
-            int i;
-            if (v < it.k) i = ri * it.k + v;
-            else if (it.num_plus) i = it.num_zero + it.num_minus + ri;
-            else break;
+        // u is the ri-th SNP outside cur: items ri * k + v (cur with slot v swapped
+        // for u: u's position is `less`, one fewer when cur[v] < u), then its plus set
+        const int ri = u - less;
+        Acc5 r[PSX_KMAX + 1];
+        const Acc5 g0 = acc[u];
+#pragma unroll
+        for (int v = 0; v <= PSX_KMAX; v++) {
+            int i = -1, j = 0;
+            if (v < k) {
+                i = ri * k + v;
+                j = less - (it.cur[v] < u);
+            } else if (v == k && it.num_plus) {
+                i = it.num_zero + it.num_minus + ri;
+                j = less;
+            }
             const int p = i + 1;
-            if (!evaluated(mark, cnt, p, lo, hi)) continue;  // seen, null, or another rank's
-            const int j = member_of(rows + (size_t)p * it.stride, it.stride, u);
-            psx::fold_acc(a, mrec[(size_t)p * it.stride + j]);
-            any = true;
+            r[v] = (i >= 0 && p >= lo && p < hi) ? mrec[(size_t)p * it.stride + j] : psx::acc_zero();
         }
-        if (any) {
-            Acc5 g = acc[u];
+#pragma unroll
+        for (int v = 0; v <= PSX_KMAX; v++) psx::fold_acc(a, r[v]);
+        if (a.post0 != 0.0 || a.post1 != 0.0 || a.shared != 0.0 || a.sll != 0.0 || a.nsll != 0.0) {
+            Acc5 g = g0;
             psx::fold_acc(g, a);
             acc[u] = g;
         }
@@ -2320,8 +2395,7 @@ __global__ __launch_bounds__(256) void k_sss_post(SssIter it, int lo, int hi, co
     if (b == it.U) {  // the scalars: the slice's set records, then the null configurations (rank 0)
         SetRec a = psx::set_zero();
         int nu = 0, nz = 0;  // unseen neighbours, unseen null neighbours
-        for (int p = lo + t; p < hi; p += 256)
-            if (evaluated(mark, cnt, p, lo, hi)) psx::fold_set(a, srec[p]);
+        for (int p = lo + t; p < hi; p += 256) psx::fold_set(a, srec[p]);  // zero where not evaluated
         for (int i = t; i < it.n_nbd; i += 256) {
             const int mk = mark[i];
             nu += mk != -1;
@@ -2388,6 +2462,7 @@ struct SssDev {
     // (start, stop) event pairs around the evals, read kRingE iterations later
     // (by then complete) instead of once per iteration
     static constexpr int kRingE = 8;
+    static constexpr int kEvEvery = 4;  // start events on every 4th iteration (kRingE a multiple)
     hipEvent_t ev[2 * kRingE] = {};
     int* rows = nullptr;      // per item: its set (evaluated items)
     int* mark = nullptr;      // per neighbour: -1 seen, -2 unseen null, else its item
@@ -2397,6 +2472,7 @@ struct SssDev {
     SetRec* shost = nullptr;  // pinned host: the scalars after the iteration
     int* hcnt = nullptr;      // pinned host: the counters
     int* hmark = nullptr;     // pinned host: per neighbour, its mark (one rank)
+    unsigned long long* trace = nullptr;  // PSX_SSS_TRACE: item 1's eval phase clocks (pinned host)
     double* hscore = nullptr; // pinned host: gathered item scores (world > 1)
     ~SssDev() {
         psx::dfree(T);
@@ -2409,6 +2485,7 @@ struct SssDev {
         if (hcnt) psx::hfree(hcnt);
         if (hmark) psx::hfree(hmark);
         if (hscore) psx::hfree(hscore);
+        if (trace) psx::hfree(trace);
         for (int i = 0; i < 2 * kRingE; i++)
             if (ev[i]) hipEventDestroy(ev[i]);
     }
@@ -2426,6 +2503,10 @@ int sss_workspace(psx_engine* e, size_t nmax, int world, hipStream_t s) {
         HIPCHK(psx::dmalloc(&D.cnt, kNCnt * sizeof(int)));
         HIPCHK(psx::hmalloc(reinterpret_cast<void**>(&D.shost), sizeof(SetRec)));
         HIPCHK(psx::hmalloc(reinterpret_cast<void**>(&D.hcnt), kNCnt * sizeof(int)));
+        if (std::getenv("PSX_SSS_TRACE")) {
+            HIPCHK(psx::hmalloc(reinterpret_cast<void**>(&D.trace), 8 * sizeof(unsigned long long)));
+            std::memset(D.trace, 0, 8 * sizeof(unsigned long long));
+        }
     }
     if (D.nmax < nmax) {
         psx::dfree(D.rows); psx::dfree(D.mark);
@@ -2487,11 +2568,13 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
     double old_sum = 0;
     int iter;
     double kms = 0;
+    int ksamples = 0;
     auto t0 = std::chrono::steady_clock::now();
     std::vector<double> pr;
     // diagnostics (PSX_SSS_PROFILE): host time per phase of the walk, on stderr
     static const bool prof = std::getenv("PSX_SSS_PROFILE") != nullptr;
     double ph[4] = {0, 0, 0, 0};  // launch, wait for the eval, sampling, wait for the post
+    double tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // PSX_SSS_TRACE: item 1's eval phases
     auto tick = [&](int i, std::chrono::steady_clock::time_point& t) {
         if (!prof) return;
         const auto n = std::chrono::steady_clock::now();
@@ -2511,6 +2594,7 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
         it.rank = rank;
         it.world = world;
         it.null_score = e->K + e->L0;
+        it.trace = D.trace;
         const int n_nbd = it.n_nbd, n_items = n_nbd + 1;
         // this rank's contiguous slice of the items
         const int lo = (int)((int64_t)n_items * rank / world), hi = (int)((int64_t)n_items * (rank + 1) / world);
@@ -2534,13 +2618,18 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
         // plain event records around the eval (the stop event is what the host
         // waits on): hipExtLaunchKernelGGL's in-packet events cost the host ~12 us
         // more per launch here (profiles/r03i_sss_host_phases.txt)
+        // The start event only on every kEvEvery-th iteration (an event record is
+        // ~1-2 us of host time): the eval time is sampled there and scaled to all
+        // iterations; the stop event (the host's wait) on every one.
         hipEvent_t* evp = D.ev + 2 * (iter % SssDev::kRingE);
-        if (iter >= SssDev::kRingE) {  // this pair's eval of kRingE iterations ago
+        const bool timed = iter % SssDev::kEvEvery == 0;
+        if (iter >= SssDev::kRingE && (iter - SssDev::kRingE) % SssDev::kEvEvery == 0) {  // kRingE iterations ago
             float ms = 0;
             HIPCHK(hipEventElapsedTime(&ms, evp[0], evp[1]));
             kms += ms;
+            ksamples++;
         }
-        HIPCHK(hipEventRecord(evp[0], e->stream));
+        if (timed) HIPCHK(hipEventRecord(evp[0], e->stream));
         hipLaunchKernelGGL(k_sss_eval, dim3((unsigned)n_items), dim3(64), 0, e->stream, e->dp, it, D.T, mask, lo, hi,
                            D.rows, D.mark, D.cnt, D.lk, e->dsrec, e->dmrec, e->dscore, world == 1 ? D.hmark : nullptr);
         HIPCHK(hipEventRecord(evp[1], e->stream));
@@ -2559,6 +2648,12 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
             tick(0, tp);
             HIPCHK(hipEventSynchronize(evp[1]));
             tick(1, tp);
+            if (D.trace && D.trace[7]) {  // item 1's eval phases (100 MHz clock)
+                const unsigned long long* q = D.trace;
+                for (int x = 0; x < 7; x++) tph[x] += (double)(q[x + 1] - q[x]) * 0.01;
+                tph[7] += 1;
+                D.trace[7] = 0;
+            }
             for (int i = 0; i < n_nbd; i++) unseen += D.hmark[i] != -1;
         } else {
             HIPCHK(hipStreamSynchronize(e->stream));
@@ -2657,11 +2752,18 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
     {  // the evals still in the event ring (iterations 0..iter ran; `iter` itself when it broke out)
         const int ran = std::min(iter + 1, 1000);
         for (int q = std::max(0, ran - SssDev::kRingE); q < ran; q++) {
+            if (q % SssDev::kEvEvery) continue;
             float ms = 0;
             HIPCHK(hipEventElapsedTime(&ms, D.ev[2 * (q % SssDev::kRingE)], D.ev[2 * (q % SssDev::kRingE) + 1]));
             kms += ms;
+            ksamples++;
         }
+        if (ksamples) kms *= (double)ran / ksamples;  // the sampled evals' mean, over every iteration
     }
+    if (D.trace && tph[7] > 0)
+        fprintf(stderr, "[psx sss] item-1 eval us: row+probe %.2f, stage %.2f, subsets %.2f, patterns %.2f, "
+                "reductions %.2f, records %.2f (%.0f evals)\n", tph[0] / tph[7], tph[1] / tph[7], tph[2] / tph[7],
+                tph[3] / tph[7], tph[4] / tph[7], (tph[5] + tph[6]) / tph[7], tph[7]);
     if (prof)
         fprintf(stderr, "[psx sss] %d iterations, host us per iteration: launch %.1f, wait eval %.1f, sampling %.1f, "
                 "wait post %.1f; workspace %.0f us\n", iter, ph[0] / std::max(iter, 1), ph[1] / std::max(iter, 1),

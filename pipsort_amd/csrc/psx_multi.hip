@@ -407,7 +407,7 @@ int psx_multi_get_timing(psx_multi* m, psx_timing* t) {
     t->exact_rerun = m->exact;
     for (psx_engine* e : m->h) {
         psx_timing u;
-        if (psx_get_timing(e, &u) == 0 && u.exact_rerun) t->exact_rerun = 1;
+        if (psx_get_timing(e, &u) == 0) t->exact_rerun |= u.exact_rerun;
     }
     return 0;
 }

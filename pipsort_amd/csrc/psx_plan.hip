@@ -1,4 +1,5 @@
-// psx_plan.hip — a sweep plan's record CSR built on the device.
+// psx_plan.hip — a sweep plan's record CSR built on the device, and the
+// merge of a batch of generic set records (k_batch_part / k_batch_fold below).
 //
 // A plan's records are unit-major (slot i = unit * rec_stride + t): the c
 // records (t < 64), the b records (64 <= t < 128) and, for k = 3, the a
@@ -17,6 +18,7 @@
 
 #include "psx_mem.h"
 #include "psx_sweep.h"
+#include "psx_sweep_dev.h"
 
 namespace psx {
 
@@ -51,6 +53,15 @@ __global__ void k_plan_keys(const int4* __restrict__ units, long n, int rec_stri
     pos[i] = key >= 0 ? (int)i : -1;
 }
 
+// keys of a flat record array (record i's SNP, -1: none)
+__global__ void k_keys_flat(const int* __restrict__ src, long n, int U, int* __restrict__ keys, int* __restrict__ vals) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int v = src[i];
+    keys[i] = v >= 0 ? v : U;
+    vals[i] = (int)i;
+}
+
 // dptr[u] = lower_bound(sorted keys, u), u = 0 .. U
 __global__ void k_plan_dptr(const int* __restrict__ skeys, long n, int U, int* __restrict__ dptr) {
     const int u = blockIdx.x * blockDim.x + threadIdx.x;
@@ -67,9 +78,9 @@ int chk(hipError_t e) { return e == hipSuccess ? 0 : -1; }
 
 }  // namespace
 
-int plan_csr_device(const int4* d_units, int n_units, int rec_stride, int k, int variant, int pad, int U, int* d_pos,
-                    int* d_dptr, int* d_gidx, PlanScratch& S, hipStream_t st) {
-    const long n = (long)n_units * rec_stride;
+// keys / slots of n records -> stable radix sort by SNP -> gidx, dptr
+template <typename FillKeys>
+int sort_to_csr(long n, int U, int* d_dptr, int* d_gidx, PlanScratch& S, hipStream_t st, FillKeys fill) {
     if (n == 0) return chk(hipMemsetAsync(d_dptr, 0, sizeof(int) * (U + 1), st));
     int end_bit = 1;
     while ((1 << end_bit) <= U) end_bit++;
@@ -90,13 +101,230 @@ int plan_csr_device(const int4* d_units, int n_units, int rec_stride, int k, int
     int* skeys = keys + n;
     int* vals = skeys + n;
     void* sort_tmp = (void*)(((uintptr_t)(vals + n) + 255) & ~(uintptr_t)255);
-    hipLaunchKernelGGL(k_plan_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d_units, n, rec_stride, k,
-                       variant, pad, U, keys, vals, d_pos);
+    fill(keys, vals);
     if (chk(hipGetLastError())) return -1;
     // stable: equal SNPs keep increasing slot order (the fold order of the merges)
     if (chk(hipcub::DeviceRadixSort::SortPairs(sort_tmp, tmp, keys, skeys, vals, d_gidx, (int)n, 0, end_bit, st)))
         return -1;
     hipLaunchKernelGGL(k_plan_dptr, dim3((U + 1 + 255) / 256), dim3(256), 0, st, skeys, n, U, d_dptr);
+    return chk(hipGetLastError());
+}
+
+int plan_csr_device(const int4* d_units, int n_units, int rec_stride, int k, int variant, int pad, int U, int* d_pos,
+                    int* d_dptr, int* d_gidx, PlanScratch& S, hipStream_t st) {
+    const long n = (long)n_units * rec_stride;
+    return sort_to_csr(n, U, d_dptr, d_gidx, S, st, [&](int* keys, int* vals) {
+        hipLaunchKernelGGL(k_plan_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d_units, n, rec_stride,
+                           k, variant, pad, U, keys, vals, d_pos);
+    });
+}
+
+// the CSR of records laid out flat with SNP keys[i] (-1: none): dptr[U + 1],
+// gidx[n] (records of SNP u in increasing index order at [dptr[u], dptr[u + 1]))
+int csr_from_keys_device(const int* d_keys, long n, int U, int* d_dptr, int* d_gidx, PlanScratch& S, hipStream_t st) {
+    return sort_to_csr(n, U, d_dptr, d_gidx, S, st, [&](int* keys, int* vals) {
+        hipLaunchKernelGGL(k_keys_flat, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d_keys, n, U, keys,
+                           vals);
+    });
+}
+
+// ---------------------------------------------------------------------------
+// Set-batch merge (psx_eval_union_batch, the generic levels): fold the member
+// records of n union sets ([set][stride], record j of a set = its j-th member)
+// into the per-SNP accumulators and the set records into the scalars, in two
+// launches and a fixed order, without a device-wide sort.
+//   k_batch_part  chunk c = 2048 records of whole sets: a block radix-sorts the
+//                 chunk's (SNP, record) pairs in LDS; each thread folds the runs
+//                 of its 8 sorted positions, a fixed binary tree over the
+//                 threads joins the runs that cross threads; every SNP's chunk
+//                 total goes to part[c][u] + a presence bit, the chunk's set
+//                 records to spart[c]
+//   k_batch_fold  a wave per SNP u folds part[0..nc)[u] (present ones, nc <= 64)
+//                 by a fixed shuffle tree into acc[u]; one wave folds
+//                 spart[0..nc) into the scalars
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr int kBT = 256, kBI = 8;
+constexpr int kBWords = 4096;  // presence bitmap words in LDS: U <= 131072
+
+// A run of equal SNPs over a range of sorted positions: the first and last runs
+// (possibly the same: full) of the range, and its first / last SNPs; the runs
+// strictly inside have been emitted.
+struct BRange {
+    int fk, lk, full, pad;
+    Acc5 F, L;
+};
+
+__global__ __launch_bounds__(kBT) void k_batch_part(const int* __restrict__ sets, int stride, long nsets, int spc,
+                                                   int U, int end_bit, const Acc5* __restrict__ rec,
+                                                   const SetRec* __restrict__ srec, Acc5* __restrict__ part,
+                                                   unsigned* __restrict__ bits, int words, SetRec* __restrict__ spart) {
+    using Sort = hipcub::BlockRadixSort<int, kBT, kBI, int>;
+    __shared__ union {
+        typename Sort::TempStorage sort;
+        BRange node[kBT];
+    } sh;
+    __shared__ SetRec sw[kBT / 64];
+    __shared__ unsigned sbits[kBWords];
+    const int t = threadIdx.x, c = blockIdx.x;
+    const long s0 = (long)c * spc, s1 = s0 + spc < nsets ? s0 + spc : nsets;
+    const int n = (int)((s1 - s0) * stride);
+    const int* ks = sets + s0 * stride;
+    const Acc5* rc = rec + s0 * stride;
+    for (int w = t; w < words; w += kBT) sbits[w] = 0u;
+    int key[kBI], val[kBI];
+#pragma unroll
+    for (int j = 0; j < kBI; j++) {
+        const int i = t * kBI + j;
+        const int v = i < n ? ks[i] : -1;
+        key[j] = v >= 0 ? v : U;  // no SNP: sorted behind every SNP
+        val[j] = i;
+    }
+    Sort(sh.sort).Sort(key, val, 0, end_bit);  // blocked: thread t holds sorted positions 8t .. 8t + 7
+    Acc5 r[kBI];
+#pragma unroll
+    for (int j = 0; j < kBI; j++) r[j] = key[j] < U ? rc[val[j]] : acc_zero();
+    auto emit = [&](int u, const Acc5& g) {
+        if (u >= U) return;
+        part[(size_t)c * U + u] = g;
+        atomicOr(&sbits[u >> 5], 1u << (u & 31));
+    };
+    // the thread's 8 positions: runs inside are complete, the first and last stay open
+    BRange A;
+    A.fk = key[0];
+    A.full = 1;
+    A.F = acc_zero();
+    Acc5 cur = acc_zero();
+    int ck = key[0];
+#pragma unroll
+    for (int j = 0; j < kBI; j++) {
+        if (key[j] != ck) {
+            if (A.full) A.F = cur;
+            else emit(ck, cur);
+            A.full = 0;
+            cur = acc_zero();
+            ck = key[j];
+        }
+        fold_acc(cur, r[j]);
+    }
+    A.lk = ck;
+    A.L = cur;
+    if (A.full) A.F = cur;
+    __syncthreads();  // the sort's LDS is reused for the ranges
+    // Fixed binary tree over the 256 ranges (left folds right): a run is
+    // emitted once it is closed on both sides, so each SNP of the chunk once.
+    for (int h = 1; h < kBT; h <<= 1) {
+        if ((t & (h - 1)) == 0 && (t & h)) sh.node[t] = A;
+        __syncthreads();
+        if ((t & (2 * h - 1)) == 0) {
+            const BRange& B = sh.node[t + h];
+            if (A.lk == B.fk) {
+                Acc5 mid = A.L;
+                fold_acc(mid, B.F);
+                if (A.full && B.full) {
+                    A.F = A.L = mid;
+                } else if (A.full) {
+                    A.F = mid;
+                    A.L = B.L;
+                    A.lk = B.lk;
+                    A.full = 0;
+                } else if (B.full) {
+                    A.L = mid;
+                } else {
+                    emit(A.lk, mid);
+                    A.L = B.L;
+                    A.lk = B.lk;
+                }
+            } else {
+                if (!A.full) emit(A.lk, A.L);
+                if (!B.full) emit(B.fk, B.F);
+                A.L = B.L;
+                A.lk = B.lk;
+                A.full = 0;
+            }
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        emit(A.fk, A.F);
+        if (!A.full) emit(A.lk, A.L);
+    }
+    // the chunk's set records, thread-strided then wave and block trees
+    SetRec a = set_zero();
+    for (long i = s0 + t; i < s1; i += kBT) fold_set(a, srec[i]);
+    wave_fold_set(a);
+    if ((t & 63) == 0) sw[t >> 6] = a;
+    __syncthreads();
+    for (int w = t; w < words; w += kBT) bits[(size_t)c * words + w] = sbits[w];
+    if (t == 0) {
+        SetRec g = sw[0];
+        for (int w = 1; w < kBT / 64; w++) fold_set(g, sw[w]);
+        spart[c] = g;
+    }
+}
+
+// a wave per SNP: lane c takes chunk c's partial (nc <= 64), a fixed shuffle
+// tree folds them, lane 0 folds the result into acc[u]
+__global__ __launch_bounds__(256) void k_batch_fold(const Acc5* __restrict__ part, const unsigned* __restrict__ bits,
+                                                   int words, int nc, int U, const SetRec* __restrict__ spart,
+                                                   Acc5* __restrict__ acc, SetRec* __restrict__ sacc) {
+    const int lane = threadIdx.x & 63;
+    const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (u < U) {
+        const bool have = lane < nc && ((bits[(size_t)lane * words + (u >> 5)] >> (u & 31)) & 1u);
+        Acc5 g = have ? part[(size_t)lane * U + u] : acc_zero();
+        const unsigned long long any = __ballot(have);
+        if (any) {
+            wave_fold_acc(g);
+            if (lane == 0) {
+                Acc5 a = acc[u];
+                fold_acc(a, g);
+                acc[u] = a;
+            }
+        }
+    }
+    if (blockIdx.x == 0) {
+        SetRec s = threadIdx.x < nc ? spart[threadIdx.x] : set_zero();
+        if (threadIdx.x < 64) {
+            wave_fold_set(s);
+            if (threadIdx.x == 0) {
+                SetRec g = *sacc;
+                fold_set(g, s);
+                *sacc = g;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+int batch_merge_chunks(long nsets, int stride) {
+    const long spc = (kBT * kBI) / stride;
+    return (int)((nsets + spc - 1) / spc);
+}
+
+size_t batch_merge_bytes(long nsets, int stride, int U) {
+    const size_t nc = (size_t)batch_merge_chunks(nsets, stride), words = ((size_t)U + 31) / 32;
+    return nc * ((size_t)U * sizeof(Acc5) + words * sizeof(unsigned) + sizeof(SetRec)) + 256;
+}
+
+int launch_merge_batch(const int* d_sets, int stride, long nsets, int U, const Acc5* rec, const SetRec* srec,
+                       void* scratch, Acc5* acc, SetRec* sacc, hipStream_t st) {
+    if (nsets <= 0) return 0;
+    const int words = (U + 31) / 32;
+    if (words > kBWords || stride < 1 || stride > kBT * kBI) return -1;
+    const int spc = (kBT * kBI) / stride, nc = batch_merge_chunks(nsets, stride);
+    int end_bit = 1;
+    while ((1 << end_bit) <= U) end_bit++;
+    Acc5* part = (Acc5*)scratch;
+    SetRec* spart = (SetRec*)(part + (size_t)nc * U);
+    unsigned* bits = (unsigned*)(spart + nc);
+    hipLaunchKernelGGL(k_batch_part, dim3(nc), dim3(kBT), 0, st, d_sets, stride, nsets, spc, U, end_bit, rec, srec,
+                       part, bits, words, spart);
+    if (chk(hipGetLastError())) return -1;
+    hipLaunchKernelGGL(k_batch_fold, dim3((U + 3) / 4), dim3(256), 0, st, part, bits, words, nc, U, spart, acc,
+                       sacc);
     return chk(hipGetLastError());
 }
 

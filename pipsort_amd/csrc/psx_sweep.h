@@ -149,6 +149,17 @@ struct PlanScratch {
 // a plan's record CSR (pos | dptr | gidx) built on the device from its units
 int plan_csr_device(const int4* d_units, int n_units, int rec_stride, int k, int variant, int pad, int U, int* d_pos,
                     int* d_dptr, int* d_gidx, PlanScratch& scratch, hipStream_t st);
+// the CSR of flat records keyed by SNP (-1: none): dptr[U + 1], gidx[n]
+int csr_from_keys_device(const int* d_keys, long n, int U, int* d_dptr, int* d_gidx, PlanScratch& scratch,
+                         hipStream_t st);
+// Merge n generic set evaluations ([set][stride] members, -1 after them;
+// member records rec[set * stride + j], set records srec[set]) into acc / sacc
+// in a fixed order (psx_plan.hip); scratch of batch_merge_bytes(); -1 when U
+// or stride is outside the kernels' range (use the CSR merge).
+size_t batch_merge_bytes(long nsets, int stride, int U);
+int batch_merge_chunks(long nsets, int stride);
+int launch_merge_batch(const int* d_sets, int stride, long nsets, int U, const Acc5* rec, const SetRec* srec,
+                       void* scratch, Acc5* acc, SetRec* sacc, hipStream_t st);
 // GPU self-check: the device CSR of a plan equals the host restatement's
 int plan_csr_selftest(int U, const unsigned char* pres, int k, int rank, int world, int variant, long* mismatches,
                       long* records);
@@ -223,6 +234,8 @@ int sweep_stats(SweepPlanCache& cache, int k, int U, int rank, int world, SweepS
 void sweep_free(SweepPlanCache& cache);
 int launch_merge_members(const Acc5* rec, const int* ptr, const int* idx, const int* rows, int n_rows, Acc5* acc,
                          hipStream_t st);
+// per-SNP folds of records through a dptr / gidx CSR (one block per SNP, empty runs return)
+int launch_merge_dptr(const Acc5* rec, const int* dptr, const int* gidx, int U, Acc5* acc, hipStream_t st);
 int launch_merge_sets(const SetRec* rec, long n, const SetRec& extra, SetRec* acc, hipStream_t st,
                       bool init = false, int* zero_flag = nullptr);
 const char* sweep_error();

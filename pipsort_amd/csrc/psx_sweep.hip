@@ -176,6 +176,42 @@ int launch_merge_members(const Acc5* rec, const int* ptr, const int* idx, const 
     return 0;
 }
 
+// k_merge_members over a dptr CSR: block u folds SNP u's records (8 loads in
+// flight per thread), the fold order of k_merge_members
+__global__ __launch_bounds__(256) void k_merge_dptr(const Acc5* __restrict__ rec, const int* __restrict__ dptr,
+                                                    const int* __restrict__ gidx, Acc5* __restrict__ acc) {
+    __shared__ Acc5 sh[4];
+    const int u = blockIdx.x;
+    const int b = dptr[u], e = dptr[u + 1];
+    if (b == e) return;  // uniform
+    Acc5 a = acc_zero();
+    for (int i0 = b + (int)threadIdx.x; i0 < e; i0 += 256 * MERGE_R) {
+        int ix[MERGE_R];
+#pragma unroll
+        for (int r = 0; r < MERGE_R; r++) ix[r] = i0 + 256 * r < e ? gidx[i0 + 256 * r] : -1;
+        Acc5 v[MERGE_R];
+#pragma unroll
+        for (int r = 0; r < MERGE_R; r++) v[r] = ix[r] >= 0 ? rec[ix[r]] : acc_zero();
+#pragma unroll
+        for (int r = 0; r < MERGE_R; r++) fold_acc(a, v[r]);
+    }
+    wave_fold_acc(a);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Acc5 g = acc[u];
+        for (int w = 0; w < 4; w++) fold_acc(g, sh[w]);
+        acc[u] = g;
+    }
+}
+
+int launch_merge_dptr(const Acc5* rec, const int* dptr, const int* gidx, int U, Acc5* acc, hipStream_t st) {
+    if (U <= 0) return 0;
+    hipLaunchKernelGGL(k_merge_dptr, dim3(U), dim3(256), 0, st, rec, dptr, gidx, acc);
+    SWCHK(hipGetLastError());
+    return 0;
+}
+
 int launch_merge_sets(const SetRec* rec, long n, const SetRec& extra, SetRec* acc, hipStream_t st, bool init,
                       int* zero_flag) {
     hipLaunchKernelGGL(k_merge_sets, dim3(1), dim3(512), 0, st, rec, n, extra, acc, init ? 1 : 0, zero_flag);

@@ -1210,8 +1210,10 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         };
         // SEP (off-diagonal units): the {} / {a} parts of the prior-weighted one-study
         // dot products and the walk sums V_s[0 .. 2] have closed forms (a prologue,
-        // after the walk).  notSharedLL (NB) stays whole: its per-set precision check
-        // (kTinyNs) needs the whole value.
+        // after the walk).  Their notSharedLL (NB) holds only the {b, c} / {a, b, c}
+        // part, so it is not checked per step: the b slot's whole notSharedLL total
+        // (closed-form + walk parts) is checked against kTinyNs once, after the
+        // unit (the `low` flag below).  Diagonal units keep the per-step NB check.
         // finish(j)'s LDS operands: its slot's {b} / {a, b} terms and scale, and the
         // exp2 table entries of the chain's split (read as soon as the chain ends)
         struct FTt {
@@ -1484,7 +1486,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             // to underflow (< 2^-1074 each) is below 2^-174 of it; below, exact rerun
             const bool low = okb && sNs[t] < kTinyNs;
             if (!wide && __builtin_amdgcn_ballot_w64(low))
-                if (low) atomicOr(flag, 1);
+                if (low) atomicOr(flag, 2);  // bit 1: the SEP b-slot trigger (psx_timing.exact_rerun)
         }
         if (diag) fold_acc(rc, rb);
         if (posC >= 0) store_rec(rec + posC, rc);

@@ -101,7 +101,7 @@ def test_async_reports_exact_flag_and_sync_path_recovers(gpu):
     mi = _extreme()
     ref = E.PostCal(mi)
     ref.run_exhaustive()  # synchronous: reruns the exact variant itself
-    assert ref.timing()["exact_rerun"] == 1
+    assert ref.timing()["exact_rerun"] != 0
     r = ref.accum()
     assert ref.sync() is False  # handled: the sticky copy was cleared
     pc = E.PostCal(mi)

@@ -392,6 +392,62 @@ def test_union_batch_heavy_rows(gpu):
     assert abs(a.total - b.total) <= 1e-12 * abs(a.total)
 
 
+def test_union_batch_merge_routes(gpu):
+    """A batch beyond 64 merge chunks (here 120,000 two-member sets) folds
+    through the device radix-sorted CSR, smaller ones through the chunked
+    two-launch merge: the same sets either way give the same accumulators up
+    to fold-order rounding, and equal scores."""
+    ld, z, _, _, u2l = synth.syn_v1(160)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    rng = np.random.default_rng(9)
+    a = rng.integers(0, 160, 120_000)
+    b = (a + 1 + rng.integers(0, 159, a.size)) % 160
+    sets = np.sort(np.stack([a, b], 1), 1).astype(np.int32)
+    big, small = E.PostCal(seam), E.PostCal(seam)
+    s1 = big.eval_union_batch(sets, accumulate=True)
+    s2 = np.concatenate([small.eval_union_batch(sets[i:i + 30_000], accumulate=True)
+                         for i in range(0, len(sets), 30_000)])
+    assert np.array_equal(s1, s2)
+    x, y = big.accum(), small.accum()
+    assert x.n_configs == y.n_configs
+    for f in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+        assert np.array_equal(getattr(x, f) == 0, getattr(y, f) == 0), f
+        np.testing.assert_allclose(getattr(x, f), getattr(y, f), rtol=1e-12, atol=0, err_msg=f)
+    assert abs(x.total - y.total) <= 1e-12 * abs(x.total)
+    # and the chunked merge is deterministic
+    again = E.PostCal(seam)
+    for i in range(0, len(sets), 30_000):
+        again.eval_union_batch(sets[i:i + 30_000], accumulate=True)
+    z2 = again.accum()
+    for f in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+        assert np.array_equal(getattr(y, f), getattr(z2, f)), f
+
+
+def test_union_batch_padding_anywhere(gpu):
+    """-1 padding may sit between members (the batch only asks ascending
+    members): the records of such a row fold into the same SNPs, bitwise equal
+    to the compacted rows, and the empty rows are null configurations."""
+    ld, z, _, _, u2l = synth.syn_v1(90)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    rng = np.random.default_rng(5)
+    rows = [np.sort(rng.choice(90, rng.integers(1, 4), replace=False)) for _ in range(400)]
+    tight = np.full((len(rows) + 2, 3), -1, np.int32)
+    holes = np.full((len(rows) + 2, 3), -1, np.int32)
+    for i, r in enumerate(rows):
+        tight[i, :len(r)] = r
+        slots = np.sort(rng.choice(3, len(r), replace=False))
+        holes[i, slots] = r
+    a_pc, b_pc = E.PostCal(seam), E.PostCal(seam)
+    sa = a_pc.eval_union_batch(tight, accumulate=True)
+    sb = b_pc.eval_union_batch(holes, accumulate=True)
+    assert np.array_equal(sa, sb)
+    a, b = a_pc.accum(), b_pc.accum()
+    assert a.n_configs == b.n_configs
+    for f in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    assert a.total == b.total
+
+
 def test_deterministic_and_reusable(gpu):
     ld, z, _, _, u2l = synth.syn_v1(300)
     seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
@@ -467,7 +523,14 @@ def test_full_size_properties(gpu):
 def test_extreme_signal_exact_rerun(gpu):
     """A shared SNP with z ~ 45 in both studies: its quadratic gain exceeds 900
     bits in both, so notSharedLL groups sit beyond the fast kernel's rescale
-    range; the engine must detect it and re-sweep with the exact variant."""
+    range; the engine must detect it and re-sweep with the exact variant.
+
+    The check that fires is bit 0 (a set's / an a or c slot's group).  Bit 1,
+    the off-diagonal b-slot total, is a backstop no locus reaches: a unit kept
+    by the fast variant adds at most kMaxRefGap = 960 bits of b over both
+    studies, so b's notSharedLL is at least 2^-480 of its slot's maximum; a unit
+    beyond that is redone by the robust variant, whose per-set check is bit 0
+    (profiles/r05l_exact_bits_scan.txt: z1 30..50 on two loci, bit 1 never)."""
     M = 80
     idx = np.arange(M)
     ld, z = [], []
@@ -483,7 +546,7 @@ def test_extreme_signal_exact_rerun(gpu):
     seam = E.seam_from_arrays(ld, z, u2l, (12000, 9000), max_causal=3, sharing_param=0.3)
     pc = E.PostCal(seam)
     pc.run_exhaustive()
-    assert pc.timing()["exact_rerun"] == 1
+    assert pc.timing()["exact_rerun"] == 1  # bit 0 only
     assert_parity(pc.accum(), O.postcal(seam), pip_tol=1e-9, ll_rtol=1e-10)
 
 
