@@ -41,6 +41,7 @@
 #include <hip/hip_ext.h>
 
 #include <string>
+#include <type_traits>
 
 #include "psx_sweep.h"
 #include "psx_sweep_dev.h"
@@ -336,6 +337,7 @@ struct Sweep3FastSmem {
     double2 abMu[64], abMuB[64];  // the slot's {a, b} / {b} weights relative to 2^Ru_s (wave reference)
     float bW[64];  // membership weight of the slot's b (0, 1 or 3)
     double sW0[64], sW1[64], sW2[64], sSl[64], sNs[64];
+    double sW2w[64], sSlw[64];  // the current a's walk part of sW2 / sSl, at 2^(Ru_0 + Ru_1)
     union {
         struct {  // off-diagonal units (closed-form sums, sweep3_unit_fast): this lane's c terms
             double2 bcsm[64];   // the {b, c} weights of this lane's c summed over the block, both studies
@@ -739,6 +741,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     double (&sW2)[64] = F.sW2;
     double (&sSl)[64] = F.sSl;
     double (&sNs)[64] = F.sNs;
+    double (&sW2w)[64] = F.sW2w;
+    double (&sSlw)[64] = F.sSlw;
 
     const int t = threadIdx.x;
     const unsigned long long t_start = A.trace ? wall_clock64() : 0ull;
@@ -774,7 +778,9 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
     }
     bW[t] = (float)memb_weight(pbl);
     int sMt = EMPTY;  // shift of the b slots (wave-uniform: every a moves all slots alike)
+    int eZ = 0;       // this a's walk scale of the sW2 / sSl parts: 2^eZ of the slot shift
     sW0[t] = sW1[t] = sW2[t] = sSl[t] = sNs[t] = 0.0;
+    sW2w[t] = sSlw[t] = 0.0;
 
     const int vc = 64 * C + t, uc = vc - pad;
     const bool okc = vc >= pad;
@@ -1081,11 +1087,18 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             const int Ms = max(sMt, Gm), d = sMt - Ms;
             sW0[t] = ldexp(sW0[t], d);
             sW1[t] = ldexp(sW1[t], d);
-            sW2[t] = ldexp(sW2[t], d);
-            sSl[t] = ldexp(sSl[t], d);
+            sW2[t] = ldexp(sW2[t] + ldexp(sW2w[t], eZ), d);  // the previous a's walk part joins
+            sSl[t] = ldexp(sSl[t] + ldexp(sSlw[t], eZ), d);
+            sW2w[t] = sSlw[t] = 0.0;
             sNs[t] = ldexp(sNs[t], d);
             sMt = Ms;
             fS = ldexp(1.0, G - Ms);
+            // The slot's b-in-both-studies sums take fS lam_0 lam_1 = 2^(G - Ms +
+            // Ru_0 - R_0 + Ru_1 - R_1) = 2^(Ru_0 + Ru_1 - Ms) per lane: one scale for
+            // the wave (a lane clamped at kMaxSpread makes the unit wide: redone), so
+            // the walk adds them unscaled into sW2w / sSlw and the scale is applied
+            // once, when the next a (or the unit end) folds them into sW2 / sSl
+            eZ = Ru[0] + Ru[1] - Ms;
         }
         if (A.trace && ai == 0) t_fn[2] = wall_clock64();
         if (sep) {
@@ -1148,9 +1161,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         // the slot scale rides in the prior-weighted vectors (only the b-slot dot
         // products use them from here on; a power of two, so exact above underflow)
         // (uW_s / uL_s meet study 1 - s's b-weights: lam_(1 - s); the {b, c} x
-        // {a, b, c} products carry lam_0 lam_1 with the slot scale, fSz)
+        // {a, b, c} products, lam_0 lam_1 with the slot scale: 2^eZ, applied per a)
         const double fW[2] = {fS * lam1, fS * lam0};
-        const double fSz = fS * (lam0 * lam1);
 #pragma unroll
         for (int s = 0; s < 2; s++)
 #pragma unroll
@@ -1189,9 +1201,16 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         // fetched two steps ahead, the {b, c} weights one.
         bool tiny = false;
         int dA = -(1 << 20);  // largest n_abc - Ru over the walk (both studies)
-        auto chain = [&](int j, double2 g, int (&N)[2], double (&q)[2]) {
-            const int bs = (t + j) & 63;
-            const double2 aG = F.abG[bs], aI = F.abI[bs], aIW = F.abIW[bs], aH = F.abH[bs], aR = F.abR[bs];
+        // Step j's b slot is bs = (t + j) & 63; the lambdas take its LDS byte
+        // offsets (o16 = 16 bs into the double2 slot arrays, o8 = 8 bs into the
+        // double ones), stepped by the walk (one add and mask per step)
+        auto slot = [](const auto& arr, unsigned off) -> const auto& {
+            return *reinterpret_cast<const std::remove_reference_t<decltype(arr[0])>*>(
+                reinterpret_cast<const char*>(arr) + off);
+        };
+        auto chain = [&](unsigned o16, double2 g, int (&N)[2], double (&q)[2]) {
+            const double2 aG = slot(F.abG, o16), aI = slot(F.abI, o16), aIW = slot(F.abIW, o16),
+                          aH = slot(F.abH, o16), aR = slot(F.abR, o16);
 #pragma unroll
             for (int s = 0; s < 2; s++) {
                 // x = the unnormalised L entry of c against b; D_ab I_ab = 1 folds the pivot away
@@ -1220,13 +1239,13 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             double2 muB, mu;  // the slot's {b} / {a, b} weights relative to 2^Ru_s
             double tb0, tb1;
         };
-        auto ld_ft = [&](int j, const int (&N)[2]) {
-            const int bs = (t + j) & 63;
-            return FTt{F.abMuB[bs], F.abMu[bs], tab[N[0] & 255], tab[N[1] & 255]};
+        auto ld_ft = [&](unsigned o16, const int (&N)[2]) {
+            return FTt{slot(F.abMuB, o16), slot(F.abMu, o16), tab[N[0] & 255], tab[N[1] & 255]};
         };
-        auto finish_ft = [&](int j, const FTt& ft, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
+        auto finish_ft = [&](unsigned o8, const FTt& ft, const int (&N)[2], const double (&q)[2], double2 mcur,
+                             int2 ncur) {
             constexpr bool sepc = SEP;
-            const int bs = (t + j) & 63;
+            auto acc = [&](double (&arr)[64]) -> double* { return reinterpret_cast<double*>(reinterpret_cast<char*>(arr) + o8); };
             const double2 aMuB = ft.muB, aMu = ft.mu;
             // v[s][A] = E_s[A + b] relative to 2^{Ru_s}: {b}, {a, b}, {b, c}, {a, b, c}
             double v[2][4];
@@ -1282,15 +1301,16 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             // ---- b slot (LDS, x fS: WB0 / WB1 carry it from uW) ----
             // LDS float adds: no read round trip; one lane per slot per step, and a
             // wave's LDS instructions execute in issue order (deterministic)
-            __hip_atomic_fetch_add(&sW0[bs], WB0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&sW1[bs], WB1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&sW2[bs], WB2 * fSz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&sSl[bs], LB2 * fSz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&sNs[bs], sepc ? NB : NB * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (!ALLPRES) npat += wac * bW[bs];
+            __hip_atomic_fetch_add(acc(sW0), WB0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(acc(sW1), WB1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(acc(sW2w), WB2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(acc(sSlw), LB2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(acc(sNs), sepc ? NB : NB * fS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (!ALLPRES) npat += wac * *reinterpret_cast<const float*>(reinterpret_cast<const char*>(bW) + (o8 >> 1));
         };
+        auto o16of = [&](int j) { return (unsigned)((t + j) & 63) << 4; };
         auto finish = [&](int j, const int (&N)[2], const double (&q)[2], double2 mcur, int2 ncur) {
-            finish_ft(j, ld_ft(j, N), N, q, mcur, ncur);
+            finish_ft(o16of(j) >> 1, ld_ft(o16of(j), N), N, q, mcur, ncur);
         };
         // Steps on which every lane is active run pipelined: the whole walk of an
         // off-diagonal tile, and steps 1..30 of a diagonal tile whose a lies
@@ -1306,32 +1326,41 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             // Loads run up to three rows ahead unclamped (the buffers carry
             // kTileRowPad rows past the last tile; what lies past je is not used),
             // so they address off one lane offset with immediate row offsets
-            const double2* gb = A.g01 + (size_t)tile * 4096;
-            const double2* mb = A.mu01 + (size_t)tile * 4096;
-            const int2* nb = A.bcn + (size_t)tile * 4096;
-            double2 g_next = gb[(j0 + 1) * 64 + t];
+            // (the tile bases are wave-uniform and the lane's row offset a 32-bit
+            // unsigned byte count: base + offset + row immediates, one add per pair)
+            const char* gb = (const char*)(A.g01 + (size_t)tile * 4096);
+            const char* mb = (const char*)(A.mu01 + (size_t)tile * 4096);
+            const char* nb = (const char*)(A.bcn + (size_t)tile * 4096);
+            unsigned o16 = (unsigned)(j0 * 64 + t) * 16u, o8 = o16 >> 1;  // double2 / int2 rows: 1024 / 512 bytes
+            double2 g_next = *(const double2*)(gb + o16 + 1024);
             double2 m_cur = mnx;
             int2 n_cur = nnx;
             int NA[2], NB[2];
             double qA[2], qB[2];
-            chain(j0, gnx, NA, qA);
+            unsigned s8 = o16of(j0) >> 1;  // step j's slot offset (8-byte arrays)
+            chain(s8 << 1, gnx, NA, qA);
             // each finish's LDS operands are read right after the chain it follows,
             // one half step pair before the finish runs
-            FTt ftA = ld_ft(j0, NA);
+            FTt ftA = ld_ft(s8 << 1, NA);
             for (int j = j0; j < je; j += 2) {
-                const int o = j * 64 + t;
-                double2 m_nxt = mb[o + 64];
-                int2 n_nxt = nb[o + 64];
-                double2 g_after = gb[o + 128];
-                chain(j + 1, g_next, NB, qB);
-                finish_ft(j, ftA, NA, qA, m_cur, n_cur);
-                const FTt ftB = ld_ft(j + 1, NB);
+                // (advanced first: the pair's loads all address off the new offsets,
+                // so the old ones die here and the loop carries no register copy)
+                o16 += 2048u;
+                o8 += 1024u;
+                double2 m_nxt = *(const double2*)(mb + o16 - 1024);
+                int2 n_nxt = *(const int2*)(nb + o8 - 512);
+                double2 g_after = *(const double2*)(gb + o16);
+                const unsigned s8b = (s8 + 8u) & 504u;
+                chain(s8b << 1, g_next, NB, qB);
+                finish_ft(s8, ftA, NA, qA, m_cur, n_cur);
+                const FTt ftB = ld_ft(s8b << 1, NB);
+                s8 = (s8b + 8u) & 504u;  // step j + 2 (the old offset is dead: no loop copy)
                 // b-slot ownership rotates across lanes every step: the workgroup is
                 // one wave and LDS executes a wave's instructions in issue order
                 __builtin_amdgcn_wave_barrier();
-                m_cur = mb[o + 128];
-                n_cur = nb[o + 128];
-                g_next = gb[o + 192];
+                m_cur = *(const double2*)(mb + o16);
+                n_cur = *(const int2*)(nb + o8);
+                g_next = *(const double2*)(gb + o16 + 1024);
                 // the row loads at the top of this pair of steps are first used here
                 // (and this half's loads first in the next pair): pinned, so the
                 // scheduler cannot hoist a use to where it would wait for a load
@@ -1340,9 +1369,9 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
                 pin_vgpr(m_nxt);
                 pin_vgpr(n_nxt);
                 pin_vgpr(g_after);
-                chain(j + 2, g_after, NA, qA);  // (the last pair's is not used)
-                finish_ft(j + 1, ftB, NB, qB, m_nxt, n_nxt);
-                ftA = ld_ft(j + 2, NA);
+                chain(s8 << 1, g_after, NA, qA);  // (the last pair's is not used)
+                finish_ft(s8b, ftB, NB, qB, m_nxt, n_nxt);
+                ftA = ld_ft(s8 << 1, NA);
                 __builtin_amdgcn_wave_barrier();
                 pin_vgpr(m_cur);
                 pin_vgpr(n_cur);
@@ -1376,7 +1405,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
             if (act) {
                 int N[2];
                 double q[2];
-                chain(j, gcur, N, q);
+                chain(o16of(j), gcur, N, q);
                 finish(j, N, q, mcur, ncur);  // (never in SEP units: their walk is all pipelined)
                 nact++;
             }
@@ -1479,7 +1508,8 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         // a diagonal tile's lane t and b slot t are one SNP: one record (the plan
         // keys no b records there), folded here instead of in the merge
         Acc5 rc = wrec(mC, cW0, cW1, cW2, cSl, cNs, rho, A.Ck, A.pit0);
-        const Acc5 rb = wrec(sMt, sW0[t], sW1[t], sW2[t], sSl[t], sNs[t], rho, A.Ck, A.pit0);
+        const Acc5 rb = wrec(sMt, sW0[t], sW1[t], sW2[t] + ldexp(sW2w[t], eZ), sSl[t] + ldexp(sSlw[t], eZ), sNs[t],
+                             rho, A.Ck, A.pit0);
         if (sep) {
             // the b slot's notSharedLL total (closed-form and walk parts) against the
             // fast path's floor: at or above 2^-900 of the slot shift, every term lost
