@@ -1274,7 +1274,7 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     if (async) {
         if (!e->cstream) {
             // reserved CUs for overlapped sweeps (PSX_OVERLAP = n, opt-in), decided
-            // at the handle's first asynchronous pass.  Measured:
+            // at the handle's first asynchronous pass.  Measured (EXPERIMENTS.md C):
             // worlds 4 / 8 -2 .. -5 % on some boxes, neutral on others, world 1
             // +2 %; rebuilding the streams when a handle's world changed was
             // 20-25 % slower (r04u), so it is not switched per world.

@@ -353,6 +353,7 @@ int plan_units(int k, int U, int ldg, int rank, int world, const unsigned char* 
 constexpr double kTailFrac = 0.05;  // share of a shard's work cut into single-a units at the end (PSX_K3_TAIL)
 constexpr double kDiagW = 0.65;   // per-a cost of a pipelined diagonal walk (PSX_K3_DIAGW; 0.59 before r04ae)
 constexpr double kUnitW = 0.04;   // fixed cost of a unit (PSX_K3_UNITW)
+constexpr int kPlanVersion = 2;  // the shard split's rules (r05: per-class bands), in the plan hash
 constexpr double kMaskedDiagW = 0.65;  // per-a cost of a masked diagonal walk (PSX_K3_MASKW; 1.0 / 1.3 worse, r04aa; 0.65 with DIAGW 0.65 balances world 8 best, r04ae)
 
 // The plan-shaping knobs, read once per process.  PSX_K3_ROUNDS / PSX_K3_DIAG_DIV
@@ -392,7 +393,7 @@ uint64_t plan_knobs_hash() {
         for (size_t i = 0; i < n; i++) h = (h ^ ((const unsigned char*)p)[i]) * 1099511628211ull;
     };
     mix(v, sizeof(v));
-    const int c[3] = {PSX_K3_WAVES, kMaxChunkA3, PSX_KMAX};
+    const int c[4] = {PSX_K3_WAVES, kMaxChunkA3, PSX_KMAX, kPlanVersion};
     mix(c, sizeof(c));
     return h;
 }
@@ -438,9 +439,10 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // so off-diagonal tiles only see a < 64K (every lane active every step) and
     // the triangular pair structure only occurs in diagonal tiles, which walk
     // it folded (psx_sweep3.hip): no in-block masking waste.
-    auto a_work = [&](int K, int C, int a) {
-        return K < C ? 1.0 : ((a >= 64 * K && a < 64 * K + 64) || 64 * K < pad) ? maskw : diagw;
-    };
+    // a diagonal tile's walk of a is masked when a lies inside the block, or in
+    // every walk of block 0 when it holds padding
+    auto masked = [&](int K, int a) { return (a >= 64 * K && a < 64 * K + 64) || 64 * K < pad; };
+    auto a_work = [&](int K, int C, int a) { return K < C ? 1.0 : masked(K, a) ? maskw : diagw; };
     std::vector<PlanUnit> all;
     for (int C = 0; C < nblk; C++) {
         if (64 * C + 64 <= pad) continue;
@@ -462,17 +464,38 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
             }
         }
     }
-    double wsum = 0;
-    for (auto& u : all) wsum += u.work;
-    double lo = wsum * rank / world, hi = wsum * (rank + 1) / world, run = 0;
+    // Contiguous work bands in enumeration order (C, K, a), cut per unit class:
+    // off-diagonal units, diagonal units whose a all walk pipelined, and diagonal
+    // units with a masked walk (a inside the block, or block 0 holding padding).
+    // Each rank takes 1/world of every class, so the split does not depend on the
+    // relative weights of the classes (a single band over all units put most
+    // diagonal tiles, i.e. the low C, on the low ranks: the r04 rehearsal's 5-7 %
+    // per-rank spread at worlds 2 / 4 / 8 came from the diagonal weight).  (Dealing
+    // the units cyclically instead was measured box-dependent, -4 % .. +5 % at world 8.)
+    auto ucls = [&](const PlanUnit& u) {
+        if (u.B < u.T) return 0;
+        for (int a = u.a0; a < u.a1; a++)
+            if (masked(u.B, a)) return 2;
+        return 1;
+    };
     mine.clear();
-    // Contiguous work bands in enumeration order (C, K, a).  (Dealing the units
-    // cyclically instead was measured box-dependent, -4 % .. +5 % at world 8.)
-    for (auto& u : all) {
-        double mid = run + 0.5 * u.work;
-        if (mid >= lo && mid < hi) mine.push_back(u);
-        run += u.work;
+    for (int c = 0; c < 3; c++) {
+        double wsum = 0;
+        for (auto& u : all)
+            if (ucls(u) == c) wsum += u.work;
+        const double lo = wsum * rank / world, hi = wsum * (rank + 1) / world;
+        double run = 0;
+        for (auto& u : all) {
+            if (ucls(u) != c) continue;
+            const double mid = run + 0.5 * u.work;
+            if (mid >= lo && mid < hi) mine.push_back(u);
+            run += u.work;
+        }
     }
+    // (back to enumeration order: the LPT sort below is stable within a weight)
+    std::stable_sort(mine.begin(), mine.end(), [](const PlanUnit& x, const PlanUnit& y) {
+        return x.T != y.T ? x.T < y.T : x.B != y.B ? x.B < y.B : x.a0 < y.a0;
+    });
     double bytes_cls[4][4][4];
     for (int x = 1; x < 4; x++)
         for (int y = 1; y < 4; y++)
@@ -575,7 +598,7 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // ~1/8 of the tile rows — measured neutral (r01y, worlds 1-8) once the next
     // step's tile row is prefetched; not used.)
     // (Splitting the last dispatch rounds into shorter b-walk pieces was
-    // measured +1-6 % slower: a unit's fixed cost is ~11 us)
+    // measured +1-6 % slower: a unit's fixed cost is ~11 us, EXPERIMENTS.md A.)
     return 0;
 }
 

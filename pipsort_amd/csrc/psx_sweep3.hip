@@ -1569,7 +1569,7 @@ __device__ __forceinline__ void sweep3_unit_fast(const Sweep3Args& A, int unit, 
         unsigned long long* tr = A.trace + kTraceWords * (size_t)unit;
         tr[0] = t_start;
         tr[1] = wall_clock64();
-        tr[2] = hw | ((unsigned long long)xcc << 32);
+        tr[2] = hw | ((unsigned long long)xcc << 32) | ((unsigned long long)K << 40) | ((unsigned long long)C << 48);
         tr[3] = (unsigned long long)unit | ((unsigned long long)diag << 32) | ((unsigned long long)(a1 - a0) << 33) |
                 ((unsigned long long)redo << 40);
         for (int i = 0; i < 4; i++) tr[4 + i] = t_ph[i];

@@ -138,7 +138,7 @@ __device__ __forceinline__ void split2(double h, double rP, int& n, double& mu) 
 }
 
 // Record stores (plain stores: non-temporal ones were measured neutral at
-// world 1 and slower at world 8).
+// world 1 and slower at world 8, EXPERIMENTS.md A).
 template <typename T>
 __device__ __forceinline__ void store_rec(T* dst, const T& v) {
     *dst = v;

@@ -12,6 +12,6 @@ for i in $(seq 1 $R); do
     [ "$d" != "$e" ] && envs=${e#*@}
     if [ "$d" = "-" ]; then lib=""; else lib=$PWD/$d/libpipsort_engine.so; fi
     echo "== $e rep $i" >> gpurun_out/ab/abn.txt
-    env PSX_ENGINE_LIB=$lib ${envs//,/ } timeout -k 10 100 python -u tools/shard_rehearsal.py --worlds $W --steps 20 2>&1 | grep "^world" | sed 's/; sweep ms.*//' >> gpurun_out/ab/abn.txt || exit 1
+    env PSX_ENGINE_LIB=$lib ${envs//,/ } timeout -k 10 300 python -u tools/shard_rehearsal.py --worlds $W --steps 20 2>&1 | grep "^world" >> gpurun_out/ab/abn.txt || exit 1
   done
 done

@@ -85,6 +85,29 @@ print("units with 4 a: later-a time per a (us) by start decile:",
       [round(float(((en[i] - ph[i, 3]) / 100.0)[na[i] == 4].mean() / 3.0), 1) if (na[i] == 4).any() else None
        for i in sdec])
 
+# per unit class (off-diagonal / diagonal) and tile: unit-us and a-walks, to
+# check the shard split's cost model (psx_sweep.hip plan_units3c)
+tK = (tr[:, 2] >> 40) & 0xff
+tC = (tr[:, 2] >> 48) & 0xff
+for dflag in (0, 1):
+    m = diag == dflag
+    if m.any():
+        print(f"{'diagonal' if dflag else 'off-diag'}: units {int(m.sum())}, a-walks {int(na[m].sum())}, "
+              f"busy unit-us {dur[m].sum():.0f}, us per a-walk {dur[m].sum() / max(1, na[m].sum()):.2f}")
+m = diag == 0
+if m.any():
+    rows = []
+    for k in sorted(set(tK[m].tolist())):
+        mk = m & (tK == k)
+        rows.append((k, round(float(dur[mk].sum() / na[mk].sum()), 2)))
+    print("off-diag us per a-walk by K:", rows)
+m = diag == 1
+if m.any():
+    rows = []
+    for k in sorted(set(tK[m].tolist())):
+        mk = m & (tK == k)
+        rows.append((k, round(float(dur[mk].sum() / na[mk].sum()), 2)))
+    print("diagonal us per a-walk by K:", rows)
 xcc = (tr[:, 2] >> 32) & 0xf
 print("XCC of unit index (first 16):", xcc[:16].tolist(), "; fraction with XCC == index % 8:",
       round(float((xcc == (np.arange(len(xcc)) % 8)).mean()), 3))
