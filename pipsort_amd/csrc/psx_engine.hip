@@ -463,6 +463,52 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
              mrec ? mrec + (size_t)set * stride : nullptr, score ? score + set : nullptr);
 }
 
+// A user batch (psx_eval_union_batch), one wave per row: the row is validated
+// (its members, the non-negative entries, strictly ascending union indices;
+// else *bad = badv and the row adds nothing: the merges then skip the whole
+// batch and the host reports the error), compacted in place (record j of the
+// set is its j-th member: the merges' keys) and evaluated.  A row without
+// members is the null configuration (sss_postcal.cpp:463-499): set record
+// null1, score L0 (the host adds K, as for every score).
+// The rows are read from `in` and written compacted to `out` (device; may be the
+// same rows); scores and the validity word go to pinned host memory (no readback
+// copy), the word also to `bad` (device) for the merges.
+__global__ __launch_bounds__(64) void k_eval_batch(DevProb P, const int* in, int* out,
+                                                   int stride, SetRec null1, double L0, unsigned long long badv,
+                                                   unsigned long long* __restrict__ bad,
+                                                   unsigned long long* __restrict__ hbad, SetRec* __restrict__ srec,
+                                                   Acc5* __restrict__ mrec, double* __restrict__ score) {
+    __shared__ int row[PSX_KMAX];
+    const int set = blockIdx.x, lane = threadIdx.x;
+    int* S = out + (size_t)set * stride;
+    const int v = lane < stride ? in[(size_t)set * stride + lane] : -1;
+    __builtin_amdgcn_wave_barrier();  // (in may alias out: every lane has read its entry)
+    const unsigned long long m = __ballot(v >= 0);
+    const unsigned long long below = m & ((1ull << lane) - 1ull);
+    const int k = __popcll(m), pos = __popcll(below);
+    const int pl = below ? 63 - __clzll(below) : 0;  // the previous member's lane
+    const int pv = __shfl(v, pl);
+    const bool bad_lane = v >= 0 && (v >= P.U || (below != 0ull && v <= pv));
+    const bool ok = __ballot(bad_lane) == 0ull;
+    if (lane < PSX_KMAX) row[lane] = -1;
+    __builtin_amdgcn_wave_barrier();
+    if (ok && v >= 0) row[pos] = v;
+    __builtin_amdgcn_wave_barrier();
+    if (lane < stride) S[lane] = row[lane];
+    if (!ok || k == 0) {
+        if (lane == 0) {
+            if (!ok) {
+                *bad = badv;
+                *hbad = badv;
+            }
+            srec[set] = ok ? null1 : psx::set_zero();
+            if (score) score[set] = ok ? L0 : 0.0;
+        }
+        return;
+    }
+    eval_set(P, row, stride, nullptr, srec + set, mrec + (size_t)set * stride, score ? score + set : nullptr);
+}
+
 // merge `count` concatenated partial images (rank order) into acc / sacc.
 // Image layout: Acc5[ldg] followed by one Acc5-sized slot holding the SetRec.
 __global__ void k_merge_partials(const Acc5* __restrict__ parts, int U, int ldg, int count, Acc5* __restrict__ acc,
@@ -718,6 +764,7 @@ struct psx_engine {
     psx::PlanScratch gscratch;
     unsigned char* dbm = nullptr;  // chunked batch merge scratch (psx::launch_merge_batch)
     size_t cap_bm = 0;
+    uint32_t batch_seq = 0;        // user batches so far (their validity words)
     int* hstage = nullptr;
     size_t cap_stage = 0;
     hipEvent_t stage_ev = nullptr;  // last upload out of hstage (reuse waits on it)
@@ -901,32 +948,53 @@ int stage_acquire(psx_engine* e, size_t n, int** out) {
 // neighbourhood) merge in two launches (psx::launch_merge_batch); larger ones
 // (generic exhaustive levels) through the records' CSR, built by a device radix
 // sort (psx::csr_from_keys_device).
-constexpr int kBatchChunks = 64;
+constexpr int kBatchChunks = 256;  // psx::k_batch_fold's limit
+SetRec null_rec(const psx_engine* e, double count);
 
-int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool accumulate, double* scores, double* kernel_ms) {
+// user = true: a psx_eval_union_batch slice (rows validated, compacted and
+// null rows handled on the device by k_eval_batch; at most kBatchChunks merge
+// chunks); false: internal sets (canonical rows, k_eval_sets).
+int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool accumulate, double* scores, double* kernel_ms,
+                        bool user = false) {
     if (nsets == 0) return 0;
     if (stride > PSX_KMAX) return fail(PSX_ERANGE, "union set larger than PSX_KMAX");
     int rc;
     const size_t n_sets = nsets * stride;
     const bool chunked = accumulate && psx::batch_merge_chunks((long)nsets, stride) <= kBatchChunks && e->U <= 131072;
+    if (user && accumulate && !chunked) return fail(PSX_EINVAL, "internal: user batch slice beyond the chunked merge");
+    // the batch's validity word: after the scores (user batches), a 64-bit
+    // pattern unique to this call
+    const unsigned long long badv = ((unsigned long long)(++e->batch_seq) << 32) | 0xBADBA7C4ull;
     if ((rc = ensure(e->dgen, e->cap_gen, n_sets))) return rc;
     if ((rc = ensure(e->dsrec, e->cap_srec, nsets))) return rc;
     if ((rc = ensure(e->dmrec, e->cap_mrec, n_sets))) return rc;
-    if (scores && (rc = ensure(e->dscore, e->cap_score, nsets))) return rc;
+    if (!user && scores && (rc = ensure(e->dscore, e->cap_score, nsets))) return rc;
+    if (user && (rc = ensure_host(e->hscore, e->cap_hscore, nsets + 1))) return rc;
+    // (user batches) the validity word: device status slot words 10-11 for the
+    // merges, pinned hscore[nsets] for the host
+    unsigned long long* dbad = user ? reinterpret_cast<unsigned long long*>(e->dflag + 10) : nullptr;
     if (chunked && (rc = ensure(e->dbm, e->cap_bm, psx::batch_merge_bytes((long)nsets, stride, e->U)))) return rc;
     if (accumulate && !chunked && (rc = ensure(e->dgcsr, e->cap_gcsr, (size_t)e->U + 1 + n_sets))) return rc;
+    // the rows: one upload out of the pinned staging buffer (a kernel reading
+    // them from host memory measured 36 -> 55 us, r05w)
     HIPCHK(hipMemcpyAsync(e->dgen, e->hstage, n_sets * sizeof(int), hipMemcpyHostToDevice, e->stream));
     if (!e->stage_ev) HIPCHK(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
     HIPCHK(hipEventRecord(e->stage_ev, e->stream));
     e->stage_rec = true;
     if (kernel_ms) HIPCHK(hipEventRecord(e->ev[2], e->stream));
-    hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)nsets), dim3(64), 0, e->stream, e->dp, e->dgen, stride, nullptr,
-                       e->dsrec, e->dmrec, scores ? e->dscore : nullptr);
+    if (user)
+        hipLaunchKernelGGL(k_eval_batch, dim3((unsigned)nsets), dim3(64), 0, e->stream, e->dp, e->dgen, e->dgen,
+                           stride, null_rec(e, 1.0), e->L0, badv, dbad,
+                           reinterpret_cast<unsigned long long*>(e->hscore + nsets), e->dsrec, e->dmrec,
+                           scores ? e->hscore : nullptr);
+    else
+        hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)nsets), dim3(64), 0, e->stream, e->dp, e->dgen, stride,
+                           nullptr, e->dsrec, e->dmrec, scores ? e->dscore : nullptr);
     HIPCHK(hipGetLastError());
     if (kernel_ms) HIPCHK(hipEventRecord(e->ev[3], e->stream));
     if (chunked) {
         if (psx::launch_merge_batch(e->dgen, stride, (long)nsets, e->U, e->dmrec, e->dsrec, e->dbm, e->dacc,
-                                    e->dsacc, e->stream))
+                                    e->dsacc, e->stream, dbad, badv))
             return fail(PSX_EHIP, "set-batch merge failed");
     } else if (accumulate) {
         int* dptr = e->dgcsr;
@@ -939,12 +1007,14 @@ int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool accumulate
         if (psx::launch_merge_sets(e->dsrec, (long)nsets, none, e->dsacc, e->stream))
             return fail(PSX_EHIP, psx::sweep_error());
     }
-    if (scores) {
+    if (scores && !user) {
         if ((rc = ensure_host(e->hscore, e->cap_hscore, nsets))) return rc;
         HIPCHK(hipMemcpyAsync(e->hscore, e->dscore, nsets * sizeof(double), hipMemcpyDeviceToHost, e->stream));
     }
-    if (!scores && !kernel_ms) return 0;
+    if (!scores && !kernel_ms && !user) return 0;
     HIPCHK(hipStreamSynchronize(e->stream));
+    if (user && *reinterpret_cast<const unsigned long long*>(e->hscore + nsets) == badv)
+        return fail(PSX_EINVAL, "sets must be ascending union indices");
     if (scores)
         for (size_t i = 0; i < nsets; i++) scores[i] = e->K + e->hscore[i];
     if (kernel_ms) {
@@ -1978,58 +2048,33 @@ int psx_eval_union_batch(psx_engine* e, const int32_t* sets, int32_t stride, int
     HIPCHK(hipSetDevice(e->dev));
     const auto t0 = std::chrono::steady_clock::now();
     if (stride < 1 || stride > PSX_KMAX) return fail(PSX_ERANGE, "stride outside [1, 6]");
-    // the empty set is the null configuration (sss_postcal.cpp:463-499): host
-    // side.  The other sets are validated and written compacted (members first,
-    // -1 after them: record j of a set is its j-th member) straight into the
-    // pinned staging buffer, in one pass.
+    if (n_sets < 0 || (n_sets > 0 && !sets)) return fail(PSX_EINVAL, "bad set batch");
+    // Rows go to the device as given (one pinned copy per slice); k_eval_batch
+    // validates and compacts them and evaluates the null rows.  Slices of at
+    // most kBatchChunks merge chunks (an SSS neighbourhood is one slice).
+    std::memset(&e->timing, 0, sizeof(e->timing));
+    const size_t per = (size_t)kBatchChunks * (size_t)(512 / stride);
+    double kms = 0, prep = 0;
     int rc;
-    int* h = nullptr;
-    if (n_sets > 0 && (rc = stage_acquire(e, (size_t)n_sets * stride, &h))) return rc;
-    std::vector<int> where;  // batch position -> row (only when some row is empty)
-    size_t nb = 0;
-    double nulls = 0;
-    for (int i = 0; i < n_sets; i++) {
-        const int* s = sets + (size_t)i * stride;
-        int* o = h + nb * stride;
-        int prev = -1, k = 0;
-        for (int j = 0; j < stride; j++) {
-            const int v = s[j];
-            if (v < 0) continue;
-            if (v <= prev || v >= e->U) return fail(PSX_EINVAL, "sets must be ascending union indices");
-            prev = o[k++] = v;
-        }
-        if (k == 0) {
-            if (where.empty())
-                for (size_t q = 0; q < nb; q++) where.push_back((int)q);
-            nulls += 1;
-            if (score_out) score_out[i] = e->K + e->L0;
-            continue;
-        }
-        for (int j = k; j < stride; j++) o[j] = -1;
-        if (nulls > 0) where.push_back(i);
-        nb++;
+    for (size_t s0 = 0; s0 < (size_t)n_sets; s0 += per) {
+        const size_t nb = std::min(per, (size_t)n_sets - s0);
+        const auto ts = std::chrono::steady_clock::now();
+        int* h = nullptr;
+        if ((rc = stage_acquire(e, nb * stride, &h))) return rc;
+        std::memcpy(h, sets + s0 * stride, nb * stride * sizeof(int));
+        prep += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
+        if ((rc = eval_generic_staged(e, stride, nb, accumulate != 0, score_out ? score_out + s0 : nullptr, &kms,
+                                      true)))
+            return rc;
     }
-    const auto t1 = std::chrono::steady_clock::now();
-    if (nb > 0) {
-        // scores straight into score_out when no row was empty
-        std::vector<double> sc(score_out && nulls > 0 ? nb : 0);
-        double* so = score_out ? (nulls > 0 ? sc.data() : score_out) : nullptr;
-        double kms = 0;
-        if ((rc = eval_generic_staged(e, stride, nb, accumulate != 0, so, &kms))) return rc;
-        if (score_out && nulls > 0)
-            for (size_t i = 0; i < nb; i++) score_out[where[i]] = sc[i];
-        // the batch's k_eval_sets launch (HIP events around it on e->stream)
-        std::memset(&e->timing, 0, sizeof(e->timing));
-        e->timing.kernel_ms = kms;
-        e->timing.kernel_launches = 1;
-        e->timing.union_sets = nb;
-    }
-    if (accumulate && nulls > 0 && (rc = fold_null(e, nulls))) return rc;
     HIPCHK(hipStreamSynchronize(e->stream));
-    // host walls: validation + staging, the whole call
-    using ms = std::chrono::duration<double, std::milli>;
-    e->timing.prepare_ms = ms(t1 - t0).count();
-    e->timing.run_ms = ms(std::chrono::steady_clock::now() - t0).count();
+    // the batch's k_eval_batch launches (HIP events around them on e->stream)
+    // and the host walls: the staging copies, the whole call
+    e->timing.kernel_ms = kms;
+    e->timing.kernel_launches = n_sets > 0 ? (int32_t)(((size_t)n_sets + per - 1) / per) : 0;
+    e->timing.union_sets = (uint64_t)n_sets;
+    e->timing.prepare_ms = prep;
+    e->timing.run_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return 0;
 }
 

@@ -133,19 +133,19 @@ int csr_from_keys_device(const int* d_keys, long n, int U, int* d_dptr, int* d_g
 // records of n union sets ([set][stride], record j of a set = its j-th member)
 // into the per-SNP accumulators and the set records into the scalars, in two
 // launches and a fixed order, without a device-wide sort.
-//   k_batch_part  chunk c = 2048 records of whole sets: a block radix-sorts the
+//   k_batch_part  chunk c = 512 records of whole sets: a wave radix-sorts the
 //                 chunk's (SNP, record) pairs in LDS; each thread folds the runs
 //                 of its 8 sorted positions, a fixed binary tree over the
 //                 threads joins the runs that cross threads; every SNP's chunk
 //                 total goes to part[c][u] + a presence bit, the chunk's set
 //                 records to spart[c]
-//   k_batch_fold  a wave per SNP u folds part[0..nc)[u] (present ones, nc <= 64)
+//   k_batch_fold  a wave per SNP u folds part[0..nc)[u] (present ones, nc <= 256)
 //                 by a fixed shuffle tree into acc[u]; one wave folds
 //                 spart[0..nc) into the scalars
 // ---------------------------------------------------------------------------
 namespace {
 
-constexpr int kBT = 256, kBI = 8;
+constexpr int kBT = 64, kBI = 8;  // a chunk: one wave, 512 records (more chunks in flight, no cross-wave sort)
 constexpr int kBWords = 4096;  // presence bitmap words in LDS: U <= 131072
 
 // A run of equal SNPs over a range of sorted positions: the first and last runs
@@ -159,7 +159,10 @@ struct BRange {
 __global__ __launch_bounds__(kBT) void k_batch_part(const int* __restrict__ sets, int stride, long nsets, int spc,
                                                    int U, int end_bit, const Acc5* __restrict__ rec,
                                                    const SetRec* __restrict__ srec, Acc5* __restrict__ part,
-                                                   unsigned* __restrict__ bits, int words, SetRec* __restrict__ spart) {
+                                                   unsigned* __restrict__ bits, int words, SetRec* __restrict__ spart,
+                                                   const unsigned long long* __restrict__ bad,
+                                                   unsigned long long badv) {
+    if (bad && *bad == badv) return;  // an invalid row: the batch adds nothing (uniform)
     using Sort = hipcub::BlockRadixSort<int, kBT, kBI, int>;
     __shared__ union {
         typename Sort::TempStorage sort;
@@ -264,18 +267,29 @@ __global__ __launch_bounds__(kBT) void k_batch_part(const int* __restrict__ sets
     }
 }
 
-// a wave per SNP: lane c takes chunk c's partial (nc <= 64), a fixed shuffle
-// tree folds them, lane 0 folds the result into acc[u]
+// a wave per SNP: lane l folds chunks l, l + 64, l + 128, l + 192 (the present
+// ones, nc <= 256) in that order, a fixed shuffle tree folds the lanes, lane 0
+// folds the result into acc[u]
 __global__ __launch_bounds__(256) void k_batch_fold(const Acc5* __restrict__ part, const unsigned* __restrict__ bits,
                                                    int words, int nc, int U, const SetRec* __restrict__ spart,
-                                                   Acc5* __restrict__ acc, SetRec* __restrict__ sacc) {
+                                                   Acc5* __restrict__ acc, SetRec* __restrict__ sacc,
+                                                   const unsigned long long* __restrict__ bad,
+                                                   unsigned long long badv) {
+    if (bad && *bad == badv) return;
     const int lane = threadIdx.x & 63;
     const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (u < U) {
-        const bool have = lane < nc && ((bits[(size_t)lane * words + (u >> 5)] >> (u & 31)) & 1u);
-        Acc5 g = have ? part[(size_t)lane * U + u] : acc_zero();
-        const unsigned long long any = __ballot(have);
-        if (any) {
+        Acc5 g = acc_zero();
+        bool have = false;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int c = lane + 64 * r;
+            if (c < nc && ((bits[(size_t)c * words + (u >> 5)] >> (u & 31)) & 1u)) {
+                fold_acc(g, part[(size_t)c * U + u]);
+                have = true;
+            }
+        }
+        if (__ballot(have)) {
             wave_fold_acc(g);
             if (lane == 0) {
                 Acc5 a = acc[u];
@@ -284,15 +298,14 @@ __global__ __launch_bounds__(256) void k_batch_fold(const Acc5* __restrict__ par
             }
         }
     }
-    if (blockIdx.x == 0) {
-        SetRec s = threadIdx.x < nc ? spart[threadIdx.x] : set_zero();
-        if (threadIdx.x < 64) {
-            wave_fold_set(s);
-            if (threadIdx.x == 0) {
-                SetRec g = *sacc;
-                fold_set(g, s);
-                *sacc = g;
-            }
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        SetRec s = set_zero();
+        for (int c = threadIdx.x; c < nc; c += 64) fold_set(s, spart[c]);
+        wave_fold_set(s);
+        if (threadIdx.x == 0) {
+            SetRec g = *sacc;
+            fold_set(g, s);
+            *sacc = g;
         }
     }
 }
@@ -310,7 +323,8 @@ size_t batch_merge_bytes(long nsets, int stride, int U) {
 }
 
 int launch_merge_batch(const int* d_sets, int stride, long nsets, int U, const Acc5* rec, const SetRec* srec,
-                       void* scratch, Acc5* acc, SetRec* sacc, hipStream_t st) {
+                       void* scratch, Acc5* acc, SetRec* sacc, hipStream_t st, const unsigned long long* bad,
+                       unsigned long long badv) {
     if (nsets <= 0) return 0;
     const int words = (U + 31) / 32;
     if (words > kBWords || stride < 1 || stride > kBT * kBI) return -1;
@@ -321,10 +335,10 @@ int launch_merge_batch(const int* d_sets, int stride, long nsets, int U, const A
     SetRec* spart = (SetRec*)(part + (size_t)nc * U);
     unsigned* bits = (unsigned*)(spart + nc);
     hipLaunchKernelGGL(k_batch_part, dim3(nc), dim3(kBT), 0, st, d_sets, stride, nsets, spc, U, end_bit, rec, srec,
-                       part, bits, words, spart);
+                       part, bits, words, spart, bad, badv);
     if (chk(hipGetLastError())) return -1;
     hipLaunchKernelGGL(k_batch_fold, dim3((U + 3) / 4), dim3(256), 0, st, part, bits, words, nc, U, spart, acc,
-                       sacc);
+                       sacc, bad, badv);
     return chk(hipGetLastError());
 }
 

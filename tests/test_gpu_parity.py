@@ -423,6 +423,28 @@ def test_union_batch_merge_routes(gpu):
         assert np.array_equal(getattr(y, f), getattr(z2, f)), f
 
 
+@pytest.mark.parametrize("row", [[5, 3, -1], [2, 2, -1], [0, 90, -1], [-1, 7, 7]])
+def test_union_batch_rejects_bad_rows(gpu, row):
+    """Rows are validated on the device (k_eval_batch): a row whose members are
+    not strictly ascending union indices fails the whole call with EINVAL and
+    adds nothing to the accumulators; the handle stays usable."""
+    ld, z, _, _, u2l = synth.syn_v1(90)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    pc = E.PostCal(seam)
+    good = np.array([[1, 4, -1], [0, 2, 3], [-1, -1, -1]], dtype=np.int32)
+    s0 = pc.eval_union_batch(good, accumulate=True)
+    before = pc.accum()
+    bad = np.concatenate([good, np.array([row], dtype=np.int32), good])
+    with pytest.raises(E.EngineError) as ei:
+        pc.eval_union_batch(bad, accumulate=True)
+    assert ei.value.code == E.PSX_EINVAL
+    after = pc.accum()
+    for f in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+        assert np.array_equal(getattr(before, f), getattr(after, f)), f
+    assert before.total == after.total and before.n_configs == after.n_configs
+    assert np.array_equal(pc.eval_union_batch(good, accumulate=False), s0)
+
+
 def test_union_batch_padding_anywhere(gpu):
     """-1 padding may sit between members (the batch only asks ascending
     members): the records of such a row fold into the same SNPs, bitwise equal

@@ -31,6 +31,9 @@ pc.set_shard(a.rank, a.world)
 nb = pc.partials_bytes()
 mine = torch.empty(nb, dtype=torch.uint8, device="cuda")
 gathered = torch.empty(nb * a.world, dtype=torch.uint8, device="cuda")
+# the copies stand in for ranks 0..world-1: their plan tags get those ranks
+tag_rank = (nb // 56 - 1) * 56 + 8
+rank_bytes = torch.arange(a.world, dtype=torch.int32, device="cuda").view(torch.uint8).view(a.world, 4)
 
 
 def step():
@@ -38,6 +41,7 @@ def step():
     if a.world > 1:
         pc.export_partials(mine.data_ptr())
         gathered.view(a.world, nb).copy_(mine.view(1, nb).expand(a.world, nb))
+        gathered.view(a.world, nb)[:, tag_rank:tag_rank + 4].copy_(rank_bytes)
         pc.merge_partials(gathered.data_ptr(), a.world)
 
 
