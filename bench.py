@@ -328,7 +328,7 @@ def sss_probe(reps=20):
     kms = []
     for _ in range(reps):
         pc.eval_union_batch(arr, accumulate=True)
-        kms.append(pc.timing()["kernel_ms"])  # the batch's k_eval_sets launch (HIP events)
+        kms.append(pc.timing()["kernel_ms"])  # the batch's k_eval_batch launch (HIP events)
     batch_ms = (time.perf_counter() - t0) * 1e3 / reps
     pc.close()
     roof = sss_roofline(len(sets), npat, sum(kms) / len(kms))
@@ -341,12 +341,12 @@ def sss_probe(reps=20):
 
 
 def sss_roofline(n_sets, npat, kernel_ms):
-    """The batch's dominant kernel, k_eval_sets (a wave per union set: 2^k
+    """The batch's dominant kernel, k_eval_batch (a wave per union set: 2^k
     subset LDL^T per study, then the 3^k assignments), is FP64 VALU work:
     achieved = FP64 operations of one launch (PMC SQ_INSTS_VALU_FLOPS_FP64 x 64
     of this very build and batch shape, profiles/pmc_latest.json "sss_eval") /
     its launch duration measured here (HIP events around the launch)."""
-    out = {"bound": "valu_fp64", "kernel": "k_eval_sets", "kernel_ms": kernel_ms, "peak": FP64_PEAK_TFLOPS,
+    out = {"bound": "valu_fp64", "kernel": "k_eval_batch", "kernel_ms": kernel_ms, "peak": FP64_PEAK_TFLOPS,
            "unit": "TFLOP/s", "kernel_configs_per_s": npat / (kernel_ms / 1e3) if kernel_ms > 0 else None,
            "duration_source": "HIP events around the launch on the engine stream (psx_get_timing), mean of reps",
            "achieved": None, "frac": None, "eval_src_sha": eval_src_sha()}
@@ -448,7 +448,8 @@ def configs_probe(reps=3):
     return {"workload": "SYN-v1 M=1000 -c 3, -b file of 3 x 12-SNP groups per study (construct_configs_all_studies)",
             "rows": int(rows.shape[0]), "n_groups": int(rows.shape[1]), "configs_checked": int(n),
             "wall_ms": dt * 1e3, "configs_per_s": rows.shape[0] / dt, "kernel_ms": tm["kernel_ms"],
-            "note": "host rows -> parallel preprocessing -> one upload -> k_eval_sets + merges; best of %d" % reps}
+            "note": "rows -> one upload -> the device row walk (validation, index maps, evaluation: psx_configs.hip) "
+                    "+ merges; best of %d" % reps}
 
 
 def torch_allgather(backend):
@@ -590,7 +591,7 @@ EVAL_SOURCES = ("psx_engine.hip", "psx_wave.h", "psx_math.h", "psx_sweep_dev.h")
 
 
 def eval_src_sha():
-    """Hash of the sources k_eval_sets (the SSS batch evaluator) is built from."""
+    """Hash of the sources k_eval_batch (the SSS batch evaluator) is built from."""
     import hashlib
     h = hashlib.sha256()
     for f in EVAL_SOURCES:

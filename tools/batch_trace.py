@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Time the SSS proposal batch (bench.sss_batch, BASELINE configs[4] M = 2000)
 through psx_eval_union_batch: REPS calls after a warm call, wall per call and
-the k_eval_sets launch; run under rocprofv3 --kernel-trace --hip-runtime-trace
+the k_eval_batch launch; run under rocprofv3 --kernel-trace --hip-runtime-trace
 for the timeline (tools/trace_summary.py).  usage: tools/batch_trace.py [REPS]"""
 import os
 import sys
@@ -33,5 +33,5 @@ for acc in (True, False):
     m = lambda v: sum(v) / len(v)  # noqa: E731
     print(f"accumulate={acc}: wall median {w[len(w) // 2]:.4f} ms min {w[0]:.4f} ms, "
           f"in the call {m(run):.4f} ms (validate + stage {m(prep):.4f} ms), "
-          f"k_eval_sets {m(k):.4f} ms, {len(arr)} sets, {npat} configs")
+          f"k_eval_batch {m(k):.4f} ms, {len(arr)} sets, {npat} configs")
 pc.close()

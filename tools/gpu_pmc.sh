@@ -17,7 +17,7 @@ i=0
 while read -r GROUP; do
     [ -z "$GROUP" ] && continue
     i=$((i + 1))
-    timeout -k 10 300 rocprofv3 --pmc $GROUP --kernel-include-regex 'k_sweep|k_merge|k_eval_sets' --output-format csv \
+    timeout -k 10 300 rocprofv3 --pmc $GROUP --kernel-include-regex 'k_sweep|k_merge|k_eval_batch' --output-format csv \
         -d "$OUT/p$i" -o run -- $CMD > "$OUT/p$i.log" 2>&1
     rc=$?
     echo "pass $i [$GROUP] rc=$rc" >> "$OUT/status.txt"

@@ -55,13 +55,13 @@ if "SQ_INSTS_VALU" in c and "GRBM_GUI_ACTIVE" in c:
 for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
     if k in c and "SQ_WAVE_CYCLES" in c:
         out[k.lower() + "_frac"] = c[k] / c["SQ_WAVE_CYCLES"]
-# the SSS proposal batch's evaluator (bench.py sss_probe: one k_eval_sets
-# launch over the whole neighbourhood): the largest-grid k_eval_sets dispatches
+# the SSS proposal batch's evaluator (bench.py sss_probe: one k_eval_batch
+# launch over the whole neighbourhood): the largest-grid k_eval_batch dispatches
 ev = collections.defaultdict(float)
 grids = {}
 for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
-        if "k_eval_sets" not in r["Kernel_Name"]:
+        if "k_eval_batch" not in r["Kernel_Name"]:
             continue
         key = (os.path.basename(os.path.dirname(f)), r["Counter_Name"], r["Dispatch_Id"])
         ev[key] += float(r["Counter_Value"])
@@ -73,7 +73,7 @@ if ev:
         if grids[disp] == gmax:
             per_ev[cn].append(v)
     ce = {k: sum(v) / len(v) for k, v in per_ev.items()}
-    out["sss_eval"] = {"kernel": "k_eval_sets", "grid_size": gmax, "eval_src_sha": bench.eval_src_sha(),
+    out["sss_eval"] = {"kernel": "k_eval_batch", "grid_size": gmax, "eval_src_sha": bench.eval_src_sha(),
                        "counters_per_dispatch": ce}
     if "SQ_INSTS_VALU_FLOPS_FP64" in ce:
         out["sss_eval"]["fp64_flop_insts_per_launch"] = ce["SQ_INSTS_VALU_FLOPS_FP64"]
