@@ -483,6 +483,40 @@ def test_deterministic_and_reusable(gpu):
     assert a.total == b.total
 
 
+def test_generic_level_chunked_vs_cached(gpu):
+    """A generic level above 4M sets per shard runs in chunks of 2^20 sets
+    (run_level_generic: staged rows, k_eval_sets, the records merged through
+    the device radix-sorted CSR); at or below it the level is enqueued whole
+    (enqueue_generic_level, its CSR built once and cached).  U = 120,
+    c = 4: level 4 has 8.2M sets, so one handle takes the chunked route and two
+    shards (4.1M sets each) the cached one; the merged accumulators agree to
+    fold-order rounding."""
+    import torch  # noqa: F401  (device buffers for the partial images)
+    ld, z, _, _, u2l = synth.syn_v1(120)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=4, sharing_param=0.25)
+    one = E.PostCal(seam)
+    one.run_exhaustive()
+    a = one.accum()
+    nb = one.partials_bytes()
+    buf = torch.empty(2 * nb, dtype=torch.uint8, device="cuda")
+    for r in range(2):
+        pc = E.PostCal(seam)
+        pc.set_shard(r, 2)
+        pc.run_exhaustive()
+        pc.export_partials(buf.data_ptr() + r * nb)
+        pc.close()
+    torch.cuda.synchronize()
+    m = E.PostCal(seam)
+    m.merge_partials(buf.data_ptr(), 2)
+    b = m.accum()
+    assert a.n_configs == b.n_configs == seam.count_configs()
+    assert abs(a.total - b.total) <= 1e-12 * abs(a.total)
+    for f in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+        x, y = getattr(a, f), getattr(b, f)
+        assert np.array_equal(x == 0, y == 0), f
+        np.testing.assert_allclose(x, y, rtol=1e-11, atol=0, err_msg=f)
+
+
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_shard_merge_equals_single(gpu, world):
     """Config-shard + merge of partials (the multi-GPU exchange) reproduces the
