@@ -43,7 +43,7 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (spec)
 SIMDS = 256 * 4
 CLOCK_HZ = 2.4e9          # peak engine clock (spec)
 # SIMD cycles per wave64 VALU instruction on gfx950, measured by tools/valu_lat.hip
-# with 4 waves per SIMD, 8 independent chains each (profiles/r03a_valu_issue.txt):
+# with 4 waves per SIMD, 8 independent chains each (profiles/archive/r03a_valu_issue.txt):
 # FP64 FMA / MUL / ADD and v_ldexp_f64 4.2 (the 16-lane FP64 pipe), v_rsq_f64
 # 16.15, 32-bit integer / f32 ops 2.28 (the 32-lane pipe: half the FP64 cost)
 VALU_CYCLES = {"fp64": 4.20, "fp64_trans": 16.15, "int32": 2.28, "other": 4.20}
@@ -72,7 +72,7 @@ def valu_issue_roof(pmc, kernel_s, world):
            "mix_per_launch": {"fp64": fp64 / world, "fp64_trans": trans / world, "int32": int32 / world,
                               "other": other / world},
            "source": "PMC instruction classes (profiles/pmc_latest.json) x cycles per instruction measured by "
-                     "tools/valu_lat.hip (profiles/r03a_valu_issue.txt) / (1024 SIMDs x kernel_ms)"}
+                     "tools/valu_lat.hip (profiles/archive/r03a_valu_issue.txt) / (1024 SIMDs x kernel_ms)"}
     if pmc.get("gpu_cycles_per_launch") and world == 1:
         out["frac_at_measured_clock"] = cyc / SIMDS / pmc["gpu_cycles_per_launch"]
     return out

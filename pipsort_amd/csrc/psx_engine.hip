@@ -2662,7 +2662,7 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
         auto tp = std::chrono::steady_clock::now();
         // plain event records around the eval (the stop event is what the host
         // waits on): hipExtLaunchKernelGGL's in-packet events cost the host ~12 us
-        // more per launch here (profiles/r03i_sss_host_phases.txt)
+        // more per launch here (profiles/archive/r03i_sss_host_phases.txt)
         // The start event only on every kEvEvery-th iteration (an event record is
         // ~1-2 us of host time): the eval time is sampled there and scaled to all
         // iterations; the stop event (the host's wait) on every one.
@@ -2746,7 +2746,7 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
             pr.resize((size_t)(en - b));
             double mx = *std::max_element(lk + b, lk + en);
             // (slicing these exps over spinning host threads measured slower: the
-            // serial loop takes ~5 us at 1,000 neighbours, profiles/r03v_sss_threads.txt)
+            // serial loop takes ~5 us at 1,000 neighbours, profiles/archive/r03v_sss_threads.txt)
             for (int ii = b; ii < en; ii++) pr[ii - b] = std::exp(lk[ii] - mx);
             std::discrete_distribution<size_t> dist(pr.begin(), pr.end());
             smp = dist(gen);

@@ -58,7 +58,7 @@ struct SweepStats {           // indexed by causal-set level k
 // buffers of pass i - kRecBufs, so the host may run kRecBufs - 1 passes ahead of
 // the device before it blocks.  Each set is one plan's records (~90 MB at
 // M = 1000, c = 3).  12 sets (a longer lead against host stalls) measured 3 %
-// slower at world 8 than 3 on the same box (profiles/r02zf_ab_*): 3.
+// slower at world 8 than 3 on the same box (profiles/archive/r02zf_ab_*): 3.
 #ifndef PSX_REC_BUFS
 #define PSX_REC_BUFS 3
 #endif

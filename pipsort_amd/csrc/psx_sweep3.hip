@@ -307,7 +307,7 @@ __global__ void k_build_bc3(Sweep3Args A, double2* __restrict__ mu01, int2* __re
 // is held in registers.  (Three waves per SIMD, <= 13,312 bytes per block and 168
 // VGPRs, were measured 17 % slower: the walk state left no registers for the
 // per-a state, which the compiler parked in scratch behind dependent waits,
-// profiles/r03d_k3_three_waves_rejected.txt.)
+// profiles/archive/r03d_k3_three_waves_rejected.txt.)
 //
 // LDS of a k = 3 unit, ROBUST variant: (a, b) terms (per a), indexed [study][b
 // slot], the exp2 table and the rotating b-slot accumulators

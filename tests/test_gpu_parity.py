@@ -31,7 +31,7 @@ BIG_LOCUS = 10_000_000  # configurations: above this the reference's normaliser 
 def assert_parity(got: E.Accumulators, ref: dict, pip_tol=1e-9, ll_rtol=1e-10):
     """Engine vs oracle.  Above BIG_LOCUS configurations the reference's serial
     addlogSpace accumulation of the normaliser (postcal.h:102-112, restated by
-    the oracle) drifts by up to ~2e-7 log units (profiles/r01w_total_drift.txt:
+    the oracle) drifts by up to ~2e-7 log units (profiles/archive/r01w_total_drift.txt:
     the engine matches an exact fsum of the oracle's own per-configuration L to
     4e-12), which scales every PIP: there PIPs are held to the north star's
     1e-6 and the per-SNP log accumulators themselves to 1e-9 relative."""
@@ -301,7 +301,7 @@ def test_mixed_membership_loci(gpu, M0, M1, shared, c):
     log-space accumulation of the normaliser (addlogSpace, postcal.h:102-112,
     restated by the oracle) drifts by 1.9e-7 log units, while the engine's
     total matches an exact fsum of the oracle's own per-configuration values
-    to 4e-12 (profiles/r01w_total_drift.txt).  Every PIP then differs by that
+    to 4e-12 (profiles/archive/r01w_total_drift.txt).  Every PIP then differs by that
     factor, so this case is held to the north star's 1e-6 and its per-SNP log
     accumulators to 1e-9 relative (they agree to 1e-13); assert_parity applies
     that rule to every locus above BIG_LOCUS configurations."""

@@ -13,7 +13,7 @@
 // 4-cycle pipe occupancy (the cost model of bench.py's roofline.valu_issue).
 //
 // Round-1 numbers (r01y): dependent v_fma_f64 5.75 cycles, v_add_f64 7.5,
-// v_rsq_f64 ~18; independent FP64 4.3.  Round-3 table: profiles/r03*_valu_issue.txt.
+// v_rsq_f64 ~18; independent FP64 4.3.  Round-3 table: profiles/archive/r03*_valu_issue.txt.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
