@@ -860,6 +860,9 @@ def main():
             "setup": {"synthetic_locus_s": t_synth, "gpu_model_setup_and_create_ms": pc.setup_info["setup_ms"],
                       "psd_added": pc.setup_info["psd_added"], "eigen_route": pc.setup_info["eigen_route"]},
             "pass_mode": "async (no host sync per step)" if use_async else "synchronous",
+            # CUs kept for the merges / exchange beside overlapped passes (one XCD
+            # at world >= 8 by default, PSX_OVERLAP overrides; 0: not overlapped)
+            "overlap_reserved_cus": pc.overlap_cus(),
             "span_ms_per_pass": tm.get("span_ms") if use_async else None,
             "configs_checked": int(acc.n_configs) if acc is not None else None,
             "plan_hash": f"{plan_hash:016x}",

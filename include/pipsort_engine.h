@@ -89,6 +89,12 @@ typedef struct {
 int32_t psx_abi_version(void);
 const char *psx_last_error(void);
 
+/* CUs reserved for the merges / exchange beside overlapped asynchronous passes,
+ * decided at the handle's first psx_run_exhaustive_async (-1 before it): one
+ * XCD's CUs at world >= 8, 0 below; the environment variable PSX_OVERLAP = n
+ * overrides.  (No reference counterpart: reported by bench.py.) */
+int32_t psx_overlap_cus(const psx_engine *e);
+
 /* Number of HIP devices visible (0 on a host without a GPU; never initialises a context). */
 int psx_device_count(int *count);
 

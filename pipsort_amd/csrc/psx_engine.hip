@@ -1343,15 +1343,18 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     int par = 0;
     if (async) {
         if (!e->cstream) {
-            // reserved CUs for overlapped sweeps (PSX_OVERLAP = n, opt-in), decided
-            // at the handle's first asynchronous pass.  Measured (EXPERIMENTS.md C):
-            // worlds 4 / 8 -2 .. -5 % on some boxes, neutral on others, world 1
-            // +2 %; rebuilding the streams when a handle's world changed was
-            // 20-25 % slower (r04u), so it is not switched per world.
-            const char* ovl_env = getenv("PSX_OVERLAP");
-            e->ovl = ovl_env ? std::max(0, atoi(ovl_env)) : 0;
+            // reserved CUs for overlapped sweeps, decided at the handle's first
+            // asynchronous pass (rebuilding the streams when a handle's world
+            // changed was 20-25 % slower, r04u).  Default: one XCD's CUs (32 of
+            // MI355X's 256) at world >= 8, none below; PSX_OVERLAP = n overrides.
+            // Measured on one box, alternating rounds (profiles/r05zi_*, r05zj_*):
+            // world 8 step 0.132 -> 0.112 ms with 32 (16 / 24 / 48 / 64: 0.12-0.127,
+            // a whole XCD for the merges and the exchange is the sweet spot);
+            // worlds 2 and 4 are 2-7 % slower with any reservation.
             int ncu = 0;
             HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->dev));
+            const char* ovl_env = getenv("PSX_OVERLAP");
+            e->ovl = ovl_env ? std::max(0, atoi(ovl_env)) : (e->world >= 8 ? ncu / 8 : 0);
             if (e->ovl > 0 && e->ovl < ncu) {
                 // Two compute streams on their own queues, masked off e->ovl CUs
                 // (bits ncu - 1 - k * stride, PSX_RESERVE_STRIDE, default 1):
@@ -1468,6 +1471,7 @@ int fill_timing(psx_engine* e, double gms, int flag);
 extern "C" {
 
 int32_t psx_abi_version(void) { return PSX_ABI_VERSION; }
+int32_t psx_overlap_cus(const psx_engine* e) { return e ? e->ovl : -1; }
 const char* psx_last_error(void) { return g_err.c_str(); }
 
 int psx_device_count(int* count) {

@@ -31,7 +31,7 @@ PSX_EEXCHANGE = -7
 
 # Every symbol declared in include/pipsort_engine.h and include/pipsort_model.h
 EXPORTED = [
-    "psx_abi_version", "psx_last_error", "psx_device_count", "psx_warmup", "psx_warmup_for", "psx_create", "psx_destroy",
+    "psx_abi_version", "psx_overlap_cus", "psx_last_error", "psx_device_count", "psx_warmup", "psx_warmup_for", "psx_create", "psx_destroy",
     "psx_set_shard", "psx_run_exhaustive", "psx_run_configs", "psx_run_sss",
     "psx_eval_union_batch", "psx_reset", "psx_get_accum", "psx_partials_bytes",
     "psx_export_partials", "psx_merge_partials", "psx_get_timing", "psx_count_configs",
@@ -162,6 +162,7 @@ def load_library(path: str = LIB_PATH):
     vp = ctypes.c_void_p
     sig = {
         "psx_abi_version": (c_i32, []),
+        "psx_overlap_cus": (c_i32, [vp]),
         "psx_last_error": (ctypes.c_char_p, []),
         "psx_device_count": (c_int, [P(c_int)]),
         "psx_warmup": (c_int, [c_int]),
@@ -647,6 +648,11 @@ class PostCal:
 
     def set_shard(self, rank: int, world: int):
         _check(self.lib.psx_set_shard(self.h, rank, world))
+
+    def overlap_cus(self) -> int:
+        """CUs reserved beside overlapped asynchronous passes (psx_overlap_cus;
+        -1 before the handle's first asynchronous pass)."""
+        return int(self.lib.psx_overlap_cus(self.h))
 
     def plan_hash(self) -> int:
         """The shard plan's hash (psx_plan_hash): equal on every rank of a job."""

@@ -47,8 +47,11 @@ def test_async_ring_wraps(gpu):
     assert pc.timing()["kernel_launches"] == 150
 
 
-@pytest.mark.parametrize("world", [2, 5])
+@pytest.mark.parametrize("world", [2, 5, 8])
 def test_async_sharded_exchange(gpu, world):
+    """Sharded asynchronous passes with the exchange; at world >= 8 the handles
+    overlap their passes on CU-masked streams by default (one XCD kept for the
+    merges and the exchange), below it they do not."""
     import torch
     mi = _inputs()
     ref = E.PostCal(mi)
@@ -71,6 +74,7 @@ def test_async_sharded_exchange(gpu, world):
             pc.merge_partials(buf.data_ptr(), world)
     for pc in pcs:
         assert pc.sync() is False
+        assert (pc.overlap_cus() > 0) == (world >= 8), pc.overlap_cus()
         g = pc.accum()
         assert g.n_configs == r.n_configs
         for f in ("post", "no_causal", "shared"):
