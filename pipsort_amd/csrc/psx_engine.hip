@@ -1376,10 +1376,9 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
             } else {
                 // the compute stream sits below the engine / exchange stream in
                 // priority, so merges and the exchange get wave slots first.  (Two
-                // alternating compute streams on distinct queues, overlapping one
-                // sweep's tail with the next, measured +3 % at world 1 and 0 at
-                // world 8 without reserved CUs: the exchange's multi-wave blocks
-                // starve; PSX_OVERLAP reserves CUs for them.)
+                // alternating unmasked compute streams, overlapping one sweep's
+                // tail with the next: neutral at world 1, 2-7 % slower at worlds 2
+                // and 4, r05zm, profiles/r05zm_overlap_unmasked.txt.)
                 int lo_pr = 0, hi_pr = 0;
                 HIPCHK(hipDeviceGetStreamPriorityRange(&lo_pr, &hi_pr));
                 e->cstream_pr = (lo_pr + hi_pr) / 2;
