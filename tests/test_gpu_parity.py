@@ -445,6 +445,39 @@ def test_union_batch_rejects_bad_rows(gpu, row):
     assert np.array_equal(pc.eval_union_batch(good, accumulate=False), s0)
 
 
+@pytest.mark.parametrize("stride,k", [(1, 1), (6, 6), (6, 4)])
+def test_union_batch_strides(gpu, stride, k):
+    """The device batch path at the stride extremes: one row per SNP (stride
+    1, 512 sets per merge chunk) and six-member sets (stride 6, 3^6
+    assignments, 85 sets per chunk), also with padding (k = 4 of 6).  One call
+    over all rows equals the same rows fed in small calls (other chunk
+    boundaries: equal to fold-order rounding), scores exactly; each score is
+    the largest |L| over the set's assignments (the oracle's literal N x N
+    restatement on a sample of rows)."""
+    ld, z, _, _, u2l = synth.syn_v1(70)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=6, sharing_param=0.25)
+    rng = np.random.default_rng(stride * 10 + k)
+    n = 3000 if stride == 1 else 1500
+    rows = np.full((n, stride), -1, np.int32)
+    for i in range(n):
+        rows[i, :k] = np.sort(rng.choice(70, k, replace=False))
+    one, many = E.PostCal(seam), E.PostCal(seam)
+    s1 = one.eval_union_batch(rows, accumulate=True)
+    s2 = np.concatenate([many.eval_union_batch(rows[i:i + 77], accumulate=True) for i in range(0, n, 77)])
+    assert np.array_equal(s1, s2)
+    a, b = one.accum(), many.accum()
+    assert a.n_configs == b.n_configs == n * 3 ** k
+    for f in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+        assert np.array_equal(getattr(a, f) == 0, getattr(b, f) == 0), f
+        np.testing.assert_allclose(getattr(a, f), getattr(b, f), rtol=1e-12, atol=0, err_msg=f)
+    xs = [[(p // 3 ** j) % 3 + 1 for j in range(k)] for p in range(3 ** k)]
+    bits = np.array([[[v & 1 for v in x], [(v >> 1) & 1 for v in x]] for x in xs], dtype=np.int32)
+    for i in range(0, n, n // 5):
+        L, _ = O.eval_patterns(seam, np.repeat(rows[i:i + 1, :k], 3 ** k, axis=0), bits, literal=True)
+        best = L[np.argmax(np.abs(L))]
+        assert abs(s1[i] - best) <= 1e-9 * abs(best), (i, s1[i], best)
+
+
 def test_union_batch_padding_anywhere(gpu):
     """-1 padding may sit between members (the batch only asks ascending
     members): the records of such a row fold into the same SNPs, bitwise equal
