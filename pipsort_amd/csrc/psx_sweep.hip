@@ -596,7 +596,8 @@ int plan_units3c(int U, int ldg, int rank, int world, const unsigned char* pres_
     // (An XCD-aware order — runs of one tile's units packed onto the 8 XCDs,
     // workgroup i running on XCD (i + launch offset) % 8, so each 4 MB L2 serves
     // ~1/8 of the tile rows — measured neutral (r01y, worlds 1-8) once the next
-    // step's tile row is prefetched; not used.)
+    // step's tile row is prefetched, and 10 % slower in r05 with tiles dealt to
+    // 8 interleaved groups, profiles/r05zo_xcd_order_ab.txt; not used.)
     // (Splitting the last dispatch rounds into shorter b-walk pieces was
     // measured +1-6 % slower: a unit's fixed cost is ~11 us, EXPERIMENTS.md A.)
     return 0;
