@@ -961,7 +961,6 @@ int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool accumulate
     int rc;
     const size_t n_sets = nsets * stride;
     const bool chunked = accumulate && psx::batch_merge_chunks((long)nsets, stride) <= kBatchChunks && e->U <= 131072;
-    if (user && accumulate && !chunked) return fail(PSX_EINVAL, "internal: user batch slice beyond the chunked merge");
     // the batch's validity word: after the scores (user batches), a 64-bit
     // pattern unique to this call
     const unsigned long long badv = ((unsigned long long)(++e->batch_seq) << 32) | 0xBADBA7C4ull;
@@ -997,6 +996,13 @@ int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool accumulate
                                     e->dsacc, e->stream, dbad, badv))
             return fail(PSX_EHIP, "set-batch merge failed");
     } else if (accumulate) {
+        if (user) {
+            // (a user batch beyond the chunked merge, U > 131072: its validity is
+            // known before the CSR merges are enqueued, which do not check it)
+            HIPCHK(hipStreamSynchronize(e->stream));
+            if (*reinterpret_cast<const unsigned long long*>(e->hscore + nsets) == badv)
+                return fail(PSX_EINVAL, "sets must be ascending union indices");
+        }
         int* dptr = e->dgcsr;
         int* gidx = e->dgcsr + e->U + 1;
         if (psx::csr_from_keys_device(e->dgen, (long)n_sets, e->U, dptr, gidx, e->gscratch, e->stream))
