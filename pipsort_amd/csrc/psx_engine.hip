@@ -2241,6 +2241,7 @@ struct SssIter {
     int k, U, stride, num_zero, num_minus, num_plus, n_nbd, rank, world;
     double null_score;  // K + L0: a null configuration's L (postcal.cpp:797-803)
     unsigned long long* trace;  // PSX_SSS_TRACE: item 1's phase clocks (null: none)
+    unsigned int seq;  // one rank: the iteration's tag in the published mark words
 };
 
 // neighbour i (0 .. n_nbd) or, for i == -1, the current configuration: its
@@ -2290,13 +2291,29 @@ enum { kUnseen = 0, kNulls = 1, kCurPos = 2, kCurNull = 3, kNCnt = 4 };
 
 // item p of the iteration: the current configuration (p = 0, always evaluated
 // when unseen: sss_postcal.cpp:195-202) or neighbour i = p - 1.  mark[i]: -1
-// seen (its score is the map's), -2 an unseen null set, p an unseen set
+// seen (its score is the map's), -2 an unseen null set, p an unseen set.
+// One rank: every neighbour's weight and mark go to pinned host memory from
+// here.  The weight is stored first, then, once that store is acknowledged, the
+// mark word (iteration tag << 32 | mark); both at system scope (write-through,
+// no L2 write-back).  The host takes neighbour i when its word carries this
+// iteration's tag: no wait for the kernel's end (~5-8 us before its stop event
+// completes) and no contended completion counter.
+__device__ inline void publish_mark(double* lk_host, unsigned long long* mark_host, int i, double w, int mk,
+                                    unsigned int seq) {
+    __hip_atomic_store(lk_host + i, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);  // the weight's store acknowledged
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __hip_atomic_store(mark_host + i, ((unsigned long long)seq << 32) | (unsigned int)mk, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(64) void k_sss_eval(DevProb P, SssIter it, const MapEntry* __restrict__ T,
                                                  unsigned long long mask, int lo, int hi, int* __restrict__ rows,
                                                  int* __restrict__ mark, int* __restrict__ cnt,
                                                  double* __restrict__ lk_host, SetRec* __restrict__ srec,
                                                  Acc5* __restrict__ mrec, double* __restrict__ score,
-                                                 int* __restrict__ mark_host) {
+                                                 unsigned long long* __restrict__ mark_host) {
     __shared__ EvalShm shm;
     const int p = blockIdx.x, i = p - 1, lane = threadIdx.x;
     unsigned long long* const tr = (it.trace && p == 1 && lane == 0) ? it.trace : nullptr;
@@ -2315,10 +2332,10 @@ __global__ __launch_bounds__(64) void k_sss_eval(DevProb P, SssIter it, const Ma
         if (i >= 0) {
             const int mk = seen ? -1 : (n == 0 ? -2 : p);
             mark[i] = mk;
-            if (seen) lk_host[i] = v;
-            if (mark_host) {  // one rank: every item's weight and mark go to the host from here
-                mark_host[i] = mk;
-                if (mk == -2) lk_host[i] = it.null_score;
+            if (!mark_host) {
+                if (seen) lk_host[i] = v;
+            } else if (mk != p) {  // seen or null: published now (an unseen set after its evaluation)
+                publish_mark(lk_host, mark_host, i, seen ? v : it.null_score, mk, it.seq);
             }
         } else {
             cnt[kCurPos] = (seen || n == 0) ? -1 : 0;  // a null current configuration is counted, not evaluated
@@ -2334,7 +2351,10 @@ __global__ __launch_bounds__(64) void k_sss_eval(DevProb P, SssIter it, const Ma
         return;
     }
 #ifdef PSX_SSS_ABLATE
-    if (PSX_SSS_ABLATE == 1) return;
+    if (PSX_SSS_ABLATE == 1) {
+        if (mark_host && lane == 0 && i >= 0) publish_mark(lk_host, mark_host, i, 0.0, p, it.seq);
+        return;
+    }
 #endif
 #pragma unroll
     for (int j = 0; j < PSX_KMAX; j++)
@@ -2342,8 +2362,8 @@ __global__ __launch_bounds__(64) void k_sss_eval(DevProb P, SssIter it, const Ma
     eval_stage(ops, shm);
     if (tr) tr[2] = wall_clock64();
     eval_compute(P, ops, shm, nullptr, srec + p, mrec + (size_t)p * it.stride, score + p, tr);
-    if (mark_host && lane == 0 && i >= 0) lk_host[i] = score[p];  // the lane that wrote it
     if (tr) tr[7] = wall_clock64();
+    if (mark_host && lane == 0 && i >= 0) publish_mark(lk_host, mark_host, i, score[p], p, it.seq);  // the lane that wrote it
 }
 
 // blocks [0, U): per-SNP record folds; block U: the scalars; blocks > U: the
@@ -2525,9 +2545,10 @@ struct SssDev {
     double* lk = nullptr;     // pinned host: every neighbour's score
     SetRec* shost = nullptr;  // pinned host: the scalars after the iteration
     int* hcnt = nullptr;      // pinned host: the counters
-    int* hmark = nullptr;     // pinned host: per neighbour, its mark (one rank)
+    unsigned long long* hmark = nullptr;  // pinned host: per neighbour, its mark word (one rank)
     unsigned long long* trace = nullptr;  // PSX_SSS_TRACE: item 1's eval phase clocks (pinned host)
     double* hscore = nullptr; // pinned host: gathered item scores (world > 1)
+    unsigned int seq = 0;     // the last iteration tag of the mark words (never 0)
     ~SssDev() {
         psx::dfree(T);
         psx::dfree(rows);
@@ -2566,12 +2587,14 @@ int sss_workspace(psx_engine* e, size_t nmax, int world, hipStream_t s) {
         psx::dfree(D.rows); psx::dfree(D.mark);
         if (D.lk) psx::hfree(D.lk);
         if (D.hmark) psx::hfree(D.hmark);
-        D.rows = D.mark = D.hmark = nullptr;
+        D.rows = D.mark = nullptr;
+        D.hmark = nullptr;
         D.lk = nullptr;
         HIPCHK(psx::dmalloc(&D.rows, nmax * PSX_KMAX * sizeof(int)));
         HIPCHK(psx::dmalloc(&D.mark, nmax * sizeof(int)));
         HIPCHK(psx::hmalloc(reinterpret_cast<void**>(&D.lk), nmax * sizeof(double)));
-        HIPCHK(psx::hmalloc(reinterpret_cast<void**>(&D.hmark), nmax * sizeof(int)));
+        HIPCHK(psx::hmalloc(reinterpret_cast<void**>(&D.hmark), nmax * sizeof(unsigned long long)));
+        std::memset(D.hmark, 0, nmax * sizeof(unsigned long long));  // tag 0: no iteration
         D.nmax = nmax;
     }
     if (world > 1 && D.nmax_full < nmax) {
@@ -2627,6 +2650,9 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
     std::vector<double> pr;
     // diagnostics (PSX_SSS_PROFILE): host time per phase of the walk, on stderr
     static const bool prof = std::getenv("PSX_SSS_PROFILE") != nullptr;
+    // PSX_SSS_FLAG=0 (A/B): wait for the eval's stop event before reading the mark words
+    const char* fw = std::getenv("PSX_SSS_FLAG");
+    const bool event_wait = fw && fw[0] == '0';
     double ph[4] = {0, 0, 0, 0};  // launch, wait for the eval, sampling, wait for the post
     double tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // PSX_SSS_TRACE: item 1's eval phases
     auto tick = [&](int i, std::chrono::steady_clock::time_point& t) {
@@ -2649,6 +2675,8 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
         it.world = world;
         it.null_score = e->K + e->L0;
         it.trace = D.trace;
+        if (++D.seq == 0) D.seq = 1;  // (tag 0 is a word no iteration wrote)
+        it.seq = D.seq;
         const int n_nbd = it.n_nbd, n_items = n_nbd + 1;
         // this rank's contiguous slice of the items
         const int lo = (int)((int64_t)n_items * rank / world), hi = (int)((int64_t)n_items * (rank + 1) / world);
@@ -2686,7 +2714,10 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
         if (timed) HIPCHK(hipEventRecord(evp[0], e->stream));
         hipLaunchKernelGGL(k_sss_eval, dim3((unsigned)n_items), dim3(64), 0, e->stream, e->dp, it, D.T, mask, lo, hi,
                            D.rows, D.mark, D.cnt, D.lk, e->dsrec, e->dmrec, e->dscore, world == 1 ? D.hmark : nullptr);
-        HIPCHK(hipEventRecord(evp[1], e->stream));
+        // (the stop event: the host's wait without the completion word, else only
+        // the sampled eval time)
+        const bool poll = world == 1 && !event_wait;
+        if (timed || !poll) HIPCHK(hipEventRecord(evp[1], e->stream));
         const unsigned post_blocks = (unsigned)(U + 1 + (world == 1 ? (n_nbd + 255) / 256 : 0));
         hipLaunchKernelGGL(k_sss_post, dim3(post_blocks), dim3(256), 0, e->stream, it, lo, hi, D.rows, D.mark, D.cnt,
                            e->dmrec, e->dsrec, e->dscore, null1, e->dacc, e->dsacc, D.shost, D.hcnt, D.T, mask,
@@ -2700,15 +2731,39 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
             // GPU folds the records and inserts the new scores (k_sss_post); it
             // waits for the post only where the stop test needs the normaliser.
             tick(0, tp);
-            HIPCHK(hipEventSynchronize(evp[1]));
-            tick(1, tp);
-            if (D.trace && D.trace[7]) {  // item 1's eval phases (100 MHz clock)
-                const unsigned long long* q = D.trace;
-                for (int x = 0; x < 7; x++) tph[x] += (double)(q[x + 1] - q[x]) * 0.01;
-                tph[7] += 1;
-                D.trace[7] = 0;
+            if (!poll) HIPCHK(hipEventSynchronize(evp[1]));
+            // each neighbour's mark word once it carries this iteration's tag (its
+            // weight was acknowledged before it).  An idle stream (eval and post
+            // done) with a word still missing is an error.
+            const unsigned long long tag = (unsigned long long)it.seq << 32;
+            unsigned spins = 0;
+            for (int i = 0; i < n_nbd; i++) {
+                unsigned long long w;
+                while (((w = __atomic_load_n(D.hmark + i, __ATOMIC_ACQUIRE)) & ~0xffffffffULL) != tag) {
+                    if ((++spins & 4095) == 0) {
+                        const hipError_t q = hipStreamQuery(e->stream);
+                        if (q == hipSuccess) {
+                            w = __atomic_load_n(D.hmark + i, __ATOMIC_ACQUIRE);
+                            if ((w & ~0xffffffffULL) == tag) break;
+                            return fail(PSX_EHIP, "SSS: the eval finished without neighbour " + std::to_string(i) +
+                                                      "'s mark word");
+                        }
+                        if (q != hipErrorNotReady) HIPCHK(q);
+                    }
+                    __builtin_ia32_pause();
+                }
+                unseen += (int)(unsigned int)w != -1;
             }
-            for (int i = 0; i < n_nbd; i++) unseen += D.hmark[i] != -1;
+            tick(1, tp);
+            if (D.trace) {  // item 1's eval phases (100 MHz clock), after the eval's end
+                HIPCHK(hipStreamSynchronize(e->stream));
+                const unsigned long long* q = D.trace;
+                if (q[7]) {
+                    for (int x = 0; x < 7; x++) tph[x] += (double)(q[x + 1] - q[x]) * 0.01;
+                    tph[7] += 1;
+                    D.trace[7] = 0;
+                }
+            }
         } else {
             HIPCHK(hipStreamSynchronize(e->stream));
             unseen = D.hcnt[kUnseen];
