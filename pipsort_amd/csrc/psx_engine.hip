@@ -24,6 +24,7 @@
 #include "../../include/pipsort_model.h"
 #include "psx_configs.h"
 #include "psx_math.h"
+#include "psx_sample.h"
 #include "psx_setup.h"
 #include "psx_sweep.h"
 #include "psx_sweep_dev.h"
@@ -2806,21 +2807,24 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
         const double* lk = D.lk;
         double wz = 0, wm = 0, wp = 0;
         size_t zs = n_nbd, ms = n_nbd, ps = n_nbd;
+        // each group: discrete_distribution(exp(lk - max))(gen) and the weights'
+        // sum (accumulate), the draw restated without the distribution's vectors
+        // (psx_sample.h: bit-identical partial sums, the same index)
         auto group = [&](int b, int en, double& wsum, size_t& smp) {
             pr.resize((size_t)(en - b));
             double mx = *std::max_element(lk + b, lk + en);
             // (slicing these exps over spinning host threads measured slower: the
             // serial loop takes ~5 us at 1,000 neighbours, profiles/archive/r03v_sss_threads.txt)
-            for (int ii = b; ii < en; ii++) pr[ii - b] = std::exp(lk[ii] - mx);
-            std::discrete_distribution<size_t> dist(pr.begin(), pr.end());
-            smp = dist(gen);
-            wsum = std::accumulate(pr.begin(), pr.end(), 0.0);
+            double s = 0.0;
+            for (int ii = b; ii < en; ii++) s += (pr[ii - b] = std::exp(lk[ii] - mx));
+            smp = psx::discrete_draw(pr.data(), pr.size(), s, gen);
+            wsum = s;
         };
         if (it.num_zero != 0) group(0, it.num_zero, wz, zs);                               // :296-306
         if (it.num_minus != 0) group(it.num_zero, it.num_zero + it.num_minus, wm, ms);     // :307-317
         if (it.num_plus != 0) group(it.num_zero + it.num_minus, n_nbd, wp, ps);            // :318-328
-        std::discrete_distribution<size_t> dist({wz, wm, wp});                             // :330-343
-        size_t idx = dist(gen), fin = 0;
+        const double w3[3] = {wz, wm, wp};                                                 // :330-343
+        size_t idx = psx::discrete_draw(w3, 3, (0.0 + wz + wm) + wp, gen), fin = 0;
         switch (idx) {
             case 0: fin = zs; break;
             case 1: fin = ms + it.num_zero; break;
