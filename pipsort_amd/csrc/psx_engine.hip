@@ -247,14 +247,17 @@ __device__ __forceinline__ void eval_stage(const EvalOps& o, EvalShm& sh) {
 }
 
 // the set's 2^k subset weights per study and its 3^k assignments (after
-// eval_gather / eval_stage): set record, member records, score
+// eval_gather / eval_stage): set record, member records, score.  KM: the most
+// members the caller's sets have (KM = 5 for batches of at most 5: fewer live
+// registers in the unrolled factorisations and pattern sums)
+template <int KM = PSX_KMAX>
 __device__ void eval_compute(const DevProb& P, const EvalOps& o, EvalShm& shm, const int* __restrict__ fpair,
                              SetRec* __restrict__ so, Acc5* __restrict__ mo, double* __restrict__ sc,
                              unsigned long long* tr = nullptr) {
-    constexpr int KM = PSX_KMAX;
-    double (&s_g)[2][KM][KM] = shm.g;
-    double (&s_ad)[2][KM] = shm.ad;
-    double (&s_y)[2][KM] = shm.y;
+    static_assert(KM >= 1 && KM <= PSX_KMAX, "members per set");
+    double (&s_g)[2][PSX_KMAX][PSX_KMAX] = shm.g;
+    double (&s_ad)[2][PSX_KMAX] = shm.ad;
+    double (&s_y)[2][PSX_KMAX] = shm.y;
     double (&s_mu)[2][64] = shm.mu;
     double (&s_f)[2][64] = shm.f;
     int (&s_n)[2][64] = shm.n;
@@ -384,8 +387,8 @@ __device__ void eval_compute(const DevProb& P, const EvalOps& o, EvalShm& shm, c
     if (tr) tr[4] = wall_clock64();
     // every sum in one transposed batch (~7 instructions per value instead of
     // six dependent LDS shuffles each); the score's minimum by DPP
-    static_assert(4 + 5 * KM <= 36, "reduction batch");
-    double red[36];
+    constexpr int RK = (4 + 5 * KM + 3) / 4 * 4;  // the reduction batch (a multiple of 4)
+    double red[RK];
     red[0] = tot; red[1] = nc0; red[2] = nc1; red[3] = npatv;
 #pragma unroll
     for (int j = 0; j < KM; j++) {
@@ -393,7 +396,7 @@ __device__ void eval_compute(const DevProb& P, const EvalOps& o, EvalShm& shm, c
         red[7 + 5 * j] = sl[j]; red[8 + 5 * j] = ns[j];
     }
 #pragma unroll
-    for (int i = 4 + 5 * KM; i < 36; i++) red[i] = 0.0;
+    for (int i = 4 + 5 * KM; i < RK; i++) red[i] = 0.0;
     psx::wave_sum_t(red);
     tot = red[0]; nc0 = red[1]; nc1 = red[2]; npatv = red[3];
     smin = __ockl_wfred_min_f64(smin);
@@ -439,12 +442,13 @@ __device__ void eval_compute(const DevProb& P, const EvalOps& o, EvalShm& shm, c
 
 
 // one set (sorted members, -1 padded, in global or LDS memory): gather, stage, compute
+template <int KM = PSX_KMAX>
 __device__ void eval_set(const DevProb& P, const int* __restrict__ S, int stride, const int* __restrict__ fpair,
                          SetRec* __restrict__ so, Acc5* __restrict__ mo, double* __restrict__ sc) {
     __shared__ EvalShm shm;
     const EvalOps o = eval_gather(P, S, stride, shm);
     eval_stage(o, shm);
-    eval_compute(P, o, shm, fpair, so, mo, sc);
+    eval_compute<KM>(P, o, shm, fpair, so, mo, sc);
 }
 
 // span (optional, device [lo, hi)): block b evaluates set lo + b of `sets`, the
@@ -474,11 +478,11 @@ __global__ __launch_bounds__(64) void k_eval_sets(DevProb P, const int* __restri
 // The rows are read from `in` and written compacted to `out` (device; may be the
 // same rows); scores and the validity word go to pinned host memory (no readback
 // copy), the word also to `bad` (device) for the merges.
-__global__ __launch_bounds__(64) void k_eval_batch(DevProb P, const int* in, int* out,
-                                                   int stride, SetRec null1, double L0, unsigned long long badv,
-                                                   unsigned long long* __restrict__ bad,
-                                                   unsigned long long* __restrict__ hbad, SetRec* __restrict__ srec,
-                                                   Acc5* __restrict__ mrec, double* __restrict__ score) {
+template <int KM>
+__device__ __forceinline__ void eval_batch_row(const DevProb& P, const int* in, int* out, int stride, SetRec null1,
+                                               double L0, unsigned long long badv, unsigned long long* __restrict__ bad,
+                                               unsigned long long* __restrict__ hbad, SetRec* __restrict__ srec,
+                                               Acc5* __restrict__ mrec, double* __restrict__ score) {
     __shared__ int row[PSX_KMAX];
     const int set = blockIdx.x, lane = threadIdx.x;
     int* S = out + (size_t)set * stride;
@@ -507,8 +511,21 @@ __global__ __launch_bounds__(64) void k_eval_batch(DevProb P, const int* in, int
         }
         return;
     }
-    eval_set(P, row, stride, nullptr, srec + set, mrec + (size_t)set * stride, score ? score + set : nullptr);
+    eval_set<KM>(P, row, stride, nullptr, srec + set, mrec + (size_t)set * stride, score ? score + set : nullptr);
 }
+#define PSX_EVAL_BATCH_ARGS                                                                                   \
+    DevProb P, const int *in, int *out, int stride, SetRec null1, double L0, unsigned long long badv,         \
+        unsigned long long *__restrict__ bad, unsigned long long *__restrict__ hbad, SetRec *__restrict__ srec, \
+        Acc5 *__restrict__ mrec, double *__restrict__ score
+__global__ __launch_bounds__(64) void k_eval_batch(PSX_EVAL_BATCH_ARGS) {
+    eval_batch_row<PSX_KMAX>(P, in, out, stride, null1, L0, badv, bad, hbad, srec, mrec, score);
+}
+// rows of at most 5 members: 96 registers, 5 waves per SIMD (the 6-member
+// instance needs 113: 4 waves)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_eval_batch5(PSX_EVAL_BATCH_ARGS) {
+    eval_batch_row<5>(P, in, out, stride, null1, L0, badv, bad, hbad, srec, mrec, score);
+}
+#undef PSX_EVAL_BATCH_ARGS
 
 // merge `count` concatenated partial images (rank order) into acc / sacc.
 // Image layout: Acc5[ldg] followed by one Acc5-sized slot holding the SetRec.
@@ -982,9 +999,9 @@ int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool accumulate
     HIPCHK(hipEventRecord(e->stage_ev, e->stream));
     e->stage_rec = true;
     if (kernel_ms) HIPCHK(hipEventRecord(e->ev[2], e->stream));
-    if (user)
-        hipLaunchKernelGGL(k_eval_batch, dim3((unsigned)nsets), dim3(64), 0, e->stream, e->dp, e->dgen, e->dgen,
-                           stride, null_rec(e, 1.0), e->L0, badv, dbad,
+    if (user)  // (rows of at most 5 members: the 5-member instance, fewer live registers)
+        hipLaunchKernelGGL(stride <= 5 ? k_eval_batch5 : k_eval_batch, dim3((unsigned)nsets), dim3(64), 0,
+                           e->stream, e->dp, e->dgen, e->dgen, stride, null_rec(e, 1.0), e->L0, badv, dbad,
                            reinterpret_cast<unsigned long long*>(e->hscore + nsets), e->dsrec, e->dmrec,
                            scores ? e->hscore : nullptr);
     else
