@@ -2326,6 +2326,8 @@ __device__ inline void publish_mark(double* lk_host, unsigned long long* mark_ho
                        __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+extern "C++" {  // (a template, inside the ABI's extern "C" block)
+template <int KM>  // the most members of a set of the walk (max_causal; 5 for KM = 5)
 __global__ __launch_bounds__(64) void k_sss_eval(DevProb P, SssIter it, const MapEntry* __restrict__ T,
                                                  unsigned long long mask, int lo, int hi, int* __restrict__ rows,
                                                  int* __restrict__ mark, int* __restrict__ cnt,
@@ -2379,10 +2381,11 @@ __global__ __launch_bounds__(64) void k_sss_eval(DevProb P, SssIter it, const Ma
         if (j < it.stride && lane == j) rows[(size_t)p * it.stride + j] = row[j];
     eval_stage(ops, shm);
     if (tr) tr[2] = wall_clock64();
-    eval_compute(P, ops, shm, nullptr, srec + p, mrec + (size_t)p * it.stride, score + p, tr);
+    eval_compute<KM>(P, ops, shm, nullptr, srec + p, mrec + (size_t)p * it.stride, score + p, tr);
     if (tr) tr[7] = wall_clock64();
     if (mark_host && lane == 0 && i >= 0) publish_mark(lk_host, mark_host, i, score[p], p, it.seq);  // the lane that wrote it
 }
+}  // extern "C++"
 
 // blocks [0, U): per-SNP record folds; block U: the scalars; blocks > U: the
 // map inserts and the sampling weights.  mode 0: folds only, 1: folds and
@@ -2730,7 +2733,8 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
             ksamples++;
         }
         if (timed) HIPCHK(hipEventRecord(evp[0], e->stream));
-        hipLaunchKernelGGL(k_sss_eval, dim3((unsigned)n_items), dim3(64), 0, e->stream, e->dp, it, D.T, mask, lo, hi,
+        hipLaunchKernelGGL(C <= 5 ? k_sss_eval<5> : k_sss_eval<PSX_KMAX>, dim3((unsigned)n_items), dim3(64), 0,
+                           e->stream, e->dp, it, D.T, mask, lo, hi,
                            D.rows, D.mark, D.cnt, D.lk, e->dsrec, e->dmrec, e->dscore, world == 1 ? D.hmark : nullptr);
         // (the stop event: the host's wait without the completion word, else only
         // the sampled eval time)
