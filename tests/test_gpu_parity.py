@@ -260,6 +260,39 @@ def test_sss_long_walk_m100_c5(gpu):
     pc.close()
 
 
+def test_sss_mark_words_equal_event_wait(gpu, monkeypatch):
+    """The one-rank walk reads each neighbour once its tagged mark word arrives
+    (psx_engine.hip run_sss); PSX_SSS_FLAG=0 waits for the eval's stop event
+    first.  Both must visit the same configurations: bitwise-equal accumulators
+    and iteration counts, walk after walk on one handle (the tags advance)."""
+    ld, z, _, _, u2l = synth.syn_v1(100)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=5, sharing_param=0.25)
+    pc = E.PostCal(seam)
+    runs = []
+    for flag in ("1", "0", "1"):
+        monkeypatch.setenv("PSX_SSS_FLAG", flag)
+        it = pc.run_sss()
+        a = pc.accum()
+        runs.append((it, a))
+    pc.close()
+    it0, a0 = runs[0]
+    for it, a in runs[1:]:
+        assert it == it0 and a.n_configs == a0.n_configs and a.total == a0.total
+        for f in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+            assert np.array_equal(getattr(a, f), getattr(a0, f)), f
+
+
+def test_sss_synthetic_c6(gpu):
+    """max_causal 6: the walk's eval with every member slot (k_sss_eval<6>;
+    max_causal <= 5 runs the 5-member instance)."""
+    ld, z, _, _, u2l = synth.syn_v1(40)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=6, sharing_param=0.25)
+    pc = E.PostCal(seam)
+    pc.run_sss()
+    assert_parity(pc.accum(), O.postcal(seam, "sss"), ll_rtol=1e-11)
+    pc.close()
+
+
 def test_union_batch_scores(gpu):
     """expand_and_compute_lkl scores (max |L| pattern) for ragged sets incl. the null set."""
     seam, _ = loci.seam_for(loci.SMALL, c=3)
