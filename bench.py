@@ -345,12 +345,13 @@ def sss_probe(reps=20):
 
 
 def sss_roofline(n_sets, npat, kernel_ms):
-    """The batch's dominant kernel, k_eval_batch (a wave per union set: 2^k
+    """The batch's dominant kernel, k_eval_batch5 (k_eval_batch for rows of 6
+    members; a wave per union set: 2^k
     subset LDL^T per study, then the 3^k assignments), is FP64 VALU work:
     achieved = FP64 operations of one launch (PMC SQ_INSTS_VALU_FLOPS_FP64 x 64
     of this very build and batch shape, profiles/pmc_latest.json "sss_eval") /
     its launch duration measured here (HIP events around the launch)."""
-    out = {"bound": "valu_fp64", "kernel": "k_eval_batch", "kernel_ms": kernel_ms, "peak": FP64_PEAK_TFLOPS,
+    out = {"bound": "valu_fp64", "kernel": "k_eval_batch5", "kernel_ms": kernel_ms, "peak": FP64_PEAK_TFLOPS,
            "unit": "TFLOP/s", "kernel_configs_per_s": npat / (kernel_ms / 1e3) if kernel_ms > 0 else None,
            "duration_source": "HIP events around the launch on the engine stream (psx_get_timing), mean of reps",
            "achieved": None, "frac": None, "eval_src_sha": eval_src_sha()}

@@ -58,7 +58,7 @@ for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
 # the SSS proposal batch's evaluator (bench.py sss_probe: one k_eval_batch
 # launch over the whole neighbourhood): the largest-grid k_eval_batch dispatches
 ev = collections.defaultdict(float)
-grids = {}
+grids, names = {}, {}
 for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         if "k_eval_batch" not in r["Kernel_Name"]:
@@ -66,6 +66,7 @@ for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
         key = (os.path.basename(os.path.dirname(f)), r["Counter_Name"], r["Dispatch_Id"])
         ev[key] += float(r["Counter_Value"])
         grids[r["Dispatch_Id"]] = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
+        names[r["Dispatch_Id"]] = "k_eval_batch5" if "k_eval_batch5" in r["Kernel_Name"] else "k_eval_batch"
 if ev:
     gmax = max(grids.values())
     per_ev = collections.defaultdict(list)
@@ -73,7 +74,8 @@ if ev:
         if grids[disp] == gmax:
             per_ev[cn].append(v)
     ce = {k: sum(v) / len(v) for k, v in per_ev.items()}
-    out["sss_eval"] = {"kernel": "k_eval_batch", "grid_size": gmax, "eval_src_sha": bench.eval_src_sha(),
+    kname = sorted({names[x] for x in grids if grids[x] == gmax})
+    out["sss_eval"] = {"kernel": "/".join(kname), "grid_size": gmax, "eval_src_sha": bench.eval_src_sha(),
                        "counters_per_dispatch": ce}
     if "SQ_INSTS_VALU_FLOPS_FP64" in ce:
         out["sss_eval"]["fp64_flop_insts_per_launch"] = ce["SQ_INSTS_VALU_FLOPS_FP64"]
