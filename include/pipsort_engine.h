@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define PSX_ABI_VERSION 3
+#define PSX_ABI_VERSION 4
 
 #define PSX_OK 0
 #define PSX_EINVAL (-1)    /* bad argument / unsupported problem shape        */
@@ -254,6 +254,11 @@ int64_t psx_partials_bytes(psx_engine *e);
  * sweep complete. */
 int psx_set_stream(psx_engine *e, void *stream);
 int psx_export_partials(psx_engine *e, void *device_dst);
+/* The handle's own partial image in device memory (psx_partials_bytes() bytes,
+ * the psx_export_partials layout): a collective may read it in place instead of
+ * an exported copy (one launch less per exchange).  Valid until the next pass,
+ * merge or reset on the handle enqueues a write to it; read-only to the caller. */
+int psx_partials_device_ptr(psx_engine *e, void **device_ptr);
 int psx_merge_partials(psx_engine *e, const void *device_src, int32_t count);
 
 /* Host-only (no GPU needed): fold `count` partial images of `image_bytes`

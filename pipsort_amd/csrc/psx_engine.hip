@@ -42,6 +42,7 @@ namespace {
 
 thread_local std::string g_err;
 constexpr int kPlanMismatchWord = 8;  // status word raised by k_merge_partials
+constexpr int kStampWord = 4;          // status words 4..7: a single pass's sweep / merge start clocks (2 x u64)
 
 constexpr size_t kStatBytes = 3 * 56;  // SetRec, PlanTag, status words (EXACT flag first)
 
@@ -527,37 +528,107 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
 }
 #undef PSX_EVAL_BATCH_ARGS
 
+// One lane copies the status block (SetRec, PlanTag, status words: kStatBytes
+// from the scalars' slot) and the robust-redo count to pinned host memory, so
+// psx_sync needs no read-out launch after the merges that end a pass or an
+// exchange (k_merge_fin, k_merge_partials).  The lane wrote the scalars and the
+// flag words itself; the rest comes from earlier launches.
+__device__ void status_to_host(const int* __restrict__ stat, const int* __restrict__ redo, int* __restrict__ host) {
+    constexpr int nw = (int)(kStatBytes / sizeof(int));
+    int w[nw];
+#pragma unroll
+    for (int i = 0; i < nw; i++) w[i] = stat[i];
+    const int r = redo ? *redo : 0;
+#pragma unroll
+    for (int i = 0; i < nw; i++) host[i] = w[i];
+    host[nw] = r;
+}
+
 // merge `count` concatenated partial images (rank order) into acc / sacc.
-// Image layout: Acc5[ldg] followed by one Acc5-sized slot holding the SetRec.
-__global__ void k_merge_partials(const Acc5* __restrict__ parts, int U, int ldg, int count, Acc5* __restrict__ acc,
-                                 SetRec* __restrict__ sacc, int* __restrict__ flag) {
+// Image layout: Acc5[ldg] followed by one Acc5-sized slot holding the SetRec
+// and one holding the PlanTag.  The images must be shards 0 .. count - 1 of one
+// plan: every thread checks the tags first (the same few lines for all), and
+// when they disagree nothing is written — the accumulators keep their values —
+// and status word kPlanMismatchWord is raised (psx_sync / psx_merge_partials
+// report and clear it).  Grid: (U + 63) / 64 per-SNP blocks + one scalar block.
+__global__ __launch_bounds__(64) void k_merge_partials(const Acc5* __restrict__ parts, int U, int ldg, int count,
+                                                       Acc5* __restrict__ acc, SetRec* __restrict__ sacc,
+                                                       int* __restrict__ flag, const int* __restrict__ redo,
+                                                       int* __restrict__ host) {
     const size_t stride = (size_t)ldg + 2;  // ldg Acc5, SetRec, PlanTag
-    int u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u < U) {
-        Acc5 a = {0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0, 0.0};
-        for (int r = 0; r < count; r++) psx::fold_acc(a, parts[(size_t)r * stride + u]);
-        acc[u] = a;
+    const int tid = threadIdx.x;
+    const PlanTag& t0 = *reinterpret_cast<const PlanTag*>(parts + ldg + 1);
+    bool bad = false;
+    for (int r = 0; r < count; r++) {
+        const PlanTag& t = *reinterpret_cast<const PlanTag*>(parts + (size_t)r * stride + ldg + 1);
+        bad |= t.magic != kPlanMagic || t.hash != t0.hash || t.world != count || t.rank != r || t.U != U;
     }
-    if (u == 0) {
+    if (blockIdx.x == gridDim.x - 1) {  // the scalars, in rank order on lane 0
+        if (bad) {
+            if (tid == 0) {
+                flag[kPlanMismatchWord] = 1;
+                if (host) status_to_host(reinterpret_cast<const int*>(sacc), redo, host);
+            }
+            return;
+        }
         SetRec s = psx::set_zero();
         int f = 0;
-        for (int r = 0; r < count; r++) {
-            const SetRec& x = *reinterpret_cast<const SetRec*>(parts + (size_t)r * stride + ldg);
-            psx::fold_set(s, x);
-            f |= x.pad;  // any rank's EXACT flag
+        for (int r0 = 0; r0 < count; r0 += 64) {
+            SetRec x = psx::set_zero();
+            if (r0 + tid < count) x = *reinterpret_cast<const SetRec*>(parts + (size_t)(r0 + tid) * stride + ldg);
+            const int m = min(64, count - r0);
+            for (int q = 0; q < m; q++) {
+                SetRec y;
+                y.m = __shfl(x.m, q); y.m0 = __shfl(x.m0, q); y.m1 = __shfl(x.m1, q); y.pad = __shfl(x.pad, q);
+                y.tot = __shfl(x.tot, q); y.nc0 = __shfl(x.nc0, q); y.nc1 = __shfl(x.nc1, q);
+                y.score = __shfl(x.score, q); y.npat = __shfl(x.npat, q);
+                psx::fold_set(s, y);
+                f |= y.pad;  // any rank's EXACT flag
+            }
         }
-        s.pad = f;
-        flag[1] |= f;
-        *sacc = s;
-        // the images must be shards 0 .. count - 1 of one plan (PlanTag)
-        const PlanTag& t0 = *reinterpret_cast<const PlanTag*>(parts + ldg + 1);
-        int bad = 0;
-        for (int r = 0; r < count; r++) {
-            const PlanTag& t = *reinterpret_cast<const PlanTag*>(parts + (size_t)r * stride + ldg + 1);
-            bad |= t.magic != kPlanMagic || t.hash != t0.hash || t.world != count || t.rank != r || t.U != U;
+        if (tid == 0) {
+            s.pad = f;
+            flag[1] |= f;
+            *sacc = s;
+            if (host) status_to_host(reinterpret_cast<const int*>(sacc), redo, host);
         }
-        if (bad) flag[kPlanMismatchWord] = 1;
+        return;
     }
+    const int u = blockIdx.x * 64 + tid;
+    if (u >= U) return;
+    Acc5 a = {0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int r0 = 0; r0 < count; r0 += 8) {  // eight image loads in flight, folded in rank order
+        Acc5 x[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            if (r0 + q < count) x[q] = parts[(size_t)(r0 + q) * stride + u];
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            if (r0 + q < count) psx::fold_acc(a, x[q]);
+    }
+    if (!bad) acc[u] = a;  // (the image loads do not wait for the tag check)
+}
+
+// the partial image (ldg + 2 slots) to a caller's buffer, 16 bytes per thread
+__global__ __launch_bounds__(256) void k_copy_image(const int4* __restrict__ src, size_t n16, int4* __restrict__ dst) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n16) dst[i] = src[i];
+}
+
+// psx_sync's status read-out: the status block (SetRec, PlanTag, status words)
+// and the robust-redo count straight to pinned host memory, then the words the
+// host consumes are re-armed (sticky EXACT flag, plan mismatch).  One launch in
+// place of two copies and a memset.
+__global__ __launch_bounds__(64) void k_status_out(int* __restrict__ stat, const int* __restrict__ redo,
+                                                   int* __restrict__ host) {
+    constexpr int nw = (int)(kStatBytes / sizeof(int));
+    const int i = threadIdx.x;
+    if (i < nw) {
+        host[i] = stat[i];
+        constexpr int base = 2 * (int)(sizeof(SetRec) / sizeof(int));  // status words after SetRec + PlanTag
+        if (i == base + 1 || i == base + kPlanMismatchWord) stat[i] = 0;
+    }
+    if (i == nw) host[nw] = redo ? *redo : 0;
 }
 
 // Level 1 for one union SNP u, per thread: k_eval_sets with k = 1 written out
@@ -613,51 +684,115 @@ __device__ void eval_single(const DevProb& P, int u, Acc5& a, SetRec& r) {
     r.tot = tot; r.nc0 = nc0; r.nc1 = nc1; r.score = smin; r.npat = npat;
 }
 
-// The whole-pass merge of the fused exhaustive pass, with level 1 folded in.
-//   block 0:     scalars = extra (null configuration) + level-1 sets of this
-//                shard + every tiled-level unit record (srec[0, nsrec))
-//   block 1 + u: acc[u] = level-1 record of u (if in this shard), then u's
-//                records of level A and level B (dense per-SNP runs)
-// One wave per block: the merge of pass i runs beside sweep i + 1, whose
-// one-wave blocks hold every wave slot; a one-wave merge block takes the first
-// slot any sweep block frees (a wider block waits for several free slots on
-// one CU at once and was starved for the whole sweep).
+// The whole-pass merge of the fused exhaustive pass, with level 1 folded in,
+// in two launches of one-wave blocks (r06; r01-r05 had one launch whose block
+// 0 folded every scalar record in one wave: 86 us of a 0.84 ms single pass at
+// world 1, 26 us of 0.23 ms at world 8, profiles/r06a_*):
+//   k_merge_rec   blocks [0, nch):    scalar chunk c folds kScalChunk consecutive
+//                                     scalar items (the level-1 sets of this shard,
+//                                     then every unit record, srec[0, nsrec)) -> spart[c]
+//                 block nch + V u + v: slice v of V of SNP u's record run (level A
+//                                     then level B, dense per-SNP runs) -> apart[V u + v]
+//   k_merge_fin   block 0:            scalars = extra (null configuration), then
+//                                     spart in chunk order (one wave, fixed tree)
+//                 blocks 1..:         thread u: acc[u] = level-1 record of u (if in
+//                                     this shard), then apart[V u .. V u + V) in order
+// One-wave blocks throughout: a pipelined pass's merge runs beside the next
+// sweep, whose one-wave blocks hold every wave slot, and takes the first slot
+// any sweep block frees (a wider block waits for several free slots on one CU
+// at once and was starved for the whole sweep, r02).  V (slices per SNP) is a
+// function of the plan only, and every pass runs the same two launches, so
+// synchronous, pipelined and single passes give bitwise-identical results.
 // Fixed fold order: deterministic.
-// (PSX_MERGE_WAVES, A/B: one item per wave, several waves per block — a block
-// then needs that many free wave slots on one CU, which the sweep beside it
-// leaves only in its drain)
-#ifndef PSX_MERGE_WAVES
-#define PSX_MERGE_WAVES 1
-#endif
-constexpr int kMergeThreads = 64;
-constexpr int kMergeWaves = PSX_MERGE_WAVES;
-__global__ __launch_bounds__(kMergeThreads * kMergeWaves) void k_merge_pass_l1(DevProb P, int lo, int hi, const Acc5* __restrict__ recA,
-                                                       const int* __restrict__ dptrA, const int* __restrict__ gidxA,
-                                                       const Acc5* __restrict__ recB, const int* __restrict__ dptrB,
-                                                       const int* __restrict__ gidxB, const SetRec* __restrict__ srec,
-                                                       long nsrec, SetRec extra, Acc5* __restrict__ acc,
-                                                       SetRec* __restrict__ sacc, int* __restrict__ flag,
-                                                       int* __restrict__ sticky) {
-    constexpr int T = kMergeThreads;
-    const int tid = threadIdx.x & 63;
-    const int item = blockIdx.x * kMergeWaves + (threadIdx.x >> 6);
-    if (item == 0) {
+constexpr int kScalChunk = 512;   // scalar items per chunk wave (8 per lane)
+constexpr int kMergeWaysMax = 8;  // slices per SNP run
+constexpr int kMergeDepth = 8;    // record loads in flight per lane
+
+__global__ __launch_bounds__(64) void k_merge_rec(DevProb P, int lo, int nsingle, const Acc5* __restrict__ recA,
+                                                  const int* __restrict__ dptrA, const int* __restrict__ gidxA,
+                                                  const Acc5* __restrict__ recB, const int* __restrict__ dptrB,
+                                                  const int* __restrict__ gidxB, const SetRec* __restrict__ srec,
+                                                  long nsrec, int nch, int V, SetRec* __restrict__ spart,
+                                                  Acc5* __restrict__ apart, unsigned long long* __restrict__ ts) {
+    constexpr int T = 64;
+    const int tid = threadIdx.x;
+    const int b = blockIdx.x;
+    if (ts && b == 0 && tid == 0) ts[1] = wall_clock64();  // a single pass: the sweep's end (its start: ts[0])
+    if (b < nch) {
+        const long n = (long)nsingle + nsrec;
+        const long i0 = (long)b * kScalChunk + tid;
+        SetRec r[kScalChunk / T];
+#pragma unroll
+        for (int q = 0; q < kScalChunk / T; q++) {
+            const long i = i0 + (long)q * T;
+            if (i >= nsingle && i < n) r[q] = srec[i - nsingle];
+        }
+#pragma unroll
+        for (int q = 0; q < kScalChunk / T; q++) {
+            const long i = i0 + (long)q * T;
+            if (i < nsingle) {
+                Acc5 dummy;
+                eval_single(P, lo + (int)i, dummy, r[q]);
+            } else if (i >= n) {
+                r[q] = psx::set_zero();
+            }
+        }
         SetRec a = psx::set_zero();
-        for (int u = lo + tid; u < hi; u += T) {
-            Acc5 dummy;
-            SetRec r;
-            eval_single(P, u, dummy, r);
-            psx::fold_set(a, r);
-        }
-        long i = tid;
-        for (; i + 7 * T < nsrec; i += 8 * T) {  // eight independent loads in flight per lane
-            SetRec r[8];
 #pragma unroll
-            for (int q = 0; q < 8; q++) r[q] = srec[i + q * T];
+        for (int q = 0; q < kScalChunk / T; q++) psx::fold_set(a, r[q]);
+        psx::wave_fold_set(a);
+        if (tid == 0) spart[b] = a;
+        return;
+    }
+    const int item = b - nch;
+    const int u = item / V, v = item - u * V;
+    if (u >= P.U) return;
+    const int a0 = dptrA ? dptrA[u] : 0, na = dptrA ? dptrA[u + 1] - a0 : 0;
+    const int b0 = dptrB ? dptrB[u] : 0, nb = dptrB ? dptrB[u + 1] - b0 : 0;
+    const int n = na + nb;
+    const int j0 = (int)((long)n * v / V), j1 = (int)((long)n * (v + 1) / V);
+    Acc5 a = psx::acc_zero();
+    // each lane folds its records in record order, kMergeDepth loads in flight
+    // (their gather indices loaded one round ahead)
+    constexpr int D = kMergeDepth;
+    auto gidx_of = [&](int j) {
+        return j < na ? (gidxA ? gidxA[a0 + j] : a0 + j) : (gidxB ? gidxB[b0 + j - na] : b0 + j - na);
+    };
+    int g[D];
 #pragma unroll
-            for (int q = 0; q < 8; q++) psx::fold_set(a, r[q]);
+    for (int q = 0; q < D; q++) {
+        const int j = j0 + tid + q * T;
+        g[q] = j < j1 ? gidx_of(j) : 0;
+    }
+    for (int i = j0 + tid; i < j1; i += D * T) {
+        Acc5 x[D];
+#pragma unroll
+        for (int q = 0; q < D; q++) {
+            const int j = i + q * T;
+            if (j < j1) x[q] = j < na ? recA[g[q]] : recB[g[q]];
         }
-        for (; i < nsrec; i += T) psx::fold_set(a, srec[i]);
+#pragma unroll
+        for (int q = 0; q < D; q++) {
+            const int j = i + (D + q) * T;
+            g[q] = j < j1 ? gidx_of(j) : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < D; q++)
+            if (i + q * T < j1) psx::fold_acc(a, x[q]);
+    }
+    psx::wave_fold_acc(a);
+    if (tid == 0) apart[item] = a;
+}
+
+__global__ __launch_bounds__(64) void k_merge_fin(DevProb P, int lo, int hi, int nch, int V,
+                                                  const SetRec* __restrict__ spart, const Acc5* __restrict__ apart,
+                                                  SetRec extra, Acc5* __restrict__ acc, SetRec* __restrict__ sacc,
+                                                  int* __restrict__ flag, int* __restrict__ sticky,
+                                                  const int* __restrict__ redo, int* __restrict__ host) {
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0) {
+        SetRec a = psx::set_zero();
+        for (int c = tid; c < nch; c += 64) psx::fold_set(a, spart[c]);
         psx::wave_fold_set(a);
         if (tid == 0) {
             SetRec g = psx::set_zero();
@@ -670,60 +805,25 @@ __global__ __launch_bounds__(kMergeThreads * kMergeWaves) void k_merge_pass_l1(D
             g.pad = atomicExch(flag, 0);
             atomicOr(sticky, g.pad);  // sticky copy for asynchronous passes (psx_sync)
             *sacc = g;
+            if (host) status_to_host(reinterpret_cast<const int*>(sacc), redo, host);
         }
         return;
     }
-    const int u = item - 1;
+    const int u = (blockIdx.x - 1) * 64 + tid;
     if (u >= P.U) return;
-    const int a0 = dptrA ? dptrA[u] : 0, na = dptrA ? dptrA[u + 1] - a0 : 0;
-    const int b0 = dptrB ? dptrB[u] : 0, nb = dptrB ? dptrB[u + 1] - b0 : 0;
-    const int n = na + nb;
-    Acc5 a = psx::acc_zero();
-    // Eight records in flight per lane, their gather indices loaded one round
-    // ahead: a merge wave holds a wave slot of the next sweep for its lifetime
-    // (one-wave sweep blocks fill every SIMD), and its lifetime is load rounds x
-    // latency — the gathered loads of the old four-deep loop (index, then record)
-    // cost the sweep beside it ~3 % at world 1 and ~5 % at world 8 (r04ai).  Each
-    // lane folds its records in record order, as before.
-#ifndef PSX_MERGE_DEPTH
-#define PSX_MERGE_DEPTH 8
-#endif
-    constexpr int D = PSX_MERGE_DEPTH;
-    auto gidx_of = [&](int j) {
-        return j < na ? (gidxA ? gidxA[a0 + j] : a0 + j) : (gidxB ? gidxB[b0 + j - na] : b0 + j - na);
-    };
-    int g[D];
+    Acc5 x[kMergeWaysMax];
 #pragma unroll
-    for (int q = 0; q < D; q++) {
-        const int j = tid + q * T;
-        g[q] = j < n ? gidx_of(j) : 0;
+    for (int v = 0; v < kMergeWaysMax; v++)
+        if (v < V) x[v] = apart[(size_t)u * V + v];
+    Acc5 g = {0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (u >= lo && u < hi) {
+        SetRec dummy;
+        eval_single(P, u, g, dummy);
     }
-    for (int i = tid; i < n; i += D * T) {
-        Acc5 x[D];
 #pragma unroll
-        for (int q = 0; q < D; q++) {
-            const int j = i + q * T;
-            if (j < n) x[q] = j < na ? recA[g[q]] : recB[g[q]];
-        }
-#pragma unroll
-        for (int q = 0; q < D; q++) {
-            const int j = i + (D + q) * T;
-            g[q] = j < n ? gidx_of(j) : 0;
-        }
-#pragma unroll
-        for (int q = 0; q < D; q++)
-            if (i + q * T < n) psx::fold_acc(a, x[q]);
-    }
-    psx::wave_fold_acc(a);
-    if (tid == 0) {
-        Acc5 g = {0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0, 0.0};
-        if (u >= lo && u < hi) {
-            SetRec dummy;
-            eval_single(P, u, g, dummy);
-        }
-        psx::fold_acc(g, a);
-        acc[u] = g;
-    }
+    for (int v = 0; v < kMergeWaysMax; v++)
+        if (v < V) psx::fold_acc(g, x[v]);
+    acc[u] = g;
 }
 
 }  // namespace
@@ -770,6 +870,11 @@ struct psx_engine {
     // fused exhaustive pass: every unit set record of the pass in one buffer
     SetRec* dpass = nullptr;
     size_t cap_pass = 0;
+    // the pass merge's partials: per scalar chunk, per (SNP, slice)
+    SetRec* dspart = nullptr;
+    size_t cap_spart = 0;
+    Acc5* dapart = nullptr;
+    size_t cap_apart = 0;
     // sweep workspace (tiled kernel)
     psx::SweepPlanCache plans;
     // generic workspace
@@ -829,6 +934,15 @@ struct psx_engine {
     static constexpr int kBufs = psx::kRecBufs;  // record buffer sets: sweep i waits for merge i - kBufs
     hipEvent_t mdone[kBufs] = {};
     bool mdone_rec[kBufs] = {};
+    bool mdone_lazy[kBufs] = {};  // merge of a single pass on the engine stream, no event recorded
+    // a single pass (nothing in flight at its call): sweep and merge on the
+    // engine stream, no dispatch events; timed by in-kernel clock stamps
+    bool a_single = false;
+    int wclk_khz = 100000;  // wall_clock64 rate (hipDeviceAttributeWallClockRate)
+    // hstat holds the status of the last merge enqueued (k_merge_fin /
+    // k_merge_partials write it to pinned host memory) and nothing that changes
+    // the status was enqueued since: psx_sync needs no read-out launch
+    bool stat_fresh = false;
     int a_par = kBufs - 1;
     hipEvent_t aev[2 * kRing] = {};
     int a_head = 0, a_pending = 0, a_count = 0;
@@ -859,7 +973,7 @@ psx_engine::~psx_engine() {
     if (stage_ev) { hipEventSynchronize(stage_ev); hipEventDestroy(stage_ev); }
     if (hstage) psx::hfree(hstage);
     if (hscore) psx::hfree(hscore);
-    psx::dfree(dgen); psx::dfree(dgcsr); psx::dfree(dbm); psx::dfree(gscratch.p); psx::dfree(dscore); psx::dfree(dsrec); psx::dfree(dmrec); psx::dfree(dpass);
+    psx::dfree(dgen); psx::dfree(dgcsr); psx::dfree(dbm); psx::dfree(gscratch.p); psx::dfree(dscore); psx::dfree(dsrec); psx::dfree(dmrec); psx::dfree(dpass); psx::dfree(dspart); psx::dfree(dapart);
     psx::sweep_free(plans);
     psx::configs_free(cfg);
     psx::dfree(d_cfg_maps);
@@ -1156,13 +1270,18 @@ int write_tag(psx_engine* e) {
 }
 
 // after a synchronous merge of partial images
+// (reported once: the word is cleared; the refused merge wrote nothing)
 int check_plan_mismatch(psx_engine* e) {
-    int bad = 0;
-    HIPCHK(hipMemcpyAsync(&bad, e->dflag + kPlanMismatchWord, sizeof(int), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    if (bad)
+    HIPCHK(hipStreamSynchronize(e->stream));  // k_merge_partials wrote the status block to hstat
+    const int* const words = reinterpret_cast<const int*>(e->hstat + 2 * sizeof(SetRec));
+    if (words[kPlanMismatchWord]) {
+        HIPCHK(hipMemsetAsync(e->dflag + kPlanMismatchWord, 0, sizeof(int), e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        e->stat_fresh = false;
         return fail(PSX_EINVAL, "merged partial images are not shards 0..world-1 of one plan "
-                                "(ranks with different PSX_K3_* knobs, builds or shard settings)");
+                                "(ranks with different PSX_K3_* knobs, builds or shard settings); "
+                                "nothing was merged");
+    }
     return 0;
 }
 
@@ -1411,17 +1530,33 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
             for (int i = 0; i < psx_engine::kBufs; i++)
                 if (!e->mdone[i]) HIPCHK(hipEventCreateWithFlags(&e->mdone[i], hipEventDisableTiming));
         }
-        S = e->cstream;
-        if (e->cstream2) {
-            S = e->a_alt ? e->cstream2 : e->cstream;
-            e->a_alt ^= 1;
+        if (e->a_pending == 0 && !e->a_single) {
+            // nothing in flight since the last psx_sync: a single pass (one locus
+            // swept once) — sweep and merge back to back on the engine stream, on
+            // the whole GPU, with no cross-stream event between them (9 us, r06a)
+            S = X;
+        } else {
+            S = e->cstream;
+            if (e->cstream2) {
+                S = e->a_alt ? e->cstream2 : e->cstream;
+                e->a_alt ^= 1;
+            }
         }
         par = e->a_par = (e->a_par + 1) % psx_engine::kBufs;
         // the merge that last read this buffer set (pass i - kBufs) must be done.
         // Host-side flow control: blocking here only when the device is more than
         // kBufs - 1 passes behind keeps barrier packets off the compute stream
         // (back-to-back sweeps then dispatch with no marker between them).
-        if (e->mdone_rec[par]) HIPCHK(hipEventSynchronize(e->mdone[par]));
+        // A single pass's merge (on X, like its sweep) records no event (an event
+        // packet put ~5 us between the merge and the caller's exchange, r06b):
+        // a later sweep on a compute stream that reuses its buffers records one
+        // on X now, which completes after that merge (X is in order).
+        if (S != X && e->mdone_lazy[par]) {
+            HIPCHK(hipEventRecord(e->mdone[par], X));
+            e->mdone_rec[par] = true;
+            e->mdone_lazy[par] = false;
+        }
+        if (S != X && e->mdone_rec[par]) HIPCHK(hipEventSynchronize(e->mdone[par]));
     }
     SetRec* const dpass = e->dpass + par * npass;
     // EXACT flag word of this buffer set ([1]: sticky word); the words share one image slot
@@ -1432,7 +1567,12 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     // re-armed by the merge that last used it (or psx_create)
     int slot = 0;
     hipEvent_t k0 = nullptr, k1 = nullptr;  // the sweep launch's own start / stop events
-    if (async) {
+    // a single pass of the k = 3 fast kernel: no dispatch events, clock stamps
+    const bool single = async && S == X && top->k == 3 && top->variant == 1;
+    unsigned long long* const stamp = single ? reinterpret_cast<unsigned long long*>(e->dflag + kStampWord) : nullptr;
+    if (single) {
+        e->plans.stamp = stamp;
+    } else if (async) {
         if (e->a_pending == psx_engine::kRing && (rc = consume_async(e))) return rc;
         slot = e->a_head;
         for (int i = 0; i < 2; i++)
@@ -1448,36 +1588,55 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
         HIPCHK(hipEventRecord(e->ev[0], S));
     }
     // the top level; level 2 (c = 3) rides in the same launch
-    if (psx::sweep_kernel(e->plans, *top, S, sa, dpass + nl, false, low, dpass, par, pflag, !async, k0, k1))
-        return fail(PSX_EHIP, std::string("sweep level ") + std::to_string(top->k) + ": " + psx::sweep_error());
-    if (async) {
+    const int src = psx::sweep_kernel(e->plans, *top, S, sa, dpass + nl, false, low, dpass, par, pflag, !async, k0, k1);
+    e->plans.stamp = nullptr;
+    if (src) return fail(PSX_EHIP, std::string("sweep level ") + std::to_string(top->k) + ": " + psx::sweep_error());
+    if (single) e->a_single = true;
+    if (async && !single) {
         e->a_head = (e->a_head + 1) % psx_engine::kRing;
         e->a_pending++;
-        HIPCHK(hipStreamWaitEvent(X, k1, 0));  // merge i after sweep i (stop event of its dispatch)
+        if (S != X) HIPCHK(hipStreamWaitEvent(X, k1, 0));  // merge i after sweep i (stop event of its dispatch)
     }
     const int lo = (int)((int64_t)e->U * e->rank / e->world), hi = (int)((int64_t)e->U * (e->rank + 1) / e->world);
     const SetRec extra = e->rank == 0 ? null_rec(e, 1.0) : psx::set_zero();
     psx::SweepPlan* mA = low ? low : top;
     psx::SweepPlan* mB = low ? top : nullptr;
+    // the pass merge (k_merge_rec + k_merge_fin): V slices per SNP run, sized
+    // from the plan's records per SNP (about 256 records per slice on average)
+    const long nrec = (long)mA->rec_len + (mB ? (long)mB->rec_len : 0);
+    const int V = (int)std::min<long>(kMergeWaysMax, std::max<long>(1, (2 * nrec / std::max(e->U, 1) + 511) / 512));
+    const long nsingle = hi - lo, nsrec = (long)(nl + nt);
+    const int nch = (int)((nsingle + nsrec + kScalChunk - 1) / kScalChunk);
+    if ((rc = ensure(e->dspart, e->cap_spart, (size_t)std::max(nch, 1)))) return rc;
+    if ((rc = ensure(e->dapart, e->cap_apart, (size_t)e->U * V))) return rc;
     // (-DPSX_ABLATE_MERGE, a separate timing build only: the pass's merge is
     // skipped and its results are wrong; measures what the merge beside the next
     // sweep costs.  No environment switch: a shipped library always merges.)
 #ifndef PSX_ABLATE_MERGE
-    hipLaunchKernelGGL(k_merge_pass_l1, dim3((e->U + 1 + kMergeWaves - 1) / kMergeWaves), dim3(kMergeThreads * kMergeWaves), 0, X, e->dp, lo, hi, psx::plan_records(*mA, par),
-                       mA->d_dptr, mA->d_gidx, mB ? psx::plan_records(*mB, par) : nullptr, mB ? mB->d_dptr : nullptr,
-                       mB ? mB->d_gidx : nullptr, dpass,
-                       (long)(nl + nt), extra, e->dacc, e->dsacc, pflag, e->dflag + 1);
+    hipLaunchKernelGGL(k_merge_rec, dim3((unsigned)(nch + (size_t)e->U * V)), dim3(64), 0, X, e->dp, lo, (int)nsingle,
+                       psx::plan_records(*mA, par), mA->d_dptr, (const int*)nullptr,  // runs contiguous (gidx identity)
+                       mB ? psx::plan_records(*mB, par) : nullptr, mB ? mB->d_dptr : nullptr, (const int*)nullptr,
+                       dpass, nsrec, nch, V, e->dspart, e->dapart, stamp);
+    hipLaunchKernelGGL(k_merge_fin, dim3(1 + (e->U + 63) / 64), dim3(64), 0, X, e->dp, lo, hi, nch, V, e->dspart,
+                       e->dapart, extra, e->dacc, e->dsacc, pflag, e->dflag + 1, (const int*)e->plans.d_redo,
+                       reinterpret_cast<int*>(e->hstat));
 #endif
     HIPCHK(hipGetLastError());
     if (async) {
-        HIPCHK(hipEventRecord(e->mdone[par], X));
-        e->mdone_rec[par] = true;
+        if (S == X) {
+            e->mdone_lazy[par] = true;
+            e->mdone_rec[par] = false;
+        } else {
+            HIPCHK(hipEventRecord(e->mdone[par], X));
+            e->mdone_rec[par] = true;
+            e->mdone_lazy[par] = false;
+        }
         *flag = 0;
+        e->stat_fresh = true;  // k_merge_fin wrote the status to hstat
         return 0;
     }
     HIPCHK(hipEventRecord(e->ev[1], X));
-    HIPCHK(hipMemcpyAsync(e->hstat, e->dsacc, kStatBytes, hipMemcpyDeviceToHost, X));
-    HIPCHK(hipStreamSynchronize(X));
+    HIPCHK(hipStreamSynchronize(X));  // (k_merge_fin wrote the status block to hstat)
     SetRec s;
     std::memcpy(&s, e->hstat, sizeof(SetRec));
     *flag = s.pad;
@@ -1539,6 +1698,11 @@ int create_impl(const psx_problem* p, const psx_ld_problem* ld, int device, psx_
     HIPCHK(hipSetDevice(device));
     psx_engine* e = new psx_engine();
     e->dev = device;
+    {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+            e->wclk_khz = khz;
+    }
     auto bail = [&](int rc) { delete e; return rc; };
     // the engine stream carries merges and the exchange: highest priority, so its
     // short kernels get wave slots ahead of the sweeps (which run on lower-
@@ -1755,7 +1919,7 @@ int create_impl(const psx_problem* p, const psx_ld_problem* ld, int device, psx_
     e->K = -spsq / 2;
     if (psx::dmalloc(&e->dpres, e->ldg) != hipSuccess ||
         psx::dmalloc(&e->dacc, sizeof(Acc5) * ((size_t)e->ldg + 3)) != hipSuccess ||
-        psx::hmalloc(&e->hstat, kStatBytes) != hipSuccess)
+        psx::hmalloc(&e->hstat, kStatBytes + 64) != hipSuccess)  // + the redo count (k_status_out)
         return bail(fail(PSX_EHIP, "out of device memory"));
     static_assert(sizeof(SetRec) == sizeof(Acc5), "SetRec occupies one image slot");
     e->dsacc = reinterpret_cast<SetRec*>(e->dacc + e->ldg);
@@ -1927,6 +2091,7 @@ void psx_destroy(psx_engine* e) { delete e; }
 int psx_set_shard(psx_engine* e, int rank, int world) {
     if (!e || world < 1 || rank < 0 || rank >= world) return fail(PSX_EINVAL, "bad shard");
     HIPCHK(hipSetDevice(e->dev));
+    e->stat_fresh = false;  // status changes: psx_sync reads it out again
     const bool moved = rank != e->rank || world != e->world;
     e->rank = rank;
     e->world = world;
@@ -1945,6 +2110,7 @@ int psx_plan_hash(psx_engine* e, uint64_t* hash) {
 
 int psx_reset(psx_engine* e) {
     HIPCHK(hipSetDevice(e->dev));
+    e->stat_fresh = false;  // status changes: psx_sync reads it out again
     int rc = reset_acc(e);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(e->stream));
@@ -1953,6 +2119,7 @@ int psx_reset(psx_engine* e) {
 
 int psx_run_exhaustive(psx_engine* e) {
     HIPCHK(hipSetDevice(e->dev));
+    e->stat_fresh = false;  // status changes: psx_sync reads it out again
     const auto t0 = std::chrono::steady_clock::now();
     int rc;
     std::memset(&e->timing, 0, sizeof(e->timing));
@@ -1969,6 +2136,7 @@ int psx_run_exhaustive(psx_engine* e) {
         if ((rc = exhaustive_pass(e, true, &gms))) return rc;
         HIPCHK(hipMemsetAsync(e->dflag + 1, 0, sizeof(int), e->stream));  // handled: clear the sticky copy
     }
+    e->stat_fresh = false;
     if ((rc = fill_timing(e, gms, flag))) return rc;
     e->timing.prepare_ms = e->prep_ms;
     e->timing.run_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1985,14 +2153,48 @@ int psx_run_exhaustive_async(psx_engine* e) {
 int psx_sync(psx_engine* e, int32_t* exact_needed) {
     HIPCHK(hipSetDevice(e->dev));
     int rc;
-    HIPCHK(hipMemcpyAsync(e->hstat, e->dsacc, kStatBytes, hipMemcpyDeviceToHost, e->stream));
-    int sticky = 0;
-    HIPCHK(hipMemcpyAsync(&sticky, e->dflag + 1, sizeof(int), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemsetAsync(e->dflag + 1, 0, sizeof(int), e->stream));
+    const bool fresh = e->stat_fresh;
+    e->stat_fresh = false;
+    if (!fresh) {
+        // one launch reads the status block and the redo count out to pinned host
+        // memory and re-arms the sticky EXACT flag and the plan-mismatch word
+        hipLaunchKernelGGL(k_status_out, dim3(1), dim3(64), 0, e->stream, reinterpret_cast<int*>(e->dsacc),
+                           (const int*)e->plans.d_redo, reinterpret_cast<int*>(e->hstat));
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipStreamSynchronize(e->stream));
-    if (*(const int*)(e->hstat + 2 * sizeof(SetRec) + kPlanMismatchWord * sizeof(int)))
-        return fail(PSX_EINVAL, "merged partial images are not shards 0..world-1 of one plan "
-                                "(ranks with different PSX_K3_* knobs, builds or shard settings)");
+    const int* const words = reinterpret_cast<const int*>(e->hstat + 2 * sizeof(SetRec));
+    const int sticky = words[1];
+    const int redo = *reinterpret_cast<const int*>(e->hstat + kStatBytes);
+    if (fresh && (sticky || words[kPlanMismatchWord])) {
+        // the last merge wrote the status (no read-out launch): re-arm the words
+        // the host consumes here (raised flags only: the common pass skips this)
+        HIPCHK(hipMemsetAsync(e->dflag + 1, 0, sizeof(int), e->stream));
+        HIPCHK(hipMemsetAsync(e->dflag + kPlanMismatchWord, 0, sizeof(int), e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+    }
+    if (e->a_single) {
+        // the single pass's sweep: its first block's start to the merge's first
+        // block's start (in-kernel wall clocks; the merge starts ~1 us after the
+        // sweep's end)
+        unsigned long long t[2];
+        std::memcpy(t, words + kStampWord, sizeof(t));
+        const double ms = t[1] > t[0] ? (double)(t[1] - t[0]) / (double)e->wclk_khz : 0.0;
+        if (e->a_count == 0 && e->a_pending == 0) e->a_span = 0;
+        e->a_kms += ms;
+        e->a_span += ms;
+        e->a_count++;
+        e->a_single = false;
+    }
+    // a refused merge of partial images (k_merge_partials wrote nothing) is
+    // reported after the pass bookkeeping below, once (k_status_out cleared it)
+    const bool mismatch = words[kPlanMismatchWord] != 0;
+    auto done = [&]() {
+        return mismatch ? fail(PSX_EINVAL, "merged partial images are not shards 0..world-1 of one plan "
+                                           "(ranks with different PSX_K3_* knobs, builds or shard settings); "
+                                           "nothing was merged")
+                        : 0;
+    };
     if (exact_needed) *exact_needed = sticky;
     if (e->a_pending == 0 && e->a_count == 0) {
         // nothing asynchronous since the last sync: the count still follows the
@@ -2000,7 +2202,7 @@ int psx_sync(psx_engine* e, int32_t* exact_needed) {
         SetRec st;
         std::memcpy(&st, e->hstat, sizeof(SetRec));
         e->timing.configs = (uint64_t)(st.npat + 0.5);
-        return 0;
+        return done();
     }
     while (e->a_pending > 0)
         if ((rc = consume_async(e))) return rc;
@@ -2022,7 +2224,7 @@ int psx_sync(psx_engine* e, int32_t* exact_needed) {
     e->timing.alg_bytes = top->alg_bytes + top->fused_bytes;
     e->timing.flops = top->flops + top->fused_flops;
     e->timing.exact_rerun = sticky;
-    if (psx::sweep_redo_count(e->plans, &e->timing.robust_units)) return fail(PSX_EHIP, psx::sweep_error());
+    e->timing.robust_units = redo;
     SetRec st;
     std::memcpy(&st, e->hstat, sizeof(SetRec));
     e->timing.configs = (uint64_t)(st.npat + 0.5);
@@ -2030,7 +2232,7 @@ int psx_sync(psx_engine* e, int32_t* exact_needed) {
     e->a_count = 0;
     e->a_first = -1;
     e->a_span = 0;
-    return 0;
+    return done();
 }
 
 }  // extern "C"
@@ -2073,6 +2275,7 @@ extern "C" {
 int psx_eval_union_batch(psx_engine* e, const int32_t* sets, int32_t stride, int32_t n_sets, int accumulate,
                          double* score_out) {
     HIPCHK(hipSetDevice(e->dev));
+    e->stat_fresh = false;  // status changes: psx_sync reads it out again
     const auto t0 = std::chrono::steady_clock::now();
     if (stride < 1 || stride > PSX_KMAX) return fail(PSX_ERANGE, "stride outside [1, 6]");
     if (n_sets < 0 || (n_sets > 0 && !sets)) return fail(PSX_EINVAL, "bad set batch");
@@ -2083,6 +2286,21 @@ int psx_eval_union_batch(psx_engine* e, const int32_t* sets, int32_t stride, int
     const size_t per = (size_t)kBatchChunks * (size_t)(512 / stride);
     double kms = 0, prep = 0;
     int rc;
+    if ((size_t)n_sets > per) {
+        // more than one slice: every slice is merged before the next one is
+        // validated on the device, so the whole batch is checked here first (the
+        // device rule: members >= 0 strictly ascending and < U, negatives are
+        // padding) — a bad row anywhere adds nothing to the accumulators
+        for (size_t r = 0; r < (size_t)n_sets; r++) {
+            int prev = -1;
+            for (int j = 0; j < stride; j++) {
+                const int v = sets[r * stride + j];
+                if (v < 0) continue;
+                if (v >= e->U || v <= prev) return fail(PSX_EINVAL, "sets must be ascending union indices");
+                prev = v;
+            }
+        }
+    }
     for (size_t s0 = 0; s0 < (size_t)n_sets; s0 += per) {
         const size_t nb = std::min(per, (size_t)n_sets - s0);
         const auto ts = std::chrono::steady_clock::now();
@@ -2107,6 +2325,7 @@ int psx_eval_union_batch(psx_engine* e, const int32_t* sets, int32_t stride, int
 
 int psx_run_configs(psx_engine* e, const int16_t* rows, int64_t n_rows, int32_t n_groups) {
     HIPCHK(hipSetDevice(e->dev));
+    e->stat_fresh = false;  // status changes: psx_sync reads it out again
     int rc;
     if ((rc = reset_acc(e))) return rc;
     std::memset(&e->timing, 0, sizeof(e->timing));
@@ -2642,6 +2861,7 @@ int sss_workspace(psx_engine* e, size_t nmax, int world, hipStream_t s) {
 
 int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* iterations_out) {
     HIPCHK(hipSetDevice(e->dev));
+    e->stat_fresh = false;  // status changes: psx_sync reads it out again
     const int rank = allgather ? e->rank : 0, world = allgather ? e->world : 1;
     int rc;
     if ((rc = reset_acc(e))) return rc;
@@ -2951,8 +3171,24 @@ int64_t psx_partials_bytes(psx_engine* e) { return (int64_t)(sizeof(Acc5) * ((si
 int psx_export_partials(psx_engine* e, void* dst) {
     HIPCHK(hipSetDevice(e->dev));
     // per-SNP slots, the SetRec slot and the PlanTag are contiguous: the image is one copy
-    HIPCHK(hipMemcpyAsync(dst, e->dacc, sizeof(Acc5) * ((size_t)e->ldg + 2), hipMemcpyDeviceToDevice, e->stream));
+    // a copy kernel: it follows the merge kernels on the stream without the
+    // blit path's extra dependency packets (hipMemcpyAsync D2D: +6 us gap, r06a)
+    const size_t n16 = sizeof(Acc5) * ((size_t)e->ldg + 2) / 16;
+    static_assert(sizeof(Acc5) % 16 == 8 || sizeof(Acc5) % 16 == 0, "image of whole 8-byte words");
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) || (sizeof(Acc5) * ((size_t)e->ldg + 2)) % 16) {
+        HIPCHK(hipMemcpyAsync(dst, e->dacc, sizeof(Acc5) * ((size_t)e->ldg + 2), hipMemcpyDeviceToDevice, e->stream));
+    } else {
+        hipLaunchKernelGGL(k_copy_image, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, e->stream,
+                           reinterpret_cast<const int4*>(e->dacc), n16, reinterpret_cast<int4*>(dst));
+        HIPCHK(hipGetLastError());
+    }
     if (!e->external_stream) HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int psx_partials_device_ptr(psx_engine* e, void** device_ptr) {
+    if (!e || !device_ptr) return fail(PSX_EINVAL, "bad argument");
+    *device_ptr = e->dacc;  // slots 0 .. ldg + 1: the exported image
     return 0;
 }
 
@@ -2973,9 +3209,11 @@ int psx_merge_partials(psx_engine* e, const void* src, int32_t count) {
     HIPCHK(hipSetDevice(e->dev));
     if (count < 1) return fail(PSX_EINVAL, "count < 1");
     // one-wave blocks: they take the first wave slots a running sweep frees
-    hipLaunchKernelGGL(k_merge_partials, dim3((e->U + 63) / 64), dim3(64), 0, e->stream, (const Acc5*)src, e->U,
-                       e->ldg, count, e->dacc, e->dsacc, e->dflag);
+    hipLaunchKernelGGL(k_merge_partials, dim3((e->U + 63) / 64 + 1), dim3(64), 0, e->stream, (const Acc5*)src, e->U,
+                       e->ldg, count, e->dacc, e->dsacc, e->dflag, (const int*)e->plans.d_redo,
+                       reinterpret_cast<int*>(e->hstat));
     HIPCHK(hipGetLastError());
+    e->stat_fresh = true;  // k_merge_partials wrote the status to hstat
     if (e->external_stream) return 0;  // a tag mismatch is reported by psx_sync
     return check_plan_mismatch(e);
 }

@@ -5,8 +5,11 @@
 // records (t < 64), the b records (64 <= t < 128) and, for k = 3, the a
 // records (t >= 128) of each unit.  The merges need, per union SNP u, the
 // record slots that hold u in increasing slot order (a stable grouping by SNP):
-//   pos[i]   = i when slot i holds a SNP, else -1 (the sweep kernels skip it)
-//   gidx[q]  = the q-th record slot in (SNP, slot) order
+//   pos[i]   = the buffer position of slot i's record, -1: no SNP (the sweep
+//              kernels skip it); since r06 its CSR position q (below), so each
+//              SNP's records are contiguous in the buffer
+//   gidx[q]  = the buffer position of the q-th record in (SNP, slot) order
+//              (the identity since r06)
 //   dptr[u]  = first q of SNP u (dptr[U] = records in all): u's run is
 //              [dptr[u], dptr[u + 1])
 // Built on the host this was ~2M-element passes (8 ms per locus on the
@@ -51,6 +54,20 @@ __global__ void k_plan_keys(const int4* __restrict__ units, long n, int rec_stri
     keys[i] = key >= 0 ? key : U;  // no SNP: sorted behind every SNP
     vals[i] = (int)i;
     pos[i] = key >= 0 ? (int)i : -1;
+}
+
+// Records at their CSR positions (r06): slot gidx[q] is written at position q,
+// so each SNP's run is contiguous in the record buffer (the pass merge reads it
+// coalesced instead of gathering 56-byte records across units; the sweeps'
+// stores scatter instead: measured neutral at world 1 in r04al), and gidx
+// becomes the identity for every other merge of the plan's records.
+__global__ void k_plan_csr_pos(const int* __restrict__ dptr, int U, long n, int* __restrict__ gidx,
+                               int* __restrict__ pos) {
+    const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n || q >= dptr[U]) return;
+    const int slot = gidx[q];
+    pos[slot] = (int)q;
+    gidx[q] = (int)q;
 }
 
 // keys of a flat record array (record i's SNP, -1: none)
@@ -113,10 +130,14 @@ int sort_to_csr(long n, int U, int* d_dptr, int* d_gidx, PlanScratch& S, hipStre
 int plan_csr_device(const int4* d_units, int n_units, int rec_stride, int k, int variant, int pad, int U, int* d_pos,
                     int* d_dptr, int* d_gidx, PlanScratch& S, hipStream_t st) {
     const long n = (long)n_units * rec_stride;
-    return sort_to_csr(n, U, d_dptr, d_gidx, S, st, [&](int* keys, int* vals) {
-        hipLaunchKernelGGL(k_plan_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d_units, n, rec_stride,
-                           k, variant, pad, U, keys, vals, d_pos);
-    });
+    if (sort_to_csr(n, U, d_dptr, d_gidx, S, st, [&](int* keys, int* vals) {
+            hipLaunchKernelGGL(k_plan_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d_units, n,
+                               rec_stride, k, variant, pad, U, keys, vals, d_pos);
+        }))
+        return -1;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_plan_csr_pos, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d_dptr, U, n, d_gidx, d_pos);
+    return chk(hipGetLastError());
 }
 
 // the CSR of records laid out flat with SNP keys[i] (-1: none): dptr[U + 1],

@@ -111,6 +111,7 @@ struct Sweep3Args {
     int U, ldg, pad, Ck;
     unsigned long long* trace = nullptr;  // diagnostics (PSX_UNIT_TRACE): per unit {start, end, hw id, unit}
     int* redo_count = nullptr;            // units redone by the robust variant (cumulative)
+    unsigned long long* tstamp = nullptr; // single passes: block 0 stores its start clock (wall_clock64) here
 };
 // most a per k = 3 unit (plan_units3c): the fast kernel stages the unit's
 // per-a scalars in LDS
@@ -191,6 +192,7 @@ struct SweepPlanCache {
     int* d_redo = nullptr;  // k = 3 units redone by the robust variant since creation
     int* d_flag = nullptr;  // raised when a set needs the EXACT notSharedLL variant
     bool own_flag = true;   // false: d_flag lives in the engine's status block
+    unsigned long long* stamp = nullptr;  // the next k = 3 fast launch's start clock (null: none)
 };
 
 bool sweep_supports(int k, int U);

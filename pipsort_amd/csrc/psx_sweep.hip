@@ -655,9 +655,10 @@ static void host_plan_csr(const SweepPlan& P, const std::vector<int4>& hu, std::
     std::vector<int> fill(dptr.begin(), dptr.end() - 1);
     pos.assign(key.size(), -1);
     for (size_t i = 0; i < key.size(); i++)
-        if (key[i] >= 0) {
-            gidx[fill[key[i]]++] = (int)i;
-            pos[i] = (int)i;
+        if (key[i] >= 0) {  // slot i's record at its CSR position (stable in slot order)
+            const int q = fill[key[i]]++;
+            gidx[q] = q;
+            pos[i] = q;
         }
 }
 
@@ -702,11 +703,12 @@ static int build_plan(SweepPlan& P, int k, int U, int ldg, int rank, int world, 
         P.h_units[i] = variant ? make_int4(mine[i].a0, mine[i].a1, mine[i].B | (mine[i].j0 << 16),
                                            mine[i].T | (mine[i].j1 << 16))
                                : make_int4(mine[i].a0, mine[i].a1, mine[i].B, mine[i].T);
-    // Records are unit-major: the kernels write record slot i at position i
-    // (pos[i] = -1: no SNP), so a unit's 64 c (b) records are contiguous and the
-    // stores coalesce; the merges gather each SNP's records through gidx, in
-    // record order (same fold order as a per-SNP layout; same-box A/B against
-    // writing each record at its CSR position: world 1 -0.4 %, world 8 -1 %)
+    // Records at their CSR positions (since r06): the kernels write record slot
+    // i at pos[i] (-1: no SNP), each SNP's run contiguous in slot order, so the
+    // pass merge reads it coalesced (r01-r05 wrote slot i at i, unit-major, and
+    // the merges gathered through gidx: the single-pass merge then ran at ~2.6
+    // TB/s of records; the sweeps' scattered stores measured neutral at world 1
+    // and 0-2 % slower at world 8 in r04al, when the merge was hidden anyway)
     P.rec_len = (size_t)P.n_units * P.rec_stride;
     return 0;
 }
@@ -1039,6 +1041,7 @@ int sweep_kernel(SweepPlanCache& C, SweepPlan& P, hipStream_t st, const SweepArg
     const dim3 g(P.n_units), blk(64);
     if (k == 3 && !exact) {
         Sweep3Args S3 = sweep3_args(C, a, U, ldg);
+        S3.tstamp = C.stamp;
         Level2Blocks b{0, TileArgs{}, nullptr, nullptr, nullptr, nullptr};
         if (ride) {  // level 2 in the same launch: its units are the first blocks of the grid
             Acc5* rec2 = plan_records(*l2, parity);

@@ -1589,6 +1589,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PSX_K3_WAVES
                                                   Acc5* __restrict__ rec2, SetRec* __restrict__ srec2,
                                                   const int* __restrict__ pos2) {
     __shared__ SweepSmem sm;
+    // a single pass times its sweep without dispatch events (their packets left
+    // ~5 us between the sweep and the merge): the launch's first block stamps
+    // its start, the merge's first block its own (k_merge_rec)
+    if (A.tstamp && blockIdx.x == 0 && threadIdx.x == 0) *A.tstamp = wall_clock64();
     if ((int)blockIdx.x >= nk3) {
         sweep_unit<2, false>(A2, blockIdx.x - nk3, units2, rec2, srec2, 128, flag, pos2, sm.u2);
         return;

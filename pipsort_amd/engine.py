@@ -34,7 +34,7 @@ EXPORTED = [
     "psx_abi_version", "psx_overlap_cus", "psx_last_error", "psx_device_count", "psx_warmup", "psx_warmup_for", "psx_create", "psx_destroy",
     "psx_set_shard", "psx_run_exhaustive", "psx_run_configs", "psx_run_sss",
     "psx_eval_union_batch", "psx_reset", "psx_get_accum", "psx_partials_bytes",
-    "psx_export_partials", "psx_merge_partials", "psx_get_timing", "psx_count_configs",
+    "psx_export_partials", "psx_partials_device_ptr", "psx_merge_partials", "psx_get_timing", "psx_count_configs",
     "psx_fold_partials_host", "psx_plan_hash", "psx_plan_build_ms", "psx_plan_csr_selftest", "psx_shard_stats", "psx_plan_units_k3", "psx_set_stream",
     "psx_psd_shift", "psx_lowrank_study", "psx_sym_eigen", "psx_lu_det",
     "psx_create_from_ld", "psx_psd_shift_gpu", "psx_lu_det_gpu", "psx_elim_gpu",
@@ -178,6 +178,7 @@ def load_library(path: str = LIB_PATH):
         "psx_get_accum": (c_int, [vp, P(_Accum)]),
         "psx_partials_bytes": (c_i64, [vp]),
         "psx_export_partials": (c_int, [vp, vp]),
+        "psx_partials_device_ptr": (c_int, [vp, ctypes.POINTER(vp)]),
         "psx_merge_partials": (c_int, [vp, vp, c_i32]),
         "psx_get_timing": (c_int, [vp, P(Timing)]),
         "psx_count_configs": (c_u64, [P(_Problem)]),
@@ -220,8 +221,8 @@ def load_library(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.psx_abi_version() != 3 and os.environ.get("PSX_AB") != "1":
-        raise EngineError(PSX_ENODEV, f"{path}: ABI version {lib.psx_abi_version()}, this module needs 3")
+    if lib.psx_abi_version() != 4 and os.environ.get("PSX_AB") != "1":
+        raise EngineError(PSX_ENODEV, f"{path}: ABI version {lib.psx_abi_version()}, this module needs 4")
     _lib = lib
     return lib
 
@@ -743,5 +744,34 @@ class PostCal:
     def export_partials(self, device_ptr: int):
         _check(self.lib.psx_export_partials(self.h, ctypes.c_void_p(device_ptr)))
 
+    def partials_device_ptr(self) -> int:
+        """Device address of the handle's own partial image (read in place by a
+        collective instead of an exported copy; valid until the next pass /
+        merge / reset on this handle)."""
+        p = ctypes.c_void_p()
+        _check(self.lib.psx_partials_device_ptr(self.h, ctypes.byref(p)))
+        return int(p.value)
+
+    def partials_tensor(self):
+        """The handle's own partial image as a uint8 torch tensor on its device
+        (no copy: a view of psx_partials_device_ptr, for the collective to read
+        in place)."""
+        return device_bytes(self.partials_device_ptr(), self.partials_bytes())
+
     def merge_partials(self, device_ptr: int, count: int):
         _check(self.lib.psx_merge_partials(self.h, ctypes.c_void_p(device_ptr), int(count)))
+
+
+class _DeviceSpan:
+    """__cuda_array_interface__ of nbytes of device memory at ptr (uint8)."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {"shape": (int(nbytes),), "typestr": "|u1", "data": (int(ptr), False),
+                                         "version": 3, "strides": None}
+
+
+def device_bytes(ptr: int, nbytes: int):
+    """A uint8 torch tensor viewing nbytes of device memory at ptr (no copy; the
+    memory stays owned by the engine)."""
+    import torch
+    return torch.as_tensor(_DeviceSpan(ptr, nbytes), device="cuda")

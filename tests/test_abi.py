@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
     for name in decl:
         assert re.search(rf"\bT {name}\b", dyn), name
         assert getattr(lib, name)
-    assert lib.psx_abi_version() == 3  # 3: psx_timing.prepare_ms / run_ms, setup phases, partial-image PlanTag
+    assert lib.psx_abi_version() == 4  # 3: psx_timing.prepare_ms / run_ms, setup phases, partial-image PlanTag; 4: psx_partials_device_ptr
 
 
 def test_no_cpu_fallback():

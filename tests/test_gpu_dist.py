@@ -161,3 +161,54 @@ def test_merge_refuses_mismatched_plans(gpu):
             merge(h[0], 0, 2, h[2], 1, 2)
     for x in h:
         x.close()
+
+
+def test_refused_merge_leaves_handle_usable(gpu):
+    """A refused merge writes nothing and is reported once: the same merge
+    handle keeps its accumulators bitwise, and the next good merge (and the
+    next psx_sync) succeed.  With a caller stream the refusal comes from
+    psx_sync, after its pass bookkeeping."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, ROOT)
+    from pipsort_amd import engine as E
+    from pipsort_amd import synth
+    ld, z, _, _, u2l = synth.syn_v1(120)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=2, sharing_param=0.25)
+    a, b, m = E.PostCal(seam), E.PostCal(seam), E.PostCal(seam)
+    nb = a.partials_bytes()
+    good = torch.empty(2 * nb, dtype=torch.uint8, device="cuda")
+    bad = torch.empty(2 * nb, dtype=torch.uint8, device="cuda")
+    for dst, (r0, r1) in ((good, (0, 1)), (bad, (1, 0))):
+        a.set_shard(r0, 2)
+        b.set_shard(r1, 2)
+        a.run_exhaustive()
+        b.run_exhaustive()
+        a.export_partials(dst.data_ptr())       # bad: rank 1's image first
+        b.export_partials(dst.data_ptr() + nb)
+    torch.cuda.synchronize()
+    fields = ("post", "shared", "shared_ll", "notshared_ll", "no_causal")
+
+    def snap():
+        r = m.accum()
+        return r.n_configs, np.float64(r.total).tobytes(), [np.asarray(getattr(r, f)).tobytes() for f in fields]
+
+    m.merge_partials(good.data_ptr(), 2)
+    ref = snap()
+    assert ref[0] == seam.count_configs()
+    with pytest.raises(E.EngineError, match="one plan"):
+        m.merge_partials(bad.data_ptr(), 2)
+    assert snap() == ref                       # nothing folded
+    m.merge_partials(good.data_ptr(), 2)       # reported once: the handle merges again
+    assert snap() == ref
+    assert not m.sync()
+    # caller's stream: no host check in merge_partials; psx_sync reports it once
+    stream = torch.cuda.Stream()
+    m.set_stream(stream.cuda_stream)
+    m.merge_partials(bad.data_ptr(), 2)
+    with pytest.raises(E.EngineError, match="one plan"):
+        m.sync()
+    assert not m.sync()
+    assert snap() == ref
+    for x in (a, b, m):
+        x.close()

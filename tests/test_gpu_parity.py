@@ -478,6 +478,29 @@ def test_union_batch_rejects_bad_rows(gpu, row):
     assert np.array_equal(pc.eval_union_batch(good, accumulate=False), s0)
 
 
+def test_union_batch_rejects_bad_row_past_first_slice(gpu):
+    """A batch of several device slices (43,520 rows per slice at stride 3) with
+    one bad row in the second slice: the call fails with EINVAL and adds
+    nothing — the first slice is not merged before the bad row is seen."""
+    ld, z, _, _, u2l = synth.syn_v1(90)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    pc = E.PostCal(seam)
+    rng = np.random.default_rng(7)
+    rows = np.sort(np.stack([rng.choice(90, 3, replace=False) for _ in range(60_000)]), axis=1).astype(np.int32)
+    pc.eval_union_batch(rows[:10], accumulate=True)
+    before = pc.accum()
+    bad = rows.copy()
+    bad[50_000] = [4, 4, 9]
+    with pytest.raises(E.EngineError) as ei:
+        pc.eval_union_batch(bad, accumulate=True)
+    assert ei.value.code == E.PSX_EINVAL
+    after = pc.accum()
+    for f in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+        assert np.array_equal(getattr(before, f), getattr(after, f)), f
+    assert before.total == after.total and before.n_configs == after.n_configs
+    pc.close()
+
+
 @pytest.mark.parametrize("stride,k", [(1, 1), (6, 6), (6, 4)])
 def test_union_batch_strides(gpu, stride, k):
     """The device batch path at the stride extremes: one row per SNP (stride
