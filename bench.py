@@ -783,6 +783,38 @@ def main():
         return elapsed, kms, launches, exact
 
     elapsed, kms, launches, exact = timed()
+
+    def single_passes(n=15):
+        """One locus swept once (what a real per-locus run and the CLI see): each
+        pass = psx_run_exhaustive_async + (N > 1) the exchange + psx_sync, with
+        nothing overlapping the next pass; median host wall per pass (all ranks
+        start together: barrier before each)."""
+        ws = []
+        for i in range(n + 2):
+            if use_dist:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            pc.run_exhaustive_async()
+            if use_dist:
+                if backend == "nccl":
+                    dist.all_gather_into_tensor(gathered, mine_view)  # the image read in place
+                else:
+                    parts = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
+                    dist.all_gather(parts, mine_view.cpu())
+                    gathered.copy_(torch.cat(parts))
+                pc.merge_partials(gathered.data_ptr(), world)
+            pc.sync()
+            dt = (time.perf_counter() - t0) * 1e3
+            if i >= 2:
+                ws.append(dt)
+        if use_dist:
+            x = torch.tensor(ws, dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+            dist.all_reduce(x, op=dist.ReduceOp.MAX)
+            ws = x.tolist()
+        ws.sort()
+        return ws[len(ws) // 2]
+
     if exact and use_async:
         # some pass needs the exact notSharedLL variant: the asynchronous results
         # are not valid, time the validated synchronous path instead
@@ -795,6 +827,8 @@ def main():
         elapsed = float(x.item())
     tm = pc.timing()
     torch.cuda.synchronize()
+    mine_view = pc.partials_tensor() if use_dist else None
+    single_pass_ms = single_passes() if use_async else None  # after the timed region (and its timing)
     acc = pc.accum() if (world == 1 or rank == 0) else None
 
     sss_line = None
@@ -887,6 +921,10 @@ def main():
             "setup": {"synthetic_locus_s": t_synth, "gpu_model_setup_and_create_ms": pc.setup_info["setup_ms"],
                       "psd_added": pc.setup_info["psd_added"], "eigen_route": pc.setup_info["eigen_route"]},
             "pass_mode": "async (no host sync per step)" if use_async else "synchronous",
+            "single_pass_ms": single_pass_ms,
+            "single_pass_note": "one pass of this rank's shard from the host call to merged accumulators "
+                                "(psx_run_exhaustive_async + exchange + psx_sync, nothing overlapping), median of "
+                                "15, max over ranks; setup excluded — the latency of sweeping one locus once",
             # CUs kept for the merges / exchange beside overlapped passes (one XCD
             # at world >= 8 by default, PSX_OVERLAP overrides; 0: not overlapped)
             "overlap_reserved_cus": pc.overlap_cus(),

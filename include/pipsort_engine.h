@@ -97,6 +97,13 @@ int32_t psx_overlap_cus(const psx_engine *e);
 
 /* Number of HIP devices visible (0 on a host without a GPU; never initialises a context). */
 int psx_device_count(int *count);
+/* The engine keeps freed device and pinned host blocks in a caching pool (up to
+ * 4 GiB per device, 1 GiB pinned) for the next handle.  psx_pool_trim gives the
+ * cached (free) blocks back to the HIP runtime — e.g. before a co-resident
+ * framework needs the memory; blocks in use are untouched.
+ * psx_pool_cached_bytes: bytes cached now. */
+int psx_pool_trim(void);
+int64_t psx_pool_cached_bytes(void);
 
 /* Optional (no reference counterpart): bring up the HIP runtime and context of
  * `device` and load the engine's device code, so the first psx_create* does not

@@ -1530,7 +1530,10 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
             for (int i = 0; i < psx_engine::kBufs; i++)
                 if (!e->mdone[i]) HIPCHK(hipEventCreateWithFlags(&e->mdone[i], hipEventDisableTiming));
         }
-        if (e->a_pending == 0 && !e->a_single) {
+        // (PSX_SERIAL=1, A/B: every asynchronous pass on the engine stream, the
+        // merges between the sweeps instead of beside the next one)
+        static const bool serial = getenv("PSX_SERIAL") && atoi(getenv("PSX_SERIAL")) != 0;
+        if ((e->a_pending == 0 && !e->a_single) || serial) {
             // nothing in flight since the last psx_sync: a single pass (one locus
             // swept once) — sweep and merge back to back on the engine stream, on
             // the whole GPU, with no cross-stream event between them (9 us, r06a)
@@ -1655,6 +1658,12 @@ extern "C" {
 int32_t psx_abi_version(void) { return PSX_ABI_VERSION; }
 int32_t psx_overlap_cus(const psx_engine* e) { return e ? e->ovl : -1; }
 const char* psx_last_error(void) { return g_err.c_str(); }
+
+int psx_pool_trim(void) {
+    psx::pool_trim();
+    return 0;
+}
+int64_t psx_pool_cached_bytes(void) { return (int64_t)psx::pool_cached_bytes(); }
 
 int psx_device_count(int* count) {
     int c = 0;
@@ -2532,7 +2541,10 @@ enum { kUnseen = 0, kNulls = 1, kCurPos = 2, kCurNull = 3, kNCnt = 4 };
 // One rank: every neighbour's weight and mark go to pinned host memory from
 // here.  The weight is stored first, then, once that store is acknowledged, the
 // mark word (iteration tag << 32 | mark); both at system scope (write-through,
-// no L2 write-back).  The host takes neighbour i when its word carries this
+// no L2 write-back) into coherent pinned memory (hipHostMallocCoherent, uncached
+// for the device: an acknowledged store is in host memory, so the mark cannot
+// overtake the weight; a release store at system scope would add an L2
+// write-back per wave, measured 13 -> 21 us per eval in r05).  The host takes neighbour i when its word carries this
 // iteration's tag: no wait for the kernel's end (~5-8 us before its stop event
 // completes) and no contended completion counter.
 __device__ inline void publish_mark(double* lk_host, unsigned long long* mark_host, int i, double w, int mk,
@@ -2832,8 +2844,10 @@ int sss_workspace(psx_engine* e, size_t nmax, int world, hipStream_t s) {
         D.lk = nullptr;
         HIPCHK(psx::dmalloc(&D.rows, nmax * PSX_KMAX * sizeof(int)));
         HIPCHK(psx::dmalloc(&D.mark, nmax * sizeof(int)));
-        HIPCHK(psx::hmalloc(reinterpret_cast<void**>(&D.lk), nmax * sizeof(double)));
-        HIPCHK(psx::hmalloc(reinterpret_cast<void**>(&D.hmark), nmax * sizeof(unsigned long long)));
+        // coherent: the eval's weight / mark-word hand-off (publish_mark) relies on
+        // device stores reaching host memory in acknowledgement order
+        HIPCHK(psx::hmalloc_coherent_raw(reinterpret_cast<void**>(&D.lk), nmax * sizeof(double)));
+        HIPCHK(psx::hmalloc_coherent_raw(reinterpret_cast<void**>(&D.hmark), nmax * sizeof(unsigned long long)));
         std::memset(D.hmark, 0, nmax * sizeof(unsigned long long));  // tag 0: no iteration
         D.nmax = nmax;
     }

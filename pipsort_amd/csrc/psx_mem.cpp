@@ -45,8 +45,10 @@ size_t size_class(size_t bytes) {
     return (bytes + mb - 1) / mb * mb;
 }
 
+// dev -1: pinned host, -2: pinned host, coherent (hipHostMallocCoherent: device
+// stores reach host memory uncached, in order of their acknowledgement)
 hipError_t raw_alloc(void** p, size_t cls, int dev) {
-    return dev < 0 ? hipHostMalloc(p, cls) : hipMalloc(p, cls);
+    return dev == -2 ? hipHostMalloc(p, cls, hipHostMallocCoherent) : dev < 0 ? hipHostMalloc(p, cls) : hipMalloc(p, cls);
 }
 
 hipError_t raw_free(void* p, int dev) { return dev < 0 ? hipHostFree(p) : hipFree(p); }
@@ -69,9 +71,9 @@ void drain(Pool& P, int dev) {
     for (auto& b : out) (void)raw_free(b.first, b.second);
 }
 
-hipError_t alloc(void** p, size_t bytes, bool host) {
+hipError_t alloc(void** p, size_t bytes, bool host, bool coherent = false) {
     *p = nullptr;
-    int dev = -1;
+    int dev = coherent ? -2 : -1;
     if (!host && hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
     const size_t cls = size_class(bytes);
     Pool& P = pool();
@@ -166,6 +168,7 @@ hipError_t dmalloc_raw(void** p, size_t bytes) {
 }
 hipError_t dfree(void* p) { return release(p, false); }
 hipError_t hmalloc_raw(void** p, size_t bytes) { return alloc(p, bytes, true); }
+hipError_t hmalloc_coherent_raw(void** p, size_t bytes) { return alloc(p, bytes, true, true); }
 hipError_t hfree(void* p) { return release(p, true); }
 hipError_t dfree_idle(void* p) { return release(p, false, false); }
 IdleScope::IdleScope() { g_idle++; }
@@ -210,6 +213,25 @@ void stream_put(hipStream_t s, int priority) {
     StreamPool& P = streams();
     std::lock_guard<std::mutex> g(P.mu);
     P.idle[{dev, priority}].push_back(s);
+}
+
+void pool_trim() {
+    Pool& P = pool();
+    std::vector<std::pair<void*, int>> out;
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        for (auto& kv : P.free)
+            for (void* b : kv.second) out.push_back({b, kv.first.first});
+        P.free.clear();
+        P.cached.clear();
+    }
+    int cur = 0;
+    const bool have = hipGetDevice(&cur) == hipSuccess;
+    for (auto& b : out) {
+        if (b.second >= 0 && have && b.second != cur) (void)hipSetDevice(b.second);
+        (void)raw_free(b.first, b.second);
+        if (b.second >= 0 && have && b.second != cur) (void)hipSetDevice(cur);
+    }
 }
 
 size_t pool_cached_bytes() {

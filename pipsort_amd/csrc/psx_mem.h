@@ -19,6 +19,7 @@ namespace psx {
 hipError_t dmalloc_raw(void** p, size_t bytes);
 hipError_t dfree(void* p);
 hipError_t hmalloc_raw(void** p, size_t bytes);  // pinned host memory
+hipError_t hmalloc_coherent_raw(void** p, size_t bytes);  // pinned host memory, coherent (device -> host hand-offs)
 hipError_t hfree(void* p);
 
 template <typename T>
@@ -41,6 +42,9 @@ struct IdleScope {
 };
 
 // bytes currently held by the cache (all devices + pinned host), for tests
+// release every cached (free) block of every device and the pinned host pools
+// (live blocks are untouched); psx_pool_trim in the C ABI
+void pool_trim();
 size_t pool_cached_bytes();
 
 // Streams: creating a HIP stream costs ~3-20 ms on MI355X (a hardware queue)

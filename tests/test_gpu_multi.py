@@ -5,6 +5,7 @@ peer copies replaced by same-device copies."""
 import os
 import shutil
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -15,6 +16,7 @@ from pipsort_amd import engine as E
 from pipsort_amd import synth
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _same(a, b, pip_tol=1e-12, ll_rtol=1e-12):
@@ -209,3 +211,33 @@ def test_multi_device_lists_fold_identically_on_one_gpu(gpu):
     _bitwise(a.accum(), b.accum())
     a.close()
     b.close()
+
+
+def test_pool_trim_releases_cached_blocks(gpu):
+    """Freed engine buffers stay cached for the next handle; psx_pool_trim gives
+    them back (a co-resident framework can then allocate the memory)."""
+    ld, z, _, _, u2l = synth.syn_v1(150)
+    seam = E.seam_from_arrays(ld, z, u2l, (10000, 8000), max_causal=3, sharing_param=0.25)
+    pc = E.PostCal(seam)
+    pc.run_exhaustive()
+    pc.close()
+    assert E.pool_cached_bytes() > 0
+    E.pool_trim()
+    assert E.pool_cached_bytes() == 0
+    pc = E.PostCal(seam)  # the pool refills from the runtime
+    pc.run_exhaustive()
+    assert pc.accum().n_configs == seam.count_configs()
+    pc.close()
+
+
+@pytest.mark.parametrize("mod", ["test_gpu_async.py", "test_gpu_dist.py::test_refused_merge_leaves_handle_usable"])
+def test_poisoned_pool(gpu, mod):
+    """The caching pool hands out recycled blocks with old contents: with
+    PSX_POOL_POISON=1 every block comes filled with 0xFF bytes (NaN doubles,
+    -1 ints), so code that relied on fresh memory being zero would fail here."""
+    import subprocess
+    env = dict(os.environ, PSX_POOL_POISON="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
+                        os.path.join(ROOT, "tests", mod)], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]

@@ -111,4 +111,12 @@ if m.any():
 xcc = (tr[:, 2] >> 32) & 0xf
 print("XCC of unit index (first 16):", xcc[:16].tolist(), "; fraction with XCC == index % 8:",
       round(float((xcc == (np.arange(len(xcc)) % 8)).mean()), 3))
+# per XCD (blocks are dealt round-robin over the 8 XCDs): the span ends with
+# the slowest XCD; busy / (slots x span) is the occupancy the drain leaves
+print(f"ideal span at 2048 wave slots: {dur.sum() / 2048:.1f} us (busy unit-us / slots) vs span {span:.1f} us")
+for x in range(8):
+    m = xcc == x
+    if m.any():
+        print(f"  XCC {x}: units {int(m.sum())}, busy unit-us {dur[m].sum():.0f} (ideal {dur[m].sum() / 256:.1f} us), "
+              f"last end {(en[m].max() - t0) / 100.0:.1f} us, last start {(st[m].max() - t0) / 100.0:.1f} us")
 pc.close()
