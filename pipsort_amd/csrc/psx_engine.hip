@@ -42,7 +42,6 @@ namespace {
 
 thread_local std::string g_err;
 constexpr int kPlanMismatchWord = 8;  // status word raised by k_merge_partials
-constexpr int kStampWord = 4;          // status words 4..7: a single pass's sweep / merge start clocks (2 x u64)
 
 constexpr size_t kStatBytes = 3 * 56;  // SetRec, PlanTag, status words (EXACT flag first)
 
@@ -533,11 +532,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
 // psx_sync needs no read-out launch after the merges that end a pass or an
 // exchange (k_merge_fin, k_merge_partials).  The lane wrote the scalars and the
 // flag words itself; the rest comes from earlier launches.
-__device__ void status_to_host(const int* __restrict__ stat, const int* __restrict__ redo, int* __restrict__ host) {
+__device__ void status_to_host(const int* stat, const int* redo, int* host) {
     constexpr int nw = (int)(kStatBytes / sizeof(int));
+    // the lane's own stores to the block (scalars, flag words; through other
+    // pointers of the caller) complete before it reads the block back: no
+    // compiler reordering across the volatile loads, no load passing the stores
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);
+    const volatile int* vs = stat;
     int w[nw];
 #pragma unroll
-    for (int i = 0; i < nw; i++) w[i] = stat[i];
+    for (int i = 0; i < nw; i++) w[i] = vs[i];
     const int r = redo ? *redo : 0;
 #pragma unroll
     for (int i = 0; i < nw; i++) host[i] = w[i];
@@ -552,9 +557,9 @@ __device__ void status_to_host(const int* __restrict__ stat, const int* __restri
 // and status word kPlanMismatchWord is raised (psx_sync / psx_merge_partials
 // report and clear it).  Grid: (U + 63) / 64 per-SNP blocks + one scalar block.
 __global__ __launch_bounds__(64) void k_merge_partials(const Acc5* __restrict__ parts, int U, int ldg, int count,
-                                                       Acc5* __restrict__ acc, SetRec* __restrict__ sacc,
-                                                       int* __restrict__ flag, const int* __restrict__ redo,
-                                                       int* __restrict__ host) {
+                                                       Acc5* __restrict__ acc, SetRec* sacc,
+                                                       int* flag,  // (the status block: no restrict)
+                                                       const int* __restrict__ redo, int* __restrict__ host) {
     const size_t stride = (size_t)ldg + 2;  // ldg Acc5, SetRec, PlanTag
     const int tid = threadIdx.x;
     const PlanTag& t0 = *reinterpret_cast<const PlanTag*>(parts + ldg + 1);
@@ -786,11 +791,14 @@ __global__ __launch_bounds__(64) void k_merge_rec(DevProb P, int lo, int nsingle
 
 __global__ __launch_bounds__(64) void k_merge_fin(DevProb P, int lo, int hi, int nch, int V,
                                                   const SetRec* __restrict__ spart, const Acc5* __restrict__ apart,
-                                                  SetRec extra, Acc5* __restrict__ acc, SetRec* __restrict__ sacc,
-                                                  int* __restrict__ flag, int* __restrict__ sticky,
-                                                  const int* __restrict__ redo, int* __restrict__ host) {
+                                                  SetRec extra, Acc5* __restrict__ acc, SetRec* sacc,
+                                                  int* flag, int* sticky,  // (the status block: no restrict)
+                                                  const int* __restrict__ redo, int* __restrict__ host,
+                                                  const unsigned long long* __restrict__ ts,
+                                                  unsigned long long* __restrict__ hts) {
     const int tid = threadIdx.x;
     if (blockIdx.x == 0) {
+        if (ts && tid < 2) hts[tid] = ts[tid];  // the pass's clock stamps (earlier launches) to the host
         SetRec a = psx::set_zero();
         for (int c = tid; c < nch; c += 64) psx::fold_set(a, spart[c]);
         psx::wave_fold_set(a);
@@ -935,9 +943,15 @@ struct psx_engine {
     hipEvent_t mdone[kBufs] = {};
     bool mdone_rec[kBufs] = {};
     bool mdone_lazy[kBufs] = {};  // merge of a single pass on the engine stream, no event recorded
-    // a single pass (nothing in flight at its call): sweep and merge on the
-    // engine stream, no dispatch events; timed by in-kernel clock stamps
-    bool a_single = false;
+    // Passes whose sweep runs on the engine stream (a single pass — nothing in
+    // flight at its call — or every pass under PSX_SERIAL): no dispatch events;
+    // the sweep's first block and the merge's first block stamp their start
+    // clocks into dstamps[slot], k_merge_fin copies the pair to hstamps[slot]
+    // (pinned), psx_sync sums them
+    int a_stamped = 0;
+    double a_sspan = 0;  // the stamped passes' summed sweep time (their part of the span)
+    unsigned long long* dstamps = nullptr;  // [kRing][2] device
+    unsigned long long* hstamps = nullptr;  // [kRing][2] pinned host
     int wclk_khz = 100000;  // wall_clock64 rate (hipDeviceAttributeWallClockRate)
     // hstat holds the status of the last merge enqueued (k_merge_fin /
     // k_merge_partials write it to pinned host memory) and nothing that changes
@@ -973,7 +987,8 @@ psx_engine::~psx_engine() {
     if (stage_ev) { hipEventSynchronize(stage_ev); hipEventDestroy(stage_ev); }
     if (hstage) psx::hfree(hstage);
     if (hscore) psx::hfree(hscore);
-    psx::dfree(dgen); psx::dfree(dgcsr); psx::dfree(dbm); psx::dfree(gscratch.p); psx::dfree(dscore); psx::dfree(dsrec); psx::dfree(dmrec); psx::dfree(dpass); psx::dfree(dspart); psx::dfree(dapart);
+    psx::dfree(dgen); psx::dfree(dgcsr); psx::dfree(dbm); psx::dfree(gscratch.p); psx::dfree(dscore); psx::dfree(dsrec); psx::dfree(dmrec); psx::dfree(dpass); psx::dfree(dspart); psx::dfree(dapart); psx::dfree(dstamps);
+    if (hstamps) psx::hfree(hstamps);
     psx::sweep_free(plans);
     psx::configs_free(cfg);
     psx::dfree(d_cfg_maps);
@@ -1462,6 +1477,20 @@ int consume_async(psx_engine* e) {
     return 0;
 }
 
+// the stamped passes since the last take (their k_merge_fin completed): each
+// sweep from its first block's start to the merge's first block's start
+// (in-kernel wall clocks; the merge starts ~1 us after the sweep's end)
+void take_stamps(psx_engine* e) {
+    for (int i = 0; i < e->a_stamped; i++) {
+        const unsigned long long t0 = e->hstamps[2 * i], t1 = e->hstamps[2 * i + 1];
+        const double ms = t1 > t0 ? (double)(t1 - t0) / (double)e->wclk_khz : 0.0;
+        e->a_kms += ms;
+        e->a_sspan += ms;
+        e->a_count++;
+    }
+    e->a_stamped = 0;
+}
+
 // Asynchronous passes are pipelined: pass i's sweep runs on the compute stream
 // into the record buffers of parity i & 1 while the merge of pass i - 1 and the
 // caller's exchange (export / collective / merge of partials) run on the engine
@@ -1533,7 +1562,7 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
         // (PSX_SERIAL=1, A/B: every asynchronous pass on the engine stream, the
         // merges between the sweeps instead of beside the next one)
         static const bool serial = getenv("PSX_SERIAL") && atoi(getenv("PSX_SERIAL")) != 0;
-        if ((e->a_pending == 0 && !e->a_single) || serial) {
+        if ((e->a_pending == 0 && e->a_stamped == 0) || serial) {
             // nothing in flight since the last psx_sync: a single pass (one locus
             // swept once) — sweep and merge back to back on the engine stream, on
             // the whole GPU, with no cross-stream event between them (9 us, r06a)
@@ -1570,10 +1599,21 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     // re-armed by the merge that last used it (or psx_create)
     int slot = 0;
     hipEvent_t k0 = nullptr, k1 = nullptr;  // the sweep launch's own start / stop events
-    // a single pass of the k = 3 fast kernel: no dispatch events, clock stamps
+    // the k = 3 fast kernel on the engine stream: no dispatch events, clock stamps
     const bool single = async && S == X && top->k == 3 && top->variant == 1;
-    unsigned long long* const stamp = single ? reinterpret_cast<unsigned long long*>(e->dflag + kStampWord) : nullptr;
+    unsigned long long* stamp = nullptr;
+    unsigned long long* hstamp = nullptr;
     if (single) {
+        if (!e->dstamps) {
+            HIPCHK(psx::dmalloc(&e->dstamps, sizeof(unsigned long long) * 2 * psx_engine::kRing));
+            HIPCHK(psx::hmalloc(&e->hstamps, sizeof(unsigned long long) * 2 * psx_engine::kRing));
+        }
+        if (e->a_stamped == psx_engine::kRing) {  // the ring is full: take its passes now
+            HIPCHK(hipStreamSynchronize(X));
+            take_stamps(e);
+        }
+        stamp = e->dstamps + 2 * e->a_stamped;
+        hstamp = e->hstamps + 2 * e->a_stamped;
         e->plans.stamp = stamp;
     } else if (async) {
         if (e->a_pending == psx_engine::kRing && (rc = consume_async(e))) return rc;
@@ -1594,7 +1634,7 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     const int src = psx::sweep_kernel(e->plans, *top, S, sa, dpass + nl, false, low, dpass, par, pflag, !async, k0, k1);
     e->plans.stamp = nullptr;
     if (src) return fail(PSX_EHIP, std::string("sweep level ") + std::to_string(top->k) + ": " + psx::sweep_error());
-    if (single) e->a_single = true;
+    if (single) e->a_stamped++;
     if (async && !single) {
         e->a_head = (e->a_head + 1) % psx_engine::kRing;
         e->a_pending++;
@@ -1622,7 +1662,7 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
                        dpass, nsrec, nch, V, e->dspart, e->dapart, stamp);
     hipLaunchKernelGGL(k_merge_fin, dim3(1 + (e->U + 63) / 64), dim3(64), 0, X, e->dp, lo, hi, nch, V, e->dspart,
                        e->dapart, extra, e->dacc, e->dsacc, pflag, e->dflag + 1, (const int*)e->plans.d_redo,
-                       reinterpret_cast<int*>(e->hstat));
+                       reinterpret_cast<int*>(e->hstat), stamp, hstamp);
 #endif
     HIPCHK(hipGetLastError());
     if (async) {
@@ -2182,19 +2222,7 @@ int psx_sync(psx_engine* e, int32_t* exact_needed) {
         HIPCHK(hipMemsetAsync(e->dflag + kPlanMismatchWord, 0, sizeof(int), e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
     }
-    if (e->a_single) {
-        // the single pass's sweep: its first block's start to the merge's first
-        // block's start (in-kernel wall clocks; the merge starts ~1 us after the
-        // sweep's end)
-        unsigned long long t[2];
-        std::memcpy(t, words + kStampWord, sizeof(t));
-        const double ms = t[1] > t[0] ? (double)(t[1] - t[0]) / (double)e->wclk_khz : 0.0;
-        if (e->a_count == 0 && e->a_pending == 0) e->a_span = 0;
-        e->a_kms += ms;
-        e->a_span += ms;
-        e->a_count++;
-        e->a_single = false;
-    }
+    take_stamps(e);
     // a refused merge of partial images (k_merge_partials wrote nothing) is
     // reported after the pass bookkeeping below, once (k_status_out cleared it)
     const bool mismatch = words[kPlanMismatchWord] != 0;
@@ -2226,7 +2254,7 @@ int psx_sync(psx_engine* e, int32_t* exact_needed) {
         return fail(PSX_EHIP, std::string("sweep plan: ") + psx::sweep_error());
     const psx::SweepPlan* top = P3 ? P3 : P2;
     e->timing.kernel_ms = e->a_kms;
-    e->timing.span_ms = e->a_count ? e->a_span / e->a_count : 0.0;
+    e->timing.span_ms = e->a_count ? (e->a_span + e->a_sspan) / e->a_count : 0.0;
     e->timing.kernel_launches = e->a_count;
     e->timing.sweep_ms = e->a_count ? e->a_kms / e->a_count : 0.0;
     e->timing.union_sets = top->union_sets;
@@ -2241,6 +2269,7 @@ int psx_sync(psx_engine* e, int32_t* exact_needed) {
     e->a_count = 0;
     e->a_first = -1;
     e->a_span = 0;
+    e->a_sspan = 0;
     return done();
 }
 

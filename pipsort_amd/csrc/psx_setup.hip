@@ -358,9 +358,18 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_lu_step(double* __restrict_
     double uc[kPanel];  // this lane's column of the panel's U rows
 #pragma unroll
     for (int q = 0; q < kPanel; q++) uc[q] = sU[q][64 * cg + lane];
+    // the chunks' loads run one chunk ahead of their updates (r06: the update
+    // waited a full load round trip per chunk, ~4 of them per panel at M = 2000)
+    double tn[kChunk];
 #pragma unroll
     for (int c0 = 0; c0 < kRows; c0 += kChunk) {
-        if (c0 > 0) load_chunk(c0);
+        if (c0 + kChunk < kRows) {
+#pragma unroll
+            for (int m = 0; m < kChunk; m++) {
+                const int i = i0 + rs * kRows + c0 + kChunk + m;
+                tn[m] = (i < n && k < n) ? A[(size_t)i * n + k] : 0.0;
+            }
+        }
 #pragma unroll
         for (int q = 0; q < kPanel; q++) {
             if ((skip >> q) & 1) continue;
@@ -375,6 +384,8 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_lu_step(double* __restrict_
             const int ii = i0 + rs * kRows + c0 + m;
             if (ii < n && k < n) A[(size_t)ii * n + k] = t[m];
         }
+#pragma unroll
+        for (int m = 0; m < kChunk; m++) t[m] = tn[m];
     }
     stamp(3);
 }
@@ -624,11 +635,24 @@ int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipSt
                 for (int i = 0; i < 3; i++) ph[b][i] += (double)(t[i + 1] - t[i]) * 0.01;  // 100 MHz -> us
                 if (b == 0 && t[4]) ph[b][3] += (double)(t[4] - t[3]) * 0.01;
             }
+        // panel to panel: block (0, 0)'s start of panel q + 1 after its end of panel q
+        double gap = 0, per = 0;
+        int ng = 0;
+        for (int q = 0; q + 1 < npan; q++) {
+            const unsigned long long* a = h.data() + 16 * q;
+            const unsigned long long* b = h.data() + 16 * (q + 1);
+            if (!a[0] || !a[3] || !b[0]) continue;
+            gap += (double)(b[0] - a[3]) * 0.01;
+            per += (double)(b[0] - a[0]) * 0.01;
+            ng++;
+        }
         fprintf(stderr, "psx-lu-trace n=%d panels=%d block(0,0): %.2f %.2f %.2f us; block(1,1): %.2f %.2f %.2f us "
-                        "(loads + D + L pass | U solve | update)\n",
+                        "(loads + D + L pass | U solve | update); block (0,0) end -> next panel's start %.2f us, "
+                        "panel to panel %.2f us\n",
                 n, npan, ph[0][0] / std::max(1.0, cnt[0]), ph[0][1] / std::max(1.0, cnt[0]),
                 ph[0][2] / std::max(1.0, cnt[0]), ph[1][0] / std::max(1.0, cnt[1]),
-                ph[1][1] / std::max(1.0, cnt[1]), ph[1][2] / std::max(1.0, cnt[1]));
+                ph[1][1] / std::max(1.0, cnt[1]), ph[1][2] / std::max(1.0, cnt[1]), gap / std::max(1, ng),
+                per / std::max(1, ng));
         psx::dfree(tr);
     }
     return chk(hipGetLastError(), "LU launch", err);
