@@ -501,17 +501,35 @@ def sss_probe_sharded(rank, world, backend):
     mi = E.model_inputs(ld, z, u2l, (10000, 8000), max_causal=5, sharing_param=0.25)
     pc = E.PostCal(mi)
     pc.set_shard(rank, world)
-    ag = torch_allgather(backend)
-    pc.run_sss_sharded(ag)  # warm-up (allocations, collective setup)
+    dev = backend == "nccl"
+    if dev:
+        # the per-iteration exchange stays on the device: RCCL all-gather of the
+        # engine's device send block, ordered on the engine stream (torch's current)
+        stream = torch.cuda.current_stream()
+        pc.set_stream(stream.cuda_stream)
+
+        def agd(send, recv, nbytes, _stream):
+            dist.all_gather_into_tensor(E.device_bytes(recv, nbytes * world), E.device_bytes(send, nbytes))
+
+        run = lambda: pc.run_sss_sharded_dev(agd)  # noqa: E731
+    else:
+        ag = torch_allgather(backend)
+        run = lambda: pc.run_sss_sharded(ag)  # noqa: E731
+    run()  # warm-up (allocations, collective setup)
     dist.barrier()
     t0 = time.perf_counter()
-    iters = pc.run_sss_sharded(ag)
+    iters = run()
     nb = pc.partials_bytes()
-    mine = torch.empty(nb, dtype=torch.uint8, device="cuda")
-    pc.export_partials(mine.data_ptr())
-    torch.cuda.synchronize()
-    allp = torch.frombuffer(bytearray(ag(mine.cpu().numpy().tobytes())), dtype=torch.uint8).cuda()
-    pc.merge_partials(allp.data_ptr(), world)
+    gathered = torch.empty(nb * world, dtype=torch.uint8, device="cuda")
+    if dev:
+        dist.all_gather_into_tensor(gathered, pc.partials_tensor())
+    else:
+        mine = torch.empty(nb, dtype=torch.uint8, device="cuda")
+        pc.export_partials(mine.data_ptr())
+        torch.cuda.synchronize()
+        gathered.copy_(torch.frombuffer(bytearray(ag(mine.cpu().numpy().tobytes())), dtype=torch.uint8))
+    pc.merge_partials(gathered.data_ptr(), world)
+    pc.sync()
     torch.cuda.synchronize()
     walk_ms = (time.perf_counter() - t0) * 1e3
     x = torch.tensor([walk_ms], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
@@ -521,7 +539,8 @@ def sss_probe_sharded(rank, world, backend):
     return {"workload": "SYN-v1 2-study locus, M=2000 SNPs, -c 5 -p 0.25 -n 10000,8000 (BASELINE configs[4])",
             "walk_iterations": iters, "walk_configs": n, "walk_ms_incl_exchange": float(x.item()),
             "multi_gpu": f"batch split over {world} ranks, one all-gather of scores per iteration "
-                         "(psx_run_sss_sharded) + one accumulator exchange"}
+                         + ("on the device (psx_run_sss_sharded_dev, RCCL on the engine stream)" if dev else
+                            "(psx_run_sss_sharded, host-staged)") + " + one accumulator exchange"}
 
 
 def pcie_inclusive(mi, configs, device, reps=3):
@@ -845,7 +864,10 @@ def main():
     if rank == 0:
         value = configs_per_step * args.steps / elapsed
         avg_kernel_s = (kms / max(launches, 1)) / 1e3
-        dur_src = "average launch duration (start / stop events in the sweep's own dispatch packet)"
+        dur_src = ("average launch duration (in-kernel wall clocks: the sweep's first block's start to the "
+                   "merge's first block's start; serial passes on one stream, no dispatch events)" if world == 1
+                   and not os.environ.get("PSX_SERIAL") else
+                   "average launch duration (start / stop events in the sweep's own dispatch packet)")
         span_s = (tm.get("span_ms") or 0.0) / 1e3 if use_async else 0.0
         if 0 < span_s < avg_kernel_s:
             # overlapped passes (worlds >= 4): launches overlap, so a launch's own

@@ -231,6 +231,15 @@ typedef int (*psx_allgather_fn)(void *ctx, const void *send, void *recv, int64_t
  * (psx_export_partials / all-gather / psx_merge_partials).  With world 1 it
  * is psx_run_sss. */
 int psx_run_sss_sharded(psx_engine *e, psx_allgather_fn allgather, void *ctx, int32_t *iterations_out);
+/* The same walk with the per-iteration exchange kept on the device: the
+ * callback gets DEVICE pointers (send: `bytes`; recv: world x `bytes`, rank
+ * order) and the engine's stream (a hipStream_t), and enqueues the all-gather
+ * on that stream — e.g. one RCCL all-gather — returning at once (0 = enqueued).
+ * Each iteration then runs pack -> all-gather -> unpack -> insert on the stream
+ * with one host synchronisation (no score copies through host memory). */
+typedef int (*psx_allgather_dev_fn)(void *ctx, const void *device_send, void *device_recv, int64_t bytes,
+                                    void *stream);
+int psx_run_sss_sharded_dev(psx_engine *e, psx_allgather_dev_fn allgather, void *ctx, int32_t *iterations_out);
 
 /* PostCal::expand_and_compute_lkl (sss_postcal.cpp:447-685), batched: evaluate
  * n_sets union sets (ascending union indices, -1 padded to `stride`), return the

@@ -1559,9 +1559,15 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
             for (int i = 0; i < psx_engine::kBufs; i++)
                 if (!e->mdone[i]) HIPCHK(hipEventCreateWithFlags(&e->mdone[i], hipEventDisableTiming));
         }
-        // (PSX_SERIAL=1, A/B: every asynchronous pass on the engine stream, the
-        // merges between the sweeps instead of beside the next one)
-        static const bool serial = getenv("PSX_SERIAL") && atoi(getenv("PSX_SERIAL")) != 0;
+        // Serial passes at world 1 (PSX_SERIAL = 0 / 1 overrides): every pass's
+        // sweep and merge back to back on the engine stream.  With nothing to
+        // exchange, overlapping the merge with the next sweep bought nothing: same
+        // step, 0.788 vs 0.789 ms at syn1000c3, the overlapped sweep itself 7 %
+        // longer (0.808 vs 0.753 ms) for the merge's waves beside it (r06f).  At
+        // world > 1 the next sweep hides the exchange (and at world >= 8 the
+        // previous sweep's drain): pipelined.
+        static const char* ser_env = getenv("PSX_SERIAL");
+        const bool serial = ser_env ? atoi(ser_env) != 0 : e->world == 1;
         if ((e->a_pending == 0 && e->a_stamped == 0) || serial) {
             // nothing in flight since the last psx_sync: a single pass (one locus
             // swept once) — sweep and merge back to back on the engine stream, on
@@ -2045,6 +2051,7 @@ int psx_warmup_for(int device, int32_t max_causal, int32_t configs_file) {
     const bool trace = getenv("PSX_TIMING") != nullptr;
     auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     double t[7] = {now(), 0, 0, 0, 0, 0, 0};
+    double ta = 0, tl = 0;  // engine module split: first allocation, launch enqueued
     int rc;
     if ((rc = gpu_ready(device))) return rc;
     HIPCHK(hipFree(nullptr));  // context
@@ -2052,8 +2059,10 @@ int psx_warmup_for(int device, int32_t max_causal, int32_t configs_file) {
     // one launch loads this translation unit's device code
     double* d = nullptr;
     HIPCHK(psx::dmalloc(&d, 64 * sizeof(double)));
+    ta = now();
     hipLaunchKernelGGL(k_diag, dim3(1), dim3(64), 0, nullptr, d, 8, d + 8);
     hipError_t le = hipGetLastError();
+    tl = now();
     hipError_t se = hipDeviceSynchronize();
     psx::dfree(d);
     if (le != hipSuccess || se != hipSuccess)
@@ -2075,8 +2084,11 @@ int psx_warmup_for(int device, int32_t max_causal, int32_t configs_file) {
     if (trace)
         fprintf(stderr,
                 "psx-warm {\"context_ms\": %.3f, \"engine_module_ms\": %.3f, \"setup_module_ms\": %.3f, "
-                "\"sweep_module_ms\": %.3f, \"sweep3_module_ms\": %.3f, \"configs_module_ms\": %.3f}\n",
-                t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4], t[6] - t[5]);
+                "\"sweep_module_ms\": %.3f, \"sweep3_module_ms\": %.3f, \"configs_module_ms\": %.3f, "
+                "\"engine_module_split\": {\"first_alloc_ms\": %.3f, \"first_launch_enqueue_ms\": %.3f, "
+                "\"first_launch_complete_ms\": %.3f}}\n",
+                t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4], t[6] - t[5], ta - t[1], tl - ta,
+                t[2] - tl);
     return 0;
 }
 
@@ -2573,9 +2585,10 @@ enum { kUnseen = 0, kNulls = 1, kCurPos = 2, kCurNull = 3, kNCnt = 4 };
 // no L2 write-back) into coherent pinned memory (hipHostMallocCoherent, uncached
 // for the device: an acknowledged store is in host memory, so the mark cannot
 // overtake the weight; a release store at system scope would add an L2
-// write-back per wave, measured 13 -> 21 us per eval in r05).  The host takes neighbour i when its word carries this
-// iteration's tag: no wait for the kernel's end (~5-8 us before its stop event
-// completes) and no contended completion counter.
+// write-back per wave, measured 13 -> 21 us per eval in r05).  The host takes
+// neighbour i when its word carries this iteration's tag: no wait for the
+// kernel's end (~5-8 us before its stop event completes) and no contended
+// completion counter.
 __device__ inline void publish_mark(double* lk_host, unsigned long long* mark_host, int i, double w, int mk,
                                     unsigned int seq) {
     __hip_atomic_store(lk_host + i, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2810,6 +2823,32 @@ __global__ void k_map_rehash(const MapEntry* __restrict__ old, size_t n, MapEntr
     if (i < n && old[i].state) map_insert(T, mask, old[i].lo, old[i].hi, old[i].score);
 }
 
+// Sharded walk, device exchange (psx_run_sss_sharded_dev): this rank's
+// all-gather send block [m, s of its running normaliser, its slice's item
+// scores, zero padding to `per`], built on the device after the post ...
+__global__ void k_sss_pack(const SetRec* __restrict__ sacc, const double* __restrict__ score, int lo, int n, int per,
+                           double* __restrict__ snd) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        snd[0] = (double)sacc->m;
+        snd[1] = sacc->tot;
+    }
+    if (i < per) snd[2 + i] = i < n ? score[lo + i] : 0.0;
+}
+// ... and, after the caller's stream-ordered all-gather, every rank's scores to
+// their items (full) and every rank's normaliser to pinned host memory
+__global__ void k_sss_unpack(const double* __restrict__ rcv, int world, int n_items, int per,
+                             double* __restrict__ full, double* __restrict__ hnorm) {
+    const int r = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+    const double* q = rcv + (size_t)r * (per + 2);
+    const int rlo = (int)((int64_t)n_items * r / world), rn = (int)((int64_t)n_items * (r + 1) / world) - rlo;
+    if (i < rn) full[rlo + i] = q[2 + i];
+    if (i == 0) {
+        hnorm[2 * r] = q[0];
+        hnorm[2 * r + 1] = q[1];
+    }
+}
+
 struct SssDev {
     MapEntry* T = nullptr;
     size_t cap = 0, used = 0;
@@ -2829,6 +2868,10 @@ struct SssDev {
     unsigned long long* hmark = nullptr;  // pinned host: per neighbour, its mark word (one rank)
     unsigned long long* trace = nullptr;  // PSX_SSS_TRACE: item 1's eval phase clocks (pinned host)
     double* hscore = nullptr; // pinned host: gathered item scores (world > 1)
+    double* dx = nullptr;     // device exchange: send block | receive blocks (world > 1)
+    size_t cap_dx = 0;
+    double* hnorm = nullptr;  // pinned host: every rank's normaliser (m, s) (device exchange)
+    int cap_hnorm = 0;
     unsigned int seq = 0;     // the last iteration tag of the mark words (never 0)
     ~SssDev() {
         psx::dfree(T);
@@ -2842,6 +2885,8 @@ struct SssDev {
         if (hmark) psx::hfree(hmark);
         if (hscore) psx::hfree(hscore);
         if (trace) psx::hfree(trace);
+        psx::dfree(dx);
+        if (hnorm) psx::hfree(hnorm);
         for (int i = 0; i < 2 * kRingE; i++)
             if (ev[i]) hipEventDestroy(ev[i]);
     }
@@ -2902,10 +2947,12 @@ int sss_workspace(psx_engine* e, size_t nmax, int world, hipStream_t s) {
     return 0;
 }
 
-int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* iterations_out) {
+int run_sss(psx_engine* e, psx_allgather_fn allgather, psx_allgather_dev_fn dgather, void* ctx,
+            int32_t* iterations_out) {
     HIPCHK(hipSetDevice(e->dev));
     e->stat_fresh = false;  // status changes: psx_sync reads it out again
-    const int rank = allgather ? e->rank : 0, world = allgather ? e->world : 1;
+    const bool sharded = allgather || dgather;
+    const int rank = sharded ? e->rank : 0, world = sharded ? e->world : 1;
     int rc;
     if ((rc = reset_acc(e))) return rc;
     std::memset(&e->timing, 0, sizeof(e->timing));
@@ -3049,6 +3096,49 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
                     D.trace[7] = 0;
                 }
             }
+        } else if (dgather) {
+            // the exchange on the device: pack -> the caller's stream-ordered
+            // all-gather -> unpack -> insert, then one synchronisation (no score
+            // copies through the host, no host bytes for the callback)
+            const int per = (n_items + world - 1) / world, wd = 2 + per;
+            if ((size_t)wd * (world + 1) > D.cap_dx) {
+                psx::dfree(D.dx);
+                D.dx = nullptr;
+                D.cap_dx = 0;
+                HIPCHK(psx::dmalloc(&D.dx, sizeof(double) * (size_t)wd * (world + 1)));
+                D.cap_dx = (size_t)wd * (world + 1);
+            }
+            if (2 * world > D.cap_hnorm) {
+                if (D.hnorm) psx::hfree(D.hnorm);
+                D.hnorm = nullptr;
+                HIPCHK(psx::hmalloc(&D.hnorm, sizeof(double) * 2 * world));
+                D.cap_hnorm = 2 * world;
+            }
+            double* const snd = D.dx;
+            double* const rcv = D.dx + wd;
+            hipLaunchKernelGGL(k_sss_pack, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, e->stream, e->dsacc,
+                               e->dscore, lo, hi - lo, per, snd);
+            HIPCHK(hipGetLastError());
+            if (dgather(ctx, snd, rcv, (int64_t)wd * (int64_t)sizeof(double), e->stream))
+                return fail(PSX_EEXCHANGE, "SSS device all-gather callback failed");
+            hipLaunchKernelGGL(k_sss_unpack, dim3((unsigned)((per + 255) / 256), (unsigned)world), dim3(256), 0,
+                               e->stream, rcv, world, n_items, per, D.full, D.hnorm);
+            hipLaunchKernelGGL(k_sss_post, dim3((unsigned)(U + 1 + (n_nbd + 255) / 256)), dim3(256), 0, e->stream, it,
+                               lo, hi, D.rows, D.mark, D.cnt, e->dmrec, e->dsrec, D.full, null1, (Acc5*)nullptr,
+                               (SetRec*)nullptr, (SetRec*)nullptr, (int*)nullptr, D.T, mask, 2, D.lk);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipStreamSynchronize(e->stream));
+            unseen = D.hcnt[kUnseen];
+            double mx = -INFINITY;
+            std::vector<double> part(world, 0.0);
+            for (int r = 0; r < world; r++) {
+                part[r] = logval(e, (int32_t)D.hnorm[2 * r], D.hnorm[2 * r + 1]);
+                if (part[r] != 0.0) mx = std::max(mx, part[r]);
+            }
+            double acc = 0.0;  // the ranks' normalisers, combined in rank order
+            for (int r = 0; r < world; r++)
+                if (part[r] != 0.0) acc += std::exp(part[r] - mx);
+            sss_sum = acc > 0 ? mx + std::log(acc) : 0.0;
         } else {
             HIPCHK(hipStreamSynchronize(e->stream));
             unseen = D.hcnt[kUnseen];
@@ -3175,11 +3265,18 @@ int run_sss(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* itera
 }
 }  // namespace
 
-int psx_run_sss(psx_engine* e, int32_t* iterations_out) { return run_sss(e, nullptr, nullptr, iterations_out); }
+int psx_run_sss(psx_engine* e, int32_t* iterations_out) {
+    return run_sss(e, nullptr, nullptr, nullptr, iterations_out);
+}
 
 int psx_run_sss_sharded(psx_engine* e, psx_allgather_fn allgather, void* ctx, int32_t* iterations_out) {
     if (!allgather && e->world > 1) return fail(PSX_EINVAL, "psx_run_sss_sharded: no all-gather callback");
-    return run_sss(e, allgather, ctx, iterations_out);
+    return run_sss(e, allgather, nullptr, ctx, iterations_out);
+}
+
+int psx_run_sss_sharded_dev(psx_engine* e, psx_allgather_dev_fn allgather, void* ctx, int32_t* iterations_out) {
+    if (!allgather && e->world > 1) return fail(PSX_EINVAL, "psx_run_sss_sharded_dev: no all-gather callback");
+    return run_sss(e, nullptr, allgather, ctx, iterations_out);
 }
 
 int psx_get_accum(psx_engine* e, psx_accum* out) {

@@ -38,7 +38,7 @@ EXPORTED = [
     "psx_fold_partials_host", "psx_plan_hash", "psx_plan_build_ms", "psx_plan_csr_selftest", "psx_shard_stats", "psx_plan_units_k3", "psx_set_stream",
     "psx_psd_shift", "psx_lowrank_study", "psx_sym_eigen", "psx_lu_det",
     "psx_create_from_ld", "psx_psd_shift_gpu", "psx_lu_det_gpu", "psx_elim_gpu",
-    "psx_run_exhaustive_async", "psx_sync", "psx_run_sss_sharded",
+    "psx_run_exhaustive_async", "psx_sync", "psx_run_sss_sharded", "psx_run_sss_sharded_dev",
     "psx_multi_create", "psx_multi_create_from_ld", "psx_multi_run_exhaustive", "psx_multi_run_configs",
     "psx_multi_run_sss", "psx_multi_get_accum", "psx_multi_get_timing", "psx_multi_count",
     "psx_multi_last_error", "psx_multi_destroy",
@@ -46,6 +46,9 @@ EXPORTED = [
 
 # psx_allgather_fn (include/pipsort_engine.h): int (*)(void *ctx, const void *send, void *recv, int64_t bytes)
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
+# device variant: (ctx, device send, device recv, bytes per rank, hipStream_t)
+ALLGATHER_DEV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                    ctypes.c_void_p)
 
 
 class EngineError(RuntimeError):
@@ -203,6 +206,7 @@ def load_library(path: str = LIB_PATH):
         "psx_run_exhaustive_async": (c_int, [vp]),
         "psx_sync": (c_int, [vp, P(c_i32)]),
         "psx_run_sss_sharded": (c_int, [vp, ALLGATHER_FN, vp, P(c_i32)]),
+        "psx_run_sss_sharded_dev": (c_int, [vp, ALLGATHER_DEV_FN, vp, P(c_i32)]),
         "psx_multi_create": (c_int, [P(_Problem), P(c_i32), c_i32, P(vp)]),
         "psx_multi_create_from_ld": (c_int, [P(_LdProblem), P(c_i32), c_i32, P(vp), P(SetupInfo)]),
         "psx_multi_run_exhaustive": (c_int, [vp]),
@@ -717,6 +721,30 @@ class PostCal:
         fn = ALLGATHER_FN(cb)
         it = ctypes.c_int32(0)
         rc = self.lib.psx_run_sss_sharded(self.h, fn, None, ctypes.byref(it))
+        if err:
+            raise err[0]
+        _check(rc)
+        return it.value
+
+    def run_sss_sharded_dev(self, allgather_dev) -> int:
+        """The sharded SSS walk with the per-iteration exchange on the device
+        (psx_run_sss_sharded_dev): allgather_dev(send, recv, nbytes, stream)
+        gets device addresses and the engine's hipStream_t and enqueues the
+        all-gather of nbytes per rank on that stream (e.g. torch.distributed's
+        all_gather_into_tensor on device_bytes views, with that stream current)."""
+        err = []
+
+        def cb(_ctx, send, recv, nbytes, stream):
+            try:
+                allgather_dev(int(send), int(recv), int(nbytes), int(stream or 0))
+                return 0
+            except BaseException as ex:  # reported through the engine's error code
+                err.append(ex)
+                return 1
+
+        fn = ALLGATHER_DEV_FN(cb)
+        it = ctypes.c_int32(0)
+        rc = self.lib.psx_run_sss_sharded_dev(self.h, fn, None, ctypes.byref(it))
         if err:
             raise err[0]
         _check(rc)

@@ -18,7 +18,10 @@ from test_gpu_parity import assert_parity
 pytestmark = pytest.mark.gpu
 
 
-def _sharded(seam, world):
+def _sharded(seam, world, dev=False):
+    """dev: psx_run_sss_sharded_dev, the all-gather on device buffers ordered on
+    each rank's engine stream (here: copies through one shared device buffer,
+    a barrier between the ranks' copy-in and copy-out)."""
     import torch
 
     pcs = []
@@ -30,6 +33,7 @@ def _sharded(seam, world):
     slots = [None] * world
     iters = [None] * world
     errs = []
+    shared = torch.empty(world * (1 << 22), dtype=torch.uint8, device="cuda") if dev else None
 
     def gather(r):
         def ag(b):
@@ -40,9 +44,25 @@ def _sharded(seam, world):
             return out
         return ag
 
+    def gather_dev(r):
+        def ag(send, recv, nbytes, stream):
+            assert world * nbytes <= shared.numel()
+            ext = torch.cuda.ExternalStream(stream)
+            with torch.cuda.stream(ext):
+                shared[r * nbytes:(r + 1) * nbytes].copy_(E.device_bytes(send, nbytes))
+            ext.synchronize()
+            bar.wait()
+            with torch.cuda.stream(ext):
+                E.device_bytes(recv, world * nbytes).copy_(shared[:world * nbytes])
+            ext.synchronize()
+            bar.wait()
+        return ag
+
     def run(r):
         try:
-            iters[r] = pcs[r].run_sss_sharded(gather(r))
+            torch.cuda.set_device(0)
+            iters[r] = (pcs[r].run_sss_sharded_dev(gather_dev(r)) if dev else
+                        pcs[r].run_sss_sharded(gather(r)))
         except BaseException as ex:  # noqa: BLE001
             errs.append(ex)
             bar.abort()
@@ -72,15 +92,16 @@ def _seams():
     return out
 
 
+@pytest.mark.parametrize("dev", [False, True], ids=["host_exchange", "device_exchange"])
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("name", ["small_c3", "example_c2", "syn60_c5"])
-def test_sss_sharded_matches_single_walk_and_oracle(gpu, name, world):
+def test_sss_sharded_matches_single_walk_and_oracle(gpu, name, world, dev):
     seam = dict(_seams())[name]
     one = E.PostCal(seam)
     it1 = one.run_sss()
     single = one.accum()
     one.close()
-    iters, got = _sharded(seam, world)
+    iters, got = _sharded(seam, world, dev)
     assert iters == [it1] * world  # the same walk on every rank
     assert got.n_configs == single.n_configs
     assert_parity(got, O.postcal(seam, "sss"), ll_rtol=1e-11)
@@ -112,3 +133,27 @@ def test_sss_sharded_world1_is_run_sss(gpu):
         assert np.array_equal(getattr(ra, f), getattr(rb, f)), f
     a.close()
     b.close()
+
+
+def test_sss_sharded_dev_exchange_bitwise_host_exchange(gpu):
+    """The device exchange walks the same path and folds the same values as
+    the host-staged one: merged accumulators bitwise equal."""
+    seam = dict(_seams())["syn60_c5"]
+    ih, gh = _sharded(seam, 2, False)
+    idv, gd = _sharded(seam, 2, True)
+    assert ih == idv and gh.n_configs == gd.n_configs and gh.total == gd.total
+    for f in ("post", "no_causal", "shared", "shared_ll", "notshared_ll"):
+        assert np.array_equal(getattr(gh, f), getattr(gd, f)), f
+
+
+def test_sss_sharded_dev_callback_error_is_reported(gpu):
+    seam = dict(_seams())["small_c3"]
+    pc = E.PostCal(seam)
+    pc.set_shard(0, 2)
+
+    def broken(*_a):
+        raise RuntimeError("collective failed")
+
+    with pytest.raises(RuntimeError, match="collective failed"):
+        pc.run_sss_sharded_dev(broken)
+    pc.close()

@@ -1,0 +1,42 @@
+// Cold-start split of a one-locus process (tests/example wall):
+// hsa_init alone, then the HIP runtime (hipGetDeviceCount), context
+// (hipFree(0)), first launch.  Prints one JSON line.  Developer tool:
+//   hipcc --offload-arch=gfx950 -O2 -o tools/init_probe tools/init_probe.cpp -lhsa-runtime64
+#include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <unistd.h>
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+__global__ void k_noop(int* p) {
+    if (p && threadIdx.x == 0) p[0] = 1;
+}
+
+int main(int argc, char** argv) {
+    const bool hsa_first = argc > 1 && atoi(argv[1]) == 1;
+    const double t0 = now_ms();
+    if (hsa_first) hsa_init();
+    const double t1 = now_ms();
+    int n = 0;
+    (void)hipGetDeviceCount(&n);
+    const double t2 = now_ms();
+    (void)hipSetDevice(0);
+    (void)hipFree(nullptr);
+    const double t3 = now_ms();
+    int* d = nullptr;
+    (void)hipMalloc(&d, 256);
+    const double t4 = now_ms();
+    hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, nullptr, d);
+    (void)hipDeviceSynchronize();
+    const double t5 = now_ms();
+    printf("{\"hsa_init_ms\": %.2f, \"hip_device_count_ms\": %.2f, \"context_ms\": %.2f, \"malloc_ms\": %.2f, "
+           "\"first_launch_ms\": %.2f, \"devices\": %d}\n", t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, n);
+    fflush(stdout);
+    _exit(0);
+}
