@@ -45,17 +45,22 @@ def _sharded(seam, world, dev=False):
         return ag
 
     def gather_dev(r):
+        n_call = [0]
+
         def ag(send, recv, nbytes, stream):
-            assert world * nbytes <= shared.numel()
+            # two shared buffers, alternating: a rank refills one only after the
+            # next call's barrier, which every rank reaches after its engine
+            # synchronised the copy-out of the previous use
+            assert world * nbytes <= shared.numel() // 2
+            buf = shared[(n_call[0] % 2) * (shared.numel() // 2):]
+            n_call[0] += 1
             ext = torch.cuda.ExternalStream(stream)
             with torch.cuda.stream(ext):
-                shared[r * nbytes:(r + 1) * nbytes].copy_(E.device_bytes(send, nbytes))
+                buf[r * nbytes:(r + 1) * nbytes].copy_(E.device_bytes(send, nbytes))
             ext.synchronize()
             bar.wait()
-            with torch.cuda.stream(ext):
-                E.device_bytes(recv, world * nbytes).copy_(shared[:world * nbytes])
-            ext.synchronize()
-            bar.wait()
+            with torch.cuda.stream(ext):  # enqueued: the engine's stream orders it
+                E.device_bytes(recv, world * nbytes).copy_(buf[:world * nbytes])
         return ag
 
     def run(r):

@@ -2,10 +2,12 @@
 BASELINE configs[4], M = 2000) at world 1 (psx_run_sss) and at world 2 with two
 rank threads on the same device, their per-iteration all-gather either
 host-staged (psx_run_sss_sharded: scores D2H, bytes, H2D) or kept on the device
-(psx_run_sss_sharded_dev: pack -> copies through one shared device buffer on
+(psx_run_sss_sharded_dev: pack -> copies through two alternating shared device buffers on
 each rank's engine stream -> unpack), the walk time per rank (median of reps).
 On one device the two ranks share the GPU, so this checks the exchange path's
-cost and correctness (same walk, same accumulators), not a speed-up.
+cost and correctness (same walk, same accumulators), not a speed-up: the
+threads' Python callbacks and barriers (GIL) dominate both exchange forms here;
+with RCCL the device form's callback only enqueues the collective.
 
     python tools/sss_shard_rehearsal.py [--reps 5]
 """
@@ -49,16 +51,19 @@ def walk_world2(seam, dev, reps):
         return ag
 
     def ag_dev(r):
+        n_call = [0]
+
         def ag(send, recv, nbytes, stream):
+            # two shared buffers, alternating (see tests/test_gpu_sss_shard.py)
+            buf = shared[(n_call[0] % 2) * (shared.numel() // 2):]
+            n_call[0] += 1
             ext = torch.cuda.ExternalStream(stream)
             with torch.cuda.stream(ext):
-                shared[r * nbytes:(r + 1) * nbytes].copy_(E.device_bytes(send, nbytes))
+                buf[r * nbytes:(r + 1) * nbytes].copy_(E.device_bytes(send, nbytes))
             ext.synchronize()
             bar.wait()
-            with torch.cuda.stream(ext):
-                E.device_bytes(recv, world * nbytes).copy_(shared[:world * nbytes])
-            ext.synchronize()
-            bar.wait()
+            with torch.cuda.stream(ext):  # enqueued: the engine's stream orders it
+                E.device_bytes(recv, world * nbytes).copy_(buf[:world * nbytes])
         return ag
 
     def run(r):
