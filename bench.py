@@ -599,12 +599,14 @@ def example_wall():
         same = all(open(os.path.join(d, f"out_{f}.txt")).read() ==
                    open(os.path.join(src, f"expected_{f}.txt")).read()
                    for f in ("study0_post", "study1_post", "study0_set", "study1_set", "nocausal"))
-    phases, warm = None, None
+    phases, warm, setup_split = None, None, None
     for line in r.stderr.splitlines():
         if line.startswith("psx-timing "):
             phases = json.loads(line[len("psx-timing "):])
         elif line.startswith("psx-warm "):  # psx_warmup_for's split of context_and_code_load
             warm = json.loads(line[len("psx-warm "):])
+        elif line.startswith("psx-setup "):  # psx_create_from_ld's phases (gpu_setup_ms)
+            setup_split = json.loads(line[len("psx-setup "):])
     if phases:
         # process exit (teardown of the HIP runtime, unmapping) until the parent sees it
         phases["exit_ms"] = t1 / 1e6 - phases.pop("end_epoch_ms")
@@ -616,6 +618,8 @@ def example_wall():
         phases["sum_ms"] -= phases["hip_runtime_ms"] + phases["context_and_code_load_ms"]
         if warm:
             phases["context_and_code_load_split"] = warm
+        if setup_split:
+            phases["gpu_setup_split"] = setup_split
     return (wall if r.returncode == 0 else None), same, phases
 
 
@@ -757,6 +761,7 @@ def main():
     setup_s = time.time() - t_setup
 
     use_async = not os.environ.get("PSX_BENCH_SYNC")
+    step_sync = bool(os.environ.get("PSX_BENCH_STEPSYNC"))  # A/B: psx_sync after every asynchronous pass
 
     def step():
         # the pass is enqueued without a host sync; the exchange is ordered after
@@ -774,6 +779,12 @@ def main():
                 dist.all_gather(parts, mine.cpu())
                 gathered.copy_(torch.cat(parts))
             pc.merge_partials(gathered.data_ptr(), world)  # ordered after the collective
+        if use_async and step_sync:
+            step_exact[0] |= bool(pc.sync())
+            step_t.append(pc.timing())
+
+    step_exact = [False]
+    step_t = []
 
     def timed():
         kms, launches = 0.0, 0
@@ -796,7 +807,11 @@ def main():
             dist.barrier()
         elapsed = time.perf_counter() - t0
         exact = pc.sync()  # EXACT flag of any pass (OR-ed over ranks by the merge)
-        if use_async:
+        if use_async and step_sync:  # the passes were synced (and timed) one by one
+            ts = step_t[-args.steps:]
+            exact = exact or step_exact[0]
+            kms, launches = sum(t["kernel_ms"] for t in ts), sum(t["kernel_launches"] for t in ts)
+        elif use_async:
             t = pc.timing()
             kms, launches = t["kernel_ms"], t["kernel_launches"]
         return elapsed, kms, launches, exact

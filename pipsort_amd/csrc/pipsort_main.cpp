@@ -242,6 +242,8 @@ struct PhaseTimes {
     double main = 0, parse0 = 0, parse1 = 0, rt0 = 0, rt1 = 0, warm1 = 0, joined = 0, setup1 = 0, sweep1 = 0,
            accum1 = 0, write1 = 0, end = 0;
 } g_ph;
+psx_setup_info g_setup_info;  // the GPU setup's own phases (PSX_TIMING)
+bool g_have_setup_info = false;
 
 void print_phases() {
     if (!getenv("PSX_TIMING")) return;
@@ -255,6 +257,14 @@ void print_phases() {
             g_ph.main - spawn, g_ph.parse0 - g_ph.main, g_ph.parse1 - g_ph.parse0, g_ph.rt1 - g_ph.rt0, g_ph.warm1 - g_ph.rt1,
             g_ph.joined - g_ph.parse1, g_ph.setup1 - g_ph.joined, g_ph.sweep1 - g_ph.setup1,
             g_ph.accum1 - g_ph.sweep1, g_ph.write1 - g_ph.accum1, g_ph.end - g_ph.write1, g_ph.end);
+    if (g_have_setup_info) {
+        const psx_setup_info& i = g_setup_info;
+        fprintf(stderr,
+                "psx-setup {\"setup_ms\": %.3f, \"alloc_ms\": %.3f, \"studies_ms\": %.3f, \"tail_ms\": %.3f, "
+                "\"upload_ms\": [%.3f, %.3f], \"psd_lu_ms\": [%.3f, %.3f], \"finish_ms\": [%.3f, %.3f]}\n",
+                i.setup_ms, i.alloc_ms, i.studies_ms, i.tail_ms, i.study_upload_ms[0], i.study_upload_ms[1],
+                i.study_psd_ms[0], i.study_psd_ms[1], i.study_finish_ms[0], i.study_finish_ms[1]);
+    }
 }
 
 // postcal.cpp:1166-1236 (stdout only): per study, the SNPs ranked by
@@ -514,6 +524,10 @@ int main(int argc, char* argv[]) {
             rc = psx_multi_create_from_ld(&q, devices.data(), (int32_t)devices.size(), &multi, &info);
         else
             rc = psx_create_from_ld(&q, device, &eng, &info);  // model.h:171-265
+        if (rc == 0) {
+            g_setup_info = info;
+            g_have_setup_info = true;
+        }
         if (rc == 0)
             for (int i = 0; i < S; i++)
                 std::cout << "study " << i << ": psd shift " << info.psd_added[i] << " ("

@@ -533,20 +533,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
 // exchange (k_merge_fin, k_merge_partials).  The lane wrote the scalars and the
 // flag words itself; the rest comes from earlier launches.
 __device__ void status_to_host(const int* stat, const int* redo, int* host) {
-    constexpr int nw = (int)(kStatBytes / sizeof(int));
+    // 16-byte pieces (the block is 8-byte aligned: pairs of 8-byte words) —
+    // each store to host memory is a fabric write the kernel's end waits for
+    constexpr int nq = (int)(kStatBytes / 8);
+    static_assert(kStatBytes % 8 == 0, "status block of 8-byte words");
     // the lane's own stores to the block (scalars, flag words; through other
     // pointers of the caller) complete before it reads the block back: no
     // compiler reordering across the volatile loads, no load passing the stores
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __builtin_amdgcn_s_waitcnt(0);
-    const volatile int* vs = stat;
-    int w[nw];
+    const volatile unsigned long long* vs = reinterpret_cast<const volatile unsigned long long*>(stat);
+    unsigned long long w[nq + 1];
 #pragma unroll
-    for (int i = 0; i < nw; i++) w[i] = vs[i];
-    const int r = redo ? *redo : 0;
+    for (int i = 0; i < nq; i++) w[i] = vs[i];
+    w[nq] = (unsigned long long)(unsigned)(redo ? *redo : 0);
+    unsigned long long* h = reinterpret_cast<unsigned long long*>(host);
 #pragma unroll
-    for (int i = 0; i < nw; i++) host[i] = w[i];
-    host[nw] = r;
+    for (int i = 0; i + 1 <= nq; i += 2) {
+        if (i + 1 <= nq) {
+            ulonglong2 v;
+            v.x = w[i];
+            v.y = w[i + 1];
+            *reinterpret_cast<ulonglong2*>(h + i) = v;  // (hstat: pinned, 64-byte aligned)
+        }
+    }
+    if ((nq + 1) % 2) h[nq] = w[nq];
 }
 
 // merge `count` concatenated partial images (rank order) into acc / sacc.

@@ -42,6 +42,9 @@ for v in variants:
     sp = {k: statistics.median([r[2]["context_and_code_load_split"].get("engine_module_split", {}).get(k, 0.0)
                                 for r in rows if r[2] and r[2].get("context_and_code_load_split")])
           for k in ("first_alloc_ms", "first_launch_enqueue_ms", "first_launch_complete_ms")}
+    ss = [r[2].get("gpu_setup_split") for r in rows if r[2] and r[2].get("gpu_setup_split")]
+    if ss:
+        print(f"  gpu_setup_split (last): {ss[-1]}")
     print(f"[{v or 'default'}] wall median {statistics.median(walls):.3f} s (min {min(walls):.3f}), outputs match "
           f"{all(r[1] for r in rows)}; " + ", ".join(f"{k} {med[k]:.1f}" for k in keys) + f", engine_module {em:.1f} ({', '.join(f'{k} {x:.1f}' for k, x in sp.items())})",
           flush=True)
