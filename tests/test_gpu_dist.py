@@ -59,6 +59,8 @@ def test_bench_rccl_path_world1(gpu):
     assert "RCCL" in out["config"]["parallelism"]
     assert out["configs_checked"] == out["config"]["configs_per_step"] == 179_701
     assert out["sss"]["walk_iterations"] == 2 and out["sss"]["walk_configs"] == 23_993
+    assert "on the device" in out["sss"]["multi_gpu"]  # psx_run_sss_sharded_dev under RCCL
+    assert out["single_pass_ms"] > 0  # one locus swept once, RCCL exchange included
 
 
 def test_bench_gpus2_launches_its_own_ranks(gpu):
