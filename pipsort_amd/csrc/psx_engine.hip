@@ -1672,10 +1672,12 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     // (-DPSX_ABLATE_MERGE, a separate timing build only: the pass's merge is
     // skipped and its results are wrong; measures what the merge beside the next
     // sweep costs.  No environment switch: a shipped library always merges.)
+    const bool csr = psx::records_at_csr_positions();
 #ifndef PSX_ABLATE_MERGE
     hipLaunchKernelGGL(k_merge_rec, dim3((unsigned)(nch + (size_t)e->U * V)), dim3(64), 0, X, e->dp, lo, (int)nsingle,
-                       psx::plan_records(*mA, par), mA->d_dptr, (const int*)nullptr,  // runs contiguous (gidx identity)
-                       mB ? psx::plan_records(*mB, par) : nullptr, mB ? mB->d_dptr : nullptr, (const int*)nullptr,
+                       psx::plan_records(*mA, par), mA->d_dptr, csr ? (const int*)nullptr : mA->d_gidx,
+                       mB ? psx::plan_records(*mB, par) : nullptr, mB ? mB->d_dptr : nullptr,
+                       csr || !mB ? (const int*)nullptr : mB->d_gidx,  // runs contiguous: gidx the identity
                        dpass, nsrec, nch, V, e->dspart, e->dapart, stamp);
     hipLaunchKernelGGL(k_merge_fin, dim3(1 + (e->U + 63) / 64), dim3(64), 0, X, e->dp, lo, hi, nch, V, e->dspart,
                        e->dapart, extra, e->dacc, e->dsacc, pflag, e->dflag + 1, (const int*)e->plans.d_redo,

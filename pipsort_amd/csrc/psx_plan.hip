@@ -19,6 +19,8 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 #include "psx_mem.h"
 #include "psx_sweep.h"
 #include "psx_sweep_dev.h"
@@ -135,9 +137,19 @@ int plan_csr_device(const int4* d_units, int n_units, int rec_stride, int k, int
                                rec_stride, k, variant, pad, U, keys, vals, d_pos);
         }))
         return -1;
-    if (n == 0) return 0;
+    if (n == 0 || !records_at_csr_positions()) return 0;
     hipLaunchKernelGGL(k_plan_csr_pos, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d_dptr, U, n, d_gidx, d_pos);
     return chk(hipGetLastError());
+}
+
+// PSX_REC_CSR=0 (A/B only): records unit-major as in r01-r05 (slot i at i), the
+// merges gather through gidx; the fold order, hence every result, is the same
+bool records_at_csr_positions() {
+    static const bool on = [] {
+        const char* e = std::getenv("PSX_REC_CSR");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 // the CSR of records laid out flat with SNP keys[i] (-1: none): dptr[U + 1],

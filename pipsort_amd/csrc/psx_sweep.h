@@ -148,6 +148,7 @@ struct PlanScratch {
     size_t bytes = 0;
 };
 // a plan's record CSR (pos | dptr | gidx) built on the device from its units
+bool records_at_csr_positions();  // plan records written at their CSR positions (default; PSX_REC_CSR=0: unit-major)
 int plan_csr_device(const int4* d_units, int n_units, int rec_stride, int k, int variant, int pad, int U, int* d_pos,
                     int* d_dptr, int* d_gidx, PlanScratch& scratch, hipStream_t st);
 // the CSR of flat records keyed by SNP (-1: none): dptr[U + 1], gidx[n]

@@ -657,8 +657,9 @@ static void host_plan_csr(const SweepPlan& P, const std::vector<int4>& hu, std::
     for (size_t i = 0; i < key.size(); i++)
         if (key[i] >= 0) {  // slot i's record at its CSR position (stable in slot order)
             const int q = fill[key[i]]++;
-            gidx[q] = q;
-            pos[i] = q;
+            const bool csr = records_at_csr_positions();
+            gidx[q] = csr ? q : (int)i;
+            pos[i] = csr ? q : (int)i;
         }
 }
 

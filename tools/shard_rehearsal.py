@@ -31,7 +31,9 @@ def main():
                     help="timed rounds over the ranks, alternating forward / reverse rank order")
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--reverse", action="store_true", help="start the rounds in reverse rank order")
-    ap.add_argument("--sync", action="store_true", help="synchronous passes (merge not overlapped with the next sweep)")
+    ap.add_argument("--sync", action="store_true",
+                    help="single passes: each step = async pass + exchange + psx_sync, nothing overlapping the next "
+                         "(the latency of sweeping one locus once; tools/single_pass.py times each pass alone)")
     ap.add_argument("--no-exchange", action="store_true", help="world > 1 without the export / all-gather / merge")
     args = ap.parse_args()
     torch.cuda.set_device(0)
@@ -57,16 +59,15 @@ def main():
         rank_bytes = torch.arange(world, dtype=torch.int32, device="cuda").view(torch.uint8).view(world, 4)
 
         def step(pc):
-            if args.sync:
-                pc.run_exhaustive()
-            else:
-                pc.run_exhaustive_async()
+            pc.run_exhaustive_async()
             if world > 1 and not args.no_exchange:
                 pc.export_partials(mine.data_ptr())
                 # one copy kernel stands in for the RCCL all-gather
                 gathered.view(world, nb).copy_(mine.view(1, nb).expand(world, nb))
                 gathered.view(world, nb)[:, tag_rank:tag_rank + 4].copy_(rank_bytes)
                 pc.merge_partials(gathered.data_ptr(), world)
+            if args.sync:
+                assert not pc.sync()
 
         acc = [{"step": [], "kernel": [], "sweep": [], "span": []} for _ in range(world)]
         for rd in range(args.rounds):
