@@ -1672,7 +1672,7 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     // (-DPSX_ABLATE_MERGE, a separate timing build only: the pass's merge is
     // skipped and its results are wrong; measures what the merge beside the next
     // sweep costs.  No environment switch: a shipped library always merges.)
-    const bool csr = psx::records_at_csr_positions();
+    const bool csr = mA->csr_pos && (!mB || mB->csr_pos);
 #ifndef PSX_ABLATE_MERGE
     hipLaunchKernelGGL(k_merge_rec, dim3((unsigned)(nch + (size_t)e->U * V)), dim3(64), 0, X, e->dp, lo, (int)nsingle,
                        psx::plan_records(*mA, par), mA->d_dptr, csr ? (const int*)nullptr : mA->d_gidx,

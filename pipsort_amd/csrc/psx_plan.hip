@@ -6,10 +6,10 @@
 // records (t >= 128) of each unit.  The merges need, per union SNP u, the
 // record slots that hold u in increasing slot order (a stable grouping by SNP):
 //   pos[i]   = the buffer position of slot i's record, -1: no SNP (the sweep
-//              kernels skip it); since r06 its CSR position q (below), so each
-//              SNP's records are contiguous in the buffer
+//              kernels skip it): i (unit-major), or, for world > 1 since r06,
+//              its CSR position q (below), so each SNP's records are contiguous
 //   gidx[q]  = the buffer position of the q-th record in (SNP, slot) order
-//              (the identity since r06)
+//              (the slot, or the identity with CSR positions)
 //   dptr[u]  = first q of SNP u (dptr[U] = records in all): u's run is
 //              [dptr[u], dptr[u + 1])
 // Built on the host this was ~2M-element passes (8 ms per locus on the
@@ -130,26 +130,30 @@ int sort_to_csr(long n, int U, int* d_dptr, int* d_gidx, PlanScratch& S, hipStre
 }
 
 int plan_csr_device(const int4* d_units, int n_units, int rec_stride, int k, int variant, int pad, int U, int* d_pos,
-                    int* d_dptr, int* d_gidx, PlanScratch& S, hipStream_t st) {
+                    int* d_dptr, int* d_gidx, PlanScratch& S, hipStream_t st, bool csr_pos) {
     const long n = (long)n_units * rec_stride;
     if (sort_to_csr(n, U, d_dptr, d_gidx, S, st, [&](int* keys, int* vals) {
             hipLaunchKernelGGL(k_plan_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d_units, n,
                                rec_stride, k, variant, pad, U, keys, vals, d_pos);
         }))
         return -1;
-    if (n == 0 || !records_at_csr_positions()) return 0;
+    if (n == 0 || !csr_pos) return 0;
     hipLaunchKernelGGL(k_plan_csr_pos, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d_dptr, U, n, d_gidx, d_pos);
     return chk(hipGetLastError());
 }
 
-// PSX_REC_CSR=0 (A/B only): records unit-major as in r01-r05 (slot i at i), the
-// merges gather through gidx; the fold order, hence every result, is the same
-bool records_at_csr_positions() {
-    static const bool on = [] {
+// Where a shard's records go (the fold order, hence every result, is the same
+// either way): at their CSR positions for world > 1, where the merge is a large
+// share of a single pass (world 8 0.165 -> 0.162 ms); unit-major (slot i at i,
+// the merges gather through gidx) at world 1, where the sweep's coalesced record
+// stores win (kernel 0.758 vs 0.771 ms, bench step 0.798 vs 0.806 ms, same-box
+// A/B, profiles/r06/r06q_*).  PSX_REC_CSR = 0 / 1 forces either.
+bool records_at_csr_positions(int world) {
+    static const int force = [] {
         const char* e = std::getenv("PSX_REC_CSR");
-        return !(e && e[0] == '0');
+        return e ? (e[0] == '0' ? 0 : 1) : -1;
     }();
-    return on;
+    return force >= 0 ? force == 1 : world > 1;
 }
 
 // the CSR of records laid out flat with SNP keys[i] (-1: none): dptr[U + 1],

@@ -86,6 +86,7 @@ struct SweepPlan {
     // the unit list on the host until upload_plan (plans built ahead on a host thread)
     std::vector<int4> h_units;
     bool uploaded = false;
+    bool csr_pos = false;        // records at their CSR positions (gidx the identity): records_at_csr_positions
 };
 
 // Arguments of the k = 3 fast kernel (psx_sweep3.hip).  Sweep indices live in
@@ -148,9 +149,10 @@ struct PlanScratch {
     size_t bytes = 0;
 };
 // a plan's record CSR (pos | dptr | gidx) built on the device from its units
-bool records_at_csr_positions();  // plan records written at their CSR positions (default; PSX_REC_CSR=0: unit-major)
+// plan records written at their CSR positions (world > 1) or unit-major (world 1); PSX_REC_CSR forces
+bool records_at_csr_positions(int world);
 int plan_csr_device(const int4* d_units, int n_units, int rec_stride, int k, int variant, int pad, int U, int* d_pos,
-                    int* d_dptr, int* d_gidx, PlanScratch& scratch, hipStream_t st);
+                    int* d_dptr, int* d_gidx, PlanScratch& scratch, hipStream_t st, bool csr_pos);
 // the CSR of flat records keyed by SNP (-1: none): dptr[U + 1], gidx[n]
 int csr_from_keys_device(const int* d_keys, long n, int U, int* d_dptr, int* d_gidx, PlanScratch& scratch,
                          hipStream_t st);

@@ -617,8 +617,9 @@ static int upload_plan(SweepPlan& P, SweepPlanCache& C, hipStream_t st) {
     P.d_pos = P.d_csr;
     P.d_dptr = P.d_csr + n;
     P.d_gidx = P.d_csr + n + P.U + 1;
+    P.csr_pos = records_at_csr_positions(P.world);
     if (plan_csr_device(P.d_units, P.n_units, P.rec_stride, P.k, P.variant, P.pad, P.U, const_cast<int*>(P.d_pos),
-                        const_cast<int*>(P.d_dptr), const_cast<int*>(P.d_gidx), C.csr_scratch, st)) {
+                        const_cast<int*>(P.d_dptr), const_cast<int*>(P.d_gidx), C.csr_scratch, st, P.csr_pos)) {
         g_sweep_err = "plan CSR on the device failed";
         return -1;
     }
@@ -657,7 +658,7 @@ static void host_plan_csr(const SweepPlan& P, const std::vector<int4>& hu, std::
     for (size_t i = 0; i < key.size(); i++)
         if (key[i] >= 0) {  // slot i's record at its CSR position (stable in slot order)
             const int q = fill[key[i]]++;
-            const bool csr = records_at_csr_positions();
+            const bool csr = records_at_csr_positions(P.world);
             gidx[q] = csr ? q : (int)i;
             pos[i] = csr ? q : (int)i;
         }
