@@ -513,17 +513,33 @@ __device__ __forceinline__ void eval_batch_row(const DevProb& P, const int* in, 
     }
     eval_set<KM>(P, row, stride, nullptr, srec + set, mrec + (size_t)set * stride, score ? score + set : nullptr);
 }
+// tstamp (optional, pinned host): block 0 stores its start clock (the batch's
+// kernel time without dispatch events, see eval_generic_staged)
 #define PSX_EVAL_BATCH_ARGS                                                                                   \
     DevProb P, const int *in, int *out, int stride, SetRec null1, double L0, unsigned long long badv,         \
         unsigned long long *__restrict__ bad, unsigned long long *__restrict__ hbad, SetRec *__restrict__ srec, \
-        Acc5 *__restrict__ mrec, double *__restrict__ score
+        Acc5 *__restrict__ mrec, double *__restrict__ score, unsigned long long *__restrict__ tstamp
 __global__ __launch_bounds__(64) void k_eval_batch(PSX_EVAL_BATCH_ARGS) {
+    if (tstamp && blockIdx.x == 0 && threadIdx.x == 0) *tstamp = wall_clock64();
     eval_batch_row<PSX_KMAX>(P, in, out, stride, null1, L0, badv, bad, hbad, srec, mrec, score);
 }
 // rows of at most 5 members: 96 registers, 5 waves per SIMD (the 6-member
 // instance needs 113: 4 waves)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_eval_batch5(PSX_EVAL_BATCH_ARGS) {
+    if (tstamp && blockIdx.x == 0 && threadIdx.x == 0) *tstamp = wall_clock64();
     eval_batch_row<5>(P, in, out, stride, null1, L0, badv, bad, hbad, srec, mrec, score);
+}
+
+// n ints out of pinned host memory (the staging buffer) into device memory,
+// 16 bytes a lane, the last lane the tail: an SDMA copy instead costs a ~16 us
+// engine hand-off before the next launch on the stream (r06t)
+__global__ __launch_bounds__(256) void k_stage_rows(const int* __restrict__ src, size_t n, int* __restrict__ dst) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x, n4 = n / 4;
+    if (i < n4) {
+        reinterpret_cast<int4*>(dst)[i] = reinterpret_cast<const int4*>(src)[i];
+    } else if (i == n4) {
+        for (size_t j = 4 * n4; j < n; j++) dst[j] = src[j];
+    }
 }
 #undef PSX_EVAL_BATCH_ARGS
 
@@ -910,7 +926,9 @@ struct psx_engine {
     int* hstage = nullptr;
     size_t cap_stage = 0;
     hipEvent_t stage_ev = nullptr;  // last upload out of hstage (reuse waits on it)
+    unsigned long long* hbclk = nullptr;  // [2] pinned coherent: a user batch's kernel clocks
     bool stage_rec = false;
+    bool stage_open = false;  // an upload out of hstage is enqueued, its event not yet
     double* dscore = nullptr;       // per-set scores (SSS), read back compactly
     size_t cap_score = 0;
     double* hscore = nullptr;
@@ -997,6 +1015,7 @@ psx_engine::~psx_engine() {
     if (hstat) psx::hfree(hstat);
     if (stage_ev) { hipEventSynchronize(stage_ev); hipEventDestroy(stage_ev); }
     if (hstage) psx::hfree(hstage);
+    if (hbclk) psx::hfree(hbclk);
     if (hscore) psx::hfree(hscore);
     psx::dfree(dgen); psx::dfree(dgcsr); psx::dfree(dbm); psx::dfree(gscratch.p); psx::dfree(dscore); psx::dfree(dsrec); psx::dfree(dmrec); psx::dfree(dpass); psx::dfree(dspart); psx::dfree(dapart); psx::dfree(dstamps);
     if (hstamps) psx::hfree(hstamps);
@@ -1092,7 +1111,12 @@ void build_csr(const std::vector<int>& sets, int stride, size_t nsets, int U, st
 
 // The pinned staging buffer, n ints, once its previous upload is done.
 int stage_acquire(psx_engine* e, size_t n, int** out) {
-    if (e->stage_rec) HIPCHK(hipEventSynchronize(e->stage_ev));
+    if (e->stage_open) {
+        HIPCHK(hipStreamSynchronize(e->stream));  // (an upload whose call failed before its event)
+        e->stage_open = false;
+    } else if (e->stage_rec) {
+        HIPCHK(hipEventSynchronize(e->stage_ev));
+    }
     int rc = ensure_host(e->hstage, e->cap_stage, n);
     if (rc) return rc;
     *out = e->hstage;
@@ -1132,26 +1156,34 @@ int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool accumulate
     unsigned long long* dbad = user ? reinterpret_cast<unsigned long long*>(e->dflag + 10) : nullptr;
     if (chunked && (rc = ensure(e->dbm, e->cap_bm, psx::batch_merge_bytes((long)nsets, stride, e->U)))) return rc;
     if (accumulate && !chunked && (rc = ensure(e->dgcsr, e->cap_gcsr, (size_t)e->U + 1 + n_sets))) return rc;
-    // the rows: one upload out of the pinned staging buffer (a kernel reading
-    // them from host memory measured 36 -> 55 us, r05w)
-    HIPCHK(hipMemcpyAsync(e->dgen, e->hstage, n_sets * sizeof(int), hipMemcpyHostToDevice, e->stream));
-    if (!e->stage_ev) HIPCHK(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
-    HIPCHK(hipEventRecord(e->stage_ev, e->stream));
-    e->stage_rec = true;
-    if (kernel_ms) HIPCHK(hipEventRecord(e->ev[2], e->stream));
+    // the rows: one upload out of the pinned staging buffer, by a copy kernel on
+    // the stream (a kernel reading them from host memory in the evaluation
+    // itself measured 36 -> 55 us, r05w)
+    hipLaunchKernelGGL(k_stage_rows, dim3((unsigned)((n_sets / 4 + 1 + 255) / 256)), dim3(256), 0, e->stream,
+                       e->hstage, n_sets, e->dgen);
+    e->stage_open = true;
+    HIPCHK(hipGetLastError());
+    // the kernel time of a user batch merged in chunks: in-kernel clocks (the
+    // evaluation's first block start -> the chunk merge's first block start,
+    // pinned host), no timing events around the launch (each costs a ~5 us gap)
+    const bool clocks = kernel_ms && user && chunked;
+    if (clocks && !e->hbclk) HIPCHK(psx::hmalloc_coherent_raw(reinterpret_cast<void**>(&e->hbclk), 64));
+    unsigned long long* const bclk = clocks ? e->hbclk : nullptr;
+    if (bclk) bclk[0] = bclk[1] = 0;
+    if (kernel_ms && !clocks) HIPCHK(hipEventRecord(e->ev[2], e->stream));
     if (user)  // (rows of at most 5 members: the 5-member instance, fewer live registers)
         hipLaunchKernelGGL(stride <= 5 ? k_eval_batch5 : k_eval_batch, dim3((unsigned)nsets), dim3(64), 0,
                            e->stream, e->dp, e->dgen, e->dgen, stride, null_rec(e, 1.0), e->L0, badv, dbad,
                            reinterpret_cast<unsigned long long*>(e->hscore + nsets), e->dsrec, e->dmrec,
-                           scores ? e->hscore : nullptr);
+                           scores ? e->hscore : nullptr, bclk);
     else
         hipLaunchKernelGGL(k_eval_sets, dim3((unsigned)nsets), dim3(64), 0, e->stream, e->dp, e->dgen, stride,
                            nullptr, e->dsrec, e->dmrec, scores ? e->dscore : nullptr);
     HIPCHK(hipGetLastError());
-    if (kernel_ms) HIPCHK(hipEventRecord(e->ev[3], e->stream));
+    if (kernel_ms && !clocks) HIPCHK(hipEventRecord(e->ev[3], e->stream));
     if (chunked) {
         if (psx::launch_merge_batch(e->dgen, stride, (long)nsets, e->U, e->dmrec, e->dsrec, e->dbm, e->dacc,
-                                    e->dsacc, e->stream, dbad, badv))
+                                    e->dsacc, e->stream, dbad, badv, bclk ? bclk + 1 : nullptr))
             return fail(PSX_EHIP, "set-batch merge failed");
     } else if (accumulate) {
         if (user) {
@@ -1171,6 +1203,12 @@ int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool accumulate
         if (psx::launch_merge_sets(e->dsrec, (long)nsets, none, e->dsacc, e->stream))
             return fail(PSX_EHIP, psx::sweep_error());
     }
+    // hstage's reuse waits for this event: recorded after the launches (one
+    // between the copy and the evaluation costs a ~6 us gap, r06u)
+    if (!e->stage_ev) HIPCHK(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(e->stage_ev, e->stream));
+    e->stage_rec = true;
+    e->stage_open = false;
     if (scores && !user) {
         if ((rc = ensure_host(e->hscore, e->cap_hscore, nsets))) return rc;
         HIPCHK(hipMemcpyAsync(e->hscore, e->dscore, nsets * sizeof(double), hipMemcpyDeviceToHost, e->stream));
@@ -1181,7 +1219,10 @@ int eval_generic_staged(psx_engine* e, int stride, size_t nsets, bool accumulate
         return fail(PSX_EINVAL, "sets must be ascending union indices");
     if (scores)
         for (size_t i = 0; i < nsets; i++) scores[i] = e->K + e->hscore[i];
-    if (kernel_ms) {
+    if (clocks) {
+        const unsigned long long t0 = bclk[0], t1 = bclk[1];
+        *kernel_ms += t1 > t0 ? (double)(t1 - t0) / (double)e->wclk_khz : 0.0;
+    } else if (kernel_ms) {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
         *kernel_ms += ms;
@@ -2346,7 +2387,7 @@ int psx_eval_union_batch(psx_engine* e, const int32_t* sets, int32_t stride, int
     // validates and compacts them and evaluates the null rows.  Slices of at
     // most kBatchChunks merge chunks (an SSS neighbourhood is one slice).
     std::memset(&e->timing, 0, sizeof(e->timing));
-    const size_t per = (size_t)kBatchChunks * (size_t)(512 / stride);
+    const size_t per = (size_t)kBatchChunks * (size_t)psx::batch_merge_sets_per_chunk(stride);
     double kms = 0, prep = 0;
     int rc;
     if ((size_t)n_sets > per) {

@@ -170,9 +170,9 @@ int csr_from_keys_device(const int* d_keys, long n, int U, int* d_dptr, int* d_g
 // records of n union sets ([set][stride], record j of a set = its j-th member)
 // into the per-SNP accumulators and the set records into the scalars, in two
 // launches and a fixed order, without a device-wide sort.
-//   k_batch_part  chunk c = 512 records of whole sets: a wave radix-sorts the
+//   k_batch_part  chunk c = 256 records of whole sets: a wave radix-sorts the
 //                 chunk's (SNP, record) pairs in LDS; each thread folds the runs
-//                 of its 8 sorted positions, a fixed binary tree over the
+//                 of its 4 sorted positions, a fixed binary tree over the
 //                 threads joins the runs that cross threads; every SNP's chunk
 //                 total goes to part[c][u] + a presence bit, the chunk's set
 //                 records to spart[c]
@@ -182,7 +182,7 @@ int csr_from_keys_device(const int* d_keys, long n, int U, int* d_dptr, int* d_g
 // ---------------------------------------------------------------------------
 namespace {
 
-constexpr int kBT = 64, kBI = 8;  // a chunk: one wave, 512 records (more chunks in flight, no cross-wave sort)
+constexpr int kBT = 64, kBI = 4;  // a chunk: one wave, 256 records (more chunks in flight, no cross-wave sort)
 constexpr int kBWords = 4096;  // presence bitmap words in LDS: U <= 131072
 
 // A run of equal SNPs over a range of sorted positions: the first and last runs
@@ -198,7 +198,8 @@ __global__ __launch_bounds__(kBT) void k_batch_part(const int* __restrict__ sets
                                                    const SetRec* __restrict__ srec, Acc5* __restrict__ part,
                                                    unsigned* __restrict__ bits, int words, SetRec* __restrict__ spart,
                                                    const unsigned long long* __restrict__ bad,
-                                                   unsigned long long badv) {
+                                                   unsigned long long badv, unsigned long long* __restrict__ tstamp) {
+    if (tstamp && blockIdx.x == 0 && threadIdx.x == 0) *tstamp = wall_clock64();  // (the batch's kernel clock)
     if (bad && *bad == badv) return;  // an invalid row: the batch adds nothing (uniform)
     using Sort = hipcub::BlockRadixSort<int, kBT, kBI, int>;
     __shared__ union {
@@ -349,6 +350,8 @@ __global__ __launch_bounds__(256) void k_batch_fold(const Acc5* __restrict__ par
 
 }  // namespace
 
+int batch_merge_sets_per_chunk(int stride) { return (kBT * kBI) / stride; }
+
 int batch_merge_chunks(long nsets, int stride) {
     const long spc = (kBT * kBI) / stride;
     return (int)((nsets + spc - 1) / spc);
@@ -361,7 +364,7 @@ size_t batch_merge_bytes(long nsets, int stride, int U) {
 
 int launch_merge_batch(const int* d_sets, int stride, long nsets, int U, const Acc5* rec, const SetRec* srec,
                        void* scratch, Acc5* acc, SetRec* sacc, hipStream_t st, const unsigned long long* bad,
-                       unsigned long long badv) {
+                       unsigned long long badv, unsigned long long* tstamp) {
     if (nsets <= 0) return 0;
     const int words = (U + 31) / 32;
     if (words > kBWords || stride < 1 || stride > kBT * kBI) return -1;
@@ -372,7 +375,7 @@ int launch_merge_batch(const int* d_sets, int stride, long nsets, int U, const A
     SetRec* spart = (SetRec*)(part + (size_t)nc * U);
     unsigned* bits = (unsigned*)(spart + nc);
     hipLaunchKernelGGL(k_batch_part, dim3(nc), dim3(kBT), 0, st, d_sets, stride, nsets, spc, U, end_bit, rec, srec,
-                       part, bits, words, spart, bad, badv);
+                       part, bits, words, spart, bad, badv, tstamp);
     if (chk(hipGetLastError())) return -1;
     hipLaunchKernelGGL(k_batch_fold, dim3((U + 3) / 4), dim3(256), 0, st, part, bits, words, nc, U, spart, acc,
                        sacc, bad, badv);

@@ -161,11 +161,15 @@ int csr_from_keys_device(const int* d_keys, long n, int U, int* d_dptr, int* d_g
 // in a fixed order (psx_plan.hip); scratch of batch_merge_bytes(); -1 when U
 // or stride is outside the kernels' range (use the CSR merge).  bad (device,
 // optional): the merges add nothing when *bad == badv (an invalid batch).
+// tstamp (optional, host or device): the first merge's block 0 stores its start
+// clock there.
 size_t batch_merge_bytes(long nsets, int stride, int U);
 int batch_merge_chunks(long nsets, int stride);
+int batch_merge_sets_per_chunk(int stride);  // whole sets per merge chunk
 int launch_merge_batch(const int* d_sets, int stride, long nsets, int U, const Acc5* rec, const SetRec* srec,
                        void* scratch, Acc5* acc, SetRec* sacc, hipStream_t st,
-                       const unsigned long long* bad = nullptr, unsigned long long badv = 0);
+                       const unsigned long long* bad = nullptr, unsigned long long badv = 0,
+                       unsigned long long* tstamp = nullptr);
 // GPU self-check: the device CSR of a plan equals the host restatement's
 int plan_csr_selftest(int U, const unsigned char* pres, int k, int rank, int world, int variant, long* mismatches,
                       long* records);
