@@ -1,19 +1,41 @@
-"""Time process exit of tools/exit_probe.bin per mode (5 reps each): the gap
-between the epoch the probe prints just before _exit(0) and the parent seeing
-it end.  python tools/exit_probe.py"""
+"""How long a HIP process takes to go away after _exit: tools/init_probe (a
+bare HIP start-up, optionally holding device / pinned memory) and the drop-in
+CLI on tests/example, each in fresh processes; the exit is the child's
+monotonic clock at _exit (its end_ms / PSX_TIMING "end") to the parent's
+return from wait.  Developer tool.
+
+    python tools/exit_probe.py [--reps 4]
+"""
+import argparse
 import json
 import os
+import statistics
 import subprocess
+import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for mode in (0, 1, 2, 3):
-    ex, tot = [], []
-    for _ in range(5):
-        t0 = time.time()
-        r = subprocess.run([os.path.join(ROOT, "tools", "exit_probe.bin"), str(mode)], capture_output=True, text=True)
-        t1 = time.time()
-        d = json.loads(r.stdout.strip().splitlines()[-1])
-        ex.append(t1 * 1e3 - d["exit_epoch_ms"])
-        tot.append((t1 - t0) * 1e3)
-    print(json.dumps({"mode": mode, "exit_ms": sorted(ex), "wall_ms": sorted(tot), "last": d}), flush=True)
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--reps", type=int, default=4)
+a = ap.parse_args()
+probe = os.path.join(ROOT, "tools", "init_probe")
+for args in ([], ["0", "0"], ["1024", "0"], ["16384", "0"], ["0", "256"]):
+    ex = []
+    for _ in range(a.reps):
+        p = subprocess.Popen([probe, "0"] + args, stdout=subprocess.PIPE, text=True)
+        line = p.stdout.readline()
+        p.wait()
+        t = time.monotonic() * 1e3
+        d = json.loads(line)
+        ex.append(t - d["end_ms"])
+    print(f"init_probe {' '.join(args) or '(bare)'}: exit {statistics.median(ex):.1f} ms "
+          f"(min {min(ex):.1f}, of {a.reps}); device MiB / pinned MiB held: {args or ['0', '0']}", flush=True)
+
+import bench  # noqa: E402
+
+for _ in range(2):
+    w, same, ph = bench.example_wall()
+    print(f"CLI tests/example: wall {w:.3f} s, outputs match {same}, exit_ms {ph.get('exit_ms') if ph else None}",
+          flush=True)

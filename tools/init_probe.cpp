@@ -1,6 +1,9 @@
 // Cold-start split of a one-locus process (tests/example wall):
 // hsa_init alone, then the HIP runtime (hipGetDeviceCount), context
-// (hipFree(0)), first launch.  Prints one JSON line.  Developer tool:
+// (hipFree(0)), first launch.  Prints one JSON line, with the monotonic clock
+// at _exit (end_ms: the parent times the exit, tools/exit_probe.py).  Optional
+// argv[2] / argv[3]: MiB of device / pinned host memory held at exit.
+// Developer tool:
 //   hipcc --offload-arch=gfx950 -O2 -o tools/init_probe tools/init_probe.cpp -lhsa-runtime64
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
@@ -35,8 +38,14 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, nullptr, d);
     (void)hipDeviceSynchronize();
     const double t5 = now_ms();
+    const size_t dmb = argc > 2 ? (size_t)atol(argv[2]) : 0, hmb = argc > 3 ? (size_t)atol(argv[3]) : 0;
+    void *big = nullptr, *pin = nullptr;
+    if (dmb) (void)hipMalloc(&big, dmb << 20);
+    if (hmb) (void)hipHostMalloc(&pin, hmb << 20);
+    const double t6 = now_ms();
     printf("{\"hsa_init_ms\": %.2f, \"hip_device_count_ms\": %.2f, \"context_ms\": %.2f, \"malloc_ms\": %.2f, "
-           "\"first_launch_ms\": %.2f, \"devices\": %d}\n", t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, n);
+           "\"first_launch_ms\": %.2f, \"held_alloc_ms\": %.2f, \"devices\": %d, \"end_ms\": %.3f}\n",
+           t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, t6 - t5, n, now_ms());
     fflush(stdout);
     _exit(0);
 }
