@@ -222,7 +222,10 @@ __global__ __launch_bounds__(kBT) void k_batch_part(const int* __restrict__ sets
         key[j] = v >= 0 ? v : U;  // no SNP: sorted behind every SNP
         val[j] = i;
     }
-    Sort(sh.sort).Sort(key, val, 0, end_bit);  // blocked: thread t holds sorted positions 8t .. 8t + 7
+    // the chunk's set records, thread-strided (their loads overlap the sort)
+    SetRec a = set_zero();
+    for (long i = s0 + t; i < s1; i += kBT) fold_set(a, srec[i]);
+    Sort(sh.sort).Sort(key, val, 0, end_bit);  // blocked: thread t holds sorted positions kBI t .. kBI t + kBI - 1
     Acc5 r[kBI];
 #pragma unroll
     for (int j = 0; j < kBI; j++) r[j] = key[j] < U ? rc[val[j]] : acc_zero();
@@ -291,9 +294,7 @@ __global__ __launch_bounds__(kBT) void k_batch_part(const int* __restrict__ sets
         emit(A.fk, A.F);
         if (!A.full) emit(A.lk, A.L);
     }
-    // the chunk's set records, thread-strided then wave and block trees
-    SetRec a = set_zero();
-    for (long i = s0 + t; i < s1; i += kBT) fold_set(a, srec[i]);
+    // the chunk's set records: wave and block trees
     wave_fold_set(a);
     if ((t & 63) == 0) sw[t >> 6] = a;
     __syncthreads();
@@ -317,22 +318,33 @@ __global__ __launch_bounds__(256) void k_batch_fold(const Acc5* __restrict__ par
     const int lane = threadIdx.x & 63;
     const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (u < U) {
+        // every load up front (the accumulator, the presence words and the
+        // partials of all the lane's chunks, absent ones discarded): one round
+        // trip instead of three dependent ones
+        Acc5 a0 = acc_zero();
+        if (lane == 0) a0 = acc[u];
+        unsigned w[4];
+        Acc5 q[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int c = lane + 64 * r;
+            w[r] = c < nc ? bits[(size_t)c * words + (u >> 5)] : 0u;
+            q[r] = c < nc ? part[(size_t)c * U + u] : acc_zero();
+        }
         Acc5 g = acc_zero();
         bool have = false;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            const int c = lane + 64 * r;
-            if (c < nc && ((bits[(size_t)c * words + (u >> 5)] >> (u & 31)) & 1u)) {
-                fold_acc(g, part[(size_t)c * U + u]);
+            if ((w[r] >> (u & 31)) & 1u) {
+                fold_acc(g, q[r]);
                 have = true;
             }
         }
         if (__ballot(have)) {
             wave_fold_acc(g);
             if (lane == 0) {
-                Acc5 a = acc[u];
-                fold_acc(a, g);
-                acc[u] = a;
+                fold_acc(a0, g);
+                acc[u] = a0;
             }
         }
     }
