@@ -479,7 +479,7 @@ def test_union_batch_rejects_bad_rows(gpu, row):
 
 
 def test_union_batch_rejects_bad_row_past_first_slice(gpu):
-    """A batch of several device slices (43,520 rows per slice at stride 3) with
+    """A batch of several device slices (21,760 rows per slice at stride 3) with
     one bad row in the second slice: the call fails with EINVAL and adds
     nothing — the first slice is not merged before the bad row is seen."""
     ld, z, _, _, u2l = synth.syn_v1(90)
