@@ -1926,7 +1926,13 @@ int create_impl(const psx_problem* p, const psx_ld_problem* ld, int device, psx_
     }
     const double alloc_ms = since(ta);
     const clk::time_point tb = clk::now();
+    psx::LuJoin join;  // the two studies' first elimination in joint launches
     auto study = [&](int s) {
+        struct Leave {  // however this study ends, the other does not wait for it
+            psx::LuJoin& j;
+            int s;
+            ~Leave() { j.leave(s); }
+        } leave{join, s};
         Scratch& x = sc[s];
         auto die = [&](int code, const std::string& msg) { x.code = code; x.err = msg; };
         if (hipSetDevice(device) != hipSuccess) return die(PSX_EHIP, "set device");
@@ -1942,7 +1948,7 @@ int create_impl(const psx_problem* p, const psx_ld_problem* ld, int device, psx_
         if (ld) {
             psx::LdStudyResult& r = x.r;
             std::string err;
-            if (psx::ld_study_setup(ld->ld + boff, ld->z + soff, M, st, x.dS, x.dyl, &r, &err))
+            if (psx::ld_study_setup(ld->ld + boff, ld->z + soff, M, st, x.dS, x.dyl, &r, &err, &join, s))
                 return die(PSX_EHIP, "GPU model setup: " + err);
             if (r.path == 0) {
                 lowrank = false;

@@ -4,6 +4,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
+#include <mutex>
 #include <string>
 
 namespace psx {
@@ -31,10 +33,39 @@ int lu_det_device(double* dA, int n, int* dswp, double* ddiag, hipStream_t st, d
 int elim_device(const double* a, int n, const double* z, int check, double* piv, double* zt, int* swap,
                 std::string* err);
 
+// The two studies' first PSD-shift elimination in joint launches (r07): each
+// study's thread arrives in ld_study_setup with its shifted copy and z staged
+// on its stream; study 0's thread then enqueues both matrices' panels, one
+// k_lu_step per panel index, on its stream, and study 1's stream waits for
+// them.  The two studies' separate panel launches contended for the CUs (a
+// panel every 18-21 us per study instead of 16 alone, profiles/r07).  A study
+// that arrives without a matrix (an early failure; the caller's guard calls
+// leave() when the study's setup returns) leaves the other to its own
+// launches.  Later shift iterations and the pivoting path stay per study.
+struct LuJoin {
+    std::mutex m;
+    std::condition_variable cv;
+    bool in[2] = {false, false};   // arrived (with or without a matrix)
+    bool mat[2] = {false, false};  // arrived with a matrix
+    double* A[2] = {nullptr, nullptr};
+    double* z[2] = {nullptr, nullptr};
+    double* work[2] = {nullptr, nullptr};
+    int* flag[2] = {nullptr, nullptr};
+    int n[2] = {0, 0};
+    hipStream_t st[2] = {nullptr, nullptr};
+    hipEvent_t ready = nullptr;  // study 1's matrix staged on its stream
+    hipEvent_t done = nullptr;   // the joint panels, on study 0's stream
+    int state = 0;               // 0: pending, 1: enqueued, 2: the enqueue failed
+    std::string err;
+    void leave(int s);
+    ~LuJoin();
+};
+
 // One study: LD (host, row-major M x M as parsed, util.cpp:86-96) and z (host,
 // M) -> dS = Sigma~_s (device, row-major M x M) and dy = y_s (device, M).
+// join / s: the first elimination joint with the other study (see LuJoin).
 int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, double* dS, double* dy,
-                   LdStudyResult* res, std::string* err);
+                   LdStudyResult* res, std::string* err, LuJoin* join = nullptr, int s = 0);
 
 // The reference's eigen route for a study whose Sigma' is not positive
 // definite (util.cpp:228-263, model.h:213-259), on the GPU (psx_eigen.hip): sig

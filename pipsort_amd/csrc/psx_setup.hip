@@ -237,11 +237,24 @@ constexpr int kStepRows = 48;   // tile rows per row wave (it holds them with D'
 constexpr int kStepWaves = 16;  // waves per block
 static_assert(kStepRows + kPanel == 64, "a row wave holds D and its tile rows");
 
+// One matrix of a k_lu_step launch.  A launch carries up to two (the setup's
+// two studies, r07): blockIdx.z picks the matrix, so both studies' panels take
+// one launch each instead of two launches contending for the CUs; a block
+// outside its matrix's trailing part returns at once.
+struct LuSet {
+    double* A;    // n x n row-major, eliminated in place
+    double* z;    // forward-solved in place (may be null)
+    int* flag;    // raised when a row swap is needed (check)
+    double* dg;   // U_ii of the panels' diagonal blocks, kept aside
+    double* zf;   // their final z, kept aside
+    int n, check;
+};
+struct LuSets {
+    LuSet s[2];
+};
+
 template <int RW, int CW>
-__global__ __launch_bounds__(64 * kStepWaves) void k_lu_step(double* __restrict__ A, int n, int j0,
-                                                               double* __restrict__ z, int check,
-                                                               int* __restrict__ flag, double* __restrict__ dg,
-                                                               double* __restrict__ zf,
+__global__ __launch_bounds__(64 * kStepWaves) void k_lu_step(const LuSets P, int j0,
                                                                unsigned long long* __restrict__ tr) {
 #pragma clang fp contract(off)
     constexpr int nb = kPanel;
@@ -253,15 +266,27 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_lu_step(double* __restrict_
     __shared__ double sL[TR][kPanel + 1];      // l of the tile's rows
     __shared__ double sU[kPanel][TC];          // u of the tile's columns
     __shared__ unsigned long long sSkip;
-    const int tb = (blockIdx.x == 0 && blockIdx.y == 0) ? 0 : (blockIdx.x == 1 && blockIdx.y == 1) ? 1 : -1;
+    const LuSet& S = blockIdx.z ? P.s[1] : P.s[0];
+    double* __restrict__ A = S.A;
+    double* __restrict__ z = S.z;
+    int* __restrict__ flag = S.flag;
+    const int n = S.n, check = S.check;
+    const int tb = blockIdx.z ? -1
+                              : (blockIdx.x == 0 && blockIdx.y == 0) ? 0 : (blockIdx.x == 1 && blockIdx.y == 1) ? 1 : -1;
     auto stamp = [&](int i) {
         if (tr && tb >= 0 && threadIdx.x == 0) tr[tb * 8 + i] = wall_clock64();
     };
     stamp(0);
-    if (check && *flag) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int j1 = j0 + nb;
     const int i0 = j1 + blockIdx.y * TR, k0 = j1 + blockIdx.x * TC;
+    // outside this matrix's trailing part (the grid covers the larger of a
+    // launch's matrices): no rows or columns to update, and the D rows' swap
+    // check is block (0, 0)'s as well
+    if (i0 >= n || k0 >= n) return;
+    if (check && *flag) return;
+    double* __restrict__ dg = S.dg;
+    double* __restrict__ zf = S.zf;
     const bool corner = blockIdx.x == 0 && blockIdx.y == 0;
     // the update's operands first (its first chunk of rows): their latency hides
     // behind the panel pass
@@ -390,24 +415,31 @@ __global__ __launch_bounds__(64 * kStepWaves) void k_lu_step(double* __restrict_
     stamp(3);
 }
 
-// one panel's k_lu_step: the smallest tile whose grid fits one round of blocks
-// (one 1024-thread block per CU), else the largest
-void launch_lu_step(double* A, int n, int j0, double* z, int check, int* flag, double* dg, double* zf,
-                    unsigned long long* tr, hipStream_t st) {
-    const int rest = n - j0 - kPanel;
+// one panel's k_lu_step over the matrices of P that still have a trailing part
+// at j0: the smallest tile whose blocks (summed over the matrices) fit one
+// round (one 1024-thread block per CU), else the largest
+void launch_lu_step(const LuSets& P, int ns, int j0, unsigned long long* tr, hipStream_t st) {
+    int rest = 0;  // the grid's extent: the largest trailing part
+    for (int s = 0; s < ns; s++) rest = std::max(rest, P.s[s].n - j0 - kPanel);
     auto blocks = [&](int rw, int cw) {
-        return (long)((rest + kStepRows * rw - 1) / (kStepRows * rw)) * ((rest + 64 * cw - 1) / (64 * cw));
+        long b = 0;
+        for (int s = 0; s < ns; s++) {
+            const int r = P.s[s].n - j0 - kPanel;
+            if (r > 0) b += (long)((r + kStepRows * rw - 1) / (kStepRows * rw)) * ((r + 64 * cw - 1) / (64 * cw));
+        }
+        return b;
     };
     constexpr long kRound = 256;
     const dim3 b(64 * kStepWaves);
 #define PSX_LU_STEP(RW, CW)                                                                                         \
-    hipLaunchKernelGGL((k_lu_step<RW, CW>), dim3((rest + 64 * CW - 1) / (64 * CW),                                  \
-                                                 (rest + kStepRows * RW - 1) / (kStepRows * RW)),                   \
-                       b, 0, st, A, n, j0, z, check, flag, dg, zf, tr)
+    hipLaunchKernelGGL((k_lu_step<RW, CW>),                                                                         \
+                       dim3((rest + 64 * CW - 1) / (64 * CW), (rest + kStepRows * RW - 1) / (kStepRows * RW), ns), \
+                       b, 0, st, P, j0, tr)
     if (blocks(1, 1) <= kRound) PSX_LU_STEP(1, 1);
     else if (blocks(1, 2) <= kRound) PSX_LU_STEP(1, 2);
     else if (blocks(2, 2) <= kRound) PSX_LU_STEP(2, 2);
-    else PSX_LU_STEP(2, 4);
+    else if (blocks(2, 4) <= kRound) PSX_LU_STEP(2, 4);
+    else PSX_LU_STEP(3, 4);
 #undef PSX_LU_STEP
 }
 
@@ -605,11 +637,18 @@ int enqueue_lu(double* A, int n, int* dswp, hipStream_t st, std::string* err) {
 // row swap (A is then partly eliminated: recopy and pivot).  Afterwards A's
 // diagonal holds U_ii and z holds z~.  work: 2 n doubles (U_ii / z kept aside).  Returns -1 with *err set when a
 // launch failed (the HIP error is read once, here).
-int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipStream_t st, std::string* err,
-                     bool check = true) {
-    if (chk(hipMemsetAsync(flag, 0, sizeof(int), st), "memset", err)) return -1;
-    // PSX_LU_TRACE (diagnostics): per-panel phase clocks of two tiles, averaged on stderr
+// The matrices of P (ns of them, each with work = 2 n doubles) in joint
+// launches: every panel of every matrix in one k_lu_step per panel index.
+int enqueue_lu_sets(const LuSets& P, int ns, hipStream_t st, std::string* err) {
+    int nmax = 0;
+    for (int s = 0; s < ns; s++) {
+        if (chk(hipMemsetAsync(P.s[s].flag, 0, sizeof(int), st), "memset", err)) return -1;
+        nmax = std::max(nmax, P.s[s].n);
+    }
+    // PSX_LU_TRACE (diagnostics): per-panel phase clocks of two tiles of the
+    // first matrix, averaged on stderr
     static const bool trace = std::getenv("PSX_LU_TRACE") != nullptr;
+    const int n = P.s[0].n;
     const int npan = std::max(0, (n - 1) / kPanel);
     unsigned long long* tr = nullptr;
     if (trace && npan > 0) {
@@ -617,11 +656,17 @@ int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipSt
         (void)hipMemsetAsync(tr, 0, sizeof(unsigned long long) * 16 * npan, st);
     }
     int p = 0, j0 = 0;
-    for (; j0 + kPanel < n; j0 += kPanel, p++)
-        launch_lu_step(A, n, j0, z, check ? 1 : 0, flag, work, work + n, tr ? tr + 16 * p : nullptr, st);
-    // the last diagonal block (n - j0 <= kPanel rows), then U_ii / z of the others
-    hipLaunchKernelGGL(k_lu_diag_at, dim3(1), dim3(64), 0, st, A, n, j0, z, check ? 1 : 0, flag, (const double*)work,
-                       (const double*)(work + n));
+    for (; j0 + kPanel < nmax; j0 += kPanel, p++)
+        launch_lu_step(P, ns, j0, tr && p < npan ? tr + 16 * p : nullptr, st);
+    // per matrix: the last diagonal block (n - j0 <= kPanel rows), then U_ii / z
+    // of the others
+    for (int s = 0; s < ns; s++) {
+        const LuSet& S = P.s[s];
+        int js = 0;
+        while (js + kPanel < S.n) js += kPanel;
+        hipLaunchKernelGGL(k_lu_diag_at, dim3(1), dim3(64), 0, st, S.A, S.n, js, S.z, S.check, S.flag,
+                           (const double*)S.dg, (const double*)S.zf);
+    }
     if (tr) {
         std::vector<unsigned long long> h(16 * (size_t)npan);
         (void)hipMemcpyAsync(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost, st);
@@ -658,7 +703,77 @@ int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipSt
     return chk(hipGetLastError(), "LU launch", err);
 }
 
+LuSet lu_set(double* A, int n, double* work, int* flag, double* z, bool check) {
+    return LuSet{A, z, flag, work, work + n, n, check ? 1 : 0};
+}
+
+int enqueue_lu_fused(double* A, int n, double* work, int* flag, double* z, hipStream_t st, std::string* err,
+                     bool check = true) {
+    LuSets P{};
+    P.s[0] = lu_set(A, n, work, flag, z, check);
+    return enqueue_lu_sets(P, 1, st, err);
+}
+
+// Study s arrives at its first elimination (LuJoin).  Returns 1 when the joint
+// launches cover this matrix (enqueued on study 0's stream; st ordered after
+// them), 0 when the study eliminates on its own, -1 on a launch error.
+int lu_join_run(LuJoin* J, int s, double* A, int n, double* work, int* flag, double* z, hipStream_t st,
+                std::string* err) {
+    std::unique_lock<std::mutex> lk(J->m);
+    if (s == 1 && (chk(hipEventCreateWithFlags(&J->ready, hipEventDisableTiming), "event", err) ||
+                   chk(hipEventRecord(J->ready, st), "event", err))) {
+        J->in[s] = true;  // arrives without a matrix: the other study goes alone
+        J->cv.notify_all();
+        return -1;
+    }
+    J->A[s] = A;
+    J->n[s] = n;
+    J->work[s] = work;
+    J->flag[s] = flag;
+    J->z[s] = z;
+    J->st[s] = st;
+    J->in[s] = J->mat[s] = true;
+    J->cv.notify_all();
+    J->cv.wait(lk, [&] { return J->in[0] && J->in[1]; });
+    if (!(J->mat[0] && J->mat[1])) return 0;
+    if (s == 1) {
+        J->cv.wait(lk, [&] { return J->state != 0; });
+        if (J->state != 1) {
+            if (err) *err = J->err;
+            return -1;
+        }
+        return chk(hipStreamWaitEvent(st, J->done, 0), "event wait", err) ? -1 : 1;
+    }
+    lk.unlock();
+    std::string e;
+    LuSets P{};
+    for (int q = 0; q < 2; q++) P.s[q] = lu_set(J->A[q], J->n[q], J->work[q], J->flag[q], J->z[q], true);
+    int rc = chk(hipStreamWaitEvent(st, J->ready, 0), "event wait", &e);
+    if (!rc) rc = enqueue_lu_sets(P, 2, st, &e);
+    if (!rc) rc = chk(hipEventCreateWithFlags(&J->done, hipEventDisableTiming), "event", &e);
+    if (!rc) rc = chk(hipEventRecord(J->done, st), "event", &e);
+    lk.lock();
+    J->state = rc ? 2 : 1;
+    J->err = e;
+    J->cv.notify_all();
+    if (rc && err) *err = e;
+    return rc ? -1 : 1;
+}
+
 }  // namespace
+
+void LuJoin::leave(int s) {
+    std::lock_guard<std::mutex> g(m);
+    if (!in[s]) {
+        in[s] = true;
+        cv.notify_all();
+    }
+}
+
+LuJoin::~LuJoin() {
+    if (ready) (void)hipEventDestroy(ready);
+    if (done) (void)hipEventDestroy(done);
+}
 
 int lu_det_device(double* dA, int n, int* dswp, double* ddiag, hipStream_t st, double* det, std::string* err) {
     if (n <= 0) return -1;
@@ -740,7 +855,7 @@ int elim_device(const double* a, int n, const double* z, int check, double* piv,
 }
 
 int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, double* dS, double* dy,
-                   LdStudyResult* res, std::string* err) {
+                   LdStudyResult* res, std::string* err, LuJoin* join, int s) {
     std::memset(res, 0, sizeof(*res));
     using clk = std::chrono::steady_clock;
     auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -791,7 +906,10 @@ int ld_study_setup(const double* ld, const double* z, int M, hipStream_t st, dou
             if (try_fused) {
                 if ((rc = chk(hipMemcpyAsync(dz, z, M * sizeof(double), hipMemcpyHostToDevice, st), "z upload", err)))
                     break;
-                if (enqueue_lu_fused(dA, M, dcol, dflag, dz, st, err)) { rc = -1; break; }
+                // the first elimination in joint launches with the other study (LuJoin)
+                const int jr = (join && it == 0) ? lu_join_run(join, s, dA, M, dcol, dflag, dz, st, err) : 0;
+                if (jr < 0) { rc = -1; break; }
+                if (jr == 0 && enqueue_lu_fused(dA, M, dcol, dflag, dz, st, err)) { rc = -1; break; }
                 hipLaunchKernelGGL(k_get_diag, dim3((M + 255) / 256), dim3(256), 0, st, dA, M, ddiag);
                 if ((rc = chk(hipMemcpyAsync(udiag.data(), ddiag, M * sizeof(double), hipMemcpyDeviceToHost, st),
                               "copy", err)) ||

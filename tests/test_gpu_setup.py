@@ -392,6 +392,36 @@ def test_blocked_swap_free_elimination_bit_identical(gpu, M):
     pc.close()
 
 
+@pytest.mark.parametrize("M0,M1", [(17, 300), (300, 33), (1000, 129), (1, 64)])
+def test_joint_study_elimination_bit_identical(gpu, M0, M1):
+    """The two studies' first elimination runs in joint launches (one
+    k_lu_step per panel index for both matrices, blockIdx.z = study; the grid
+    covers the larger one and the smaller study's blocks past its trailing part
+    return).  Studies of different sizes: each study's shift, min pivot ratio
+    and (M <= 300) ||S'||^2 equal the host restatement's bit for bit."""
+    lds, zs = [], []
+    rng = np.random.default_rng(M0 * 7 + M1)
+    for M, r in ((M0, 0.6), (M1, 0.8)):  # determinants > 0 at these sizes: no shift
+        idx = np.arange(M)
+        lds.append(r ** np.abs(idx[:, None] - idx[None, :]))
+        zs.append(rng.standard_normal(M) * 1.5)
+    U = max(M0, M1)
+    u2l = -np.ones((2, U), dtype=np.int32)
+    u2l[0, :M0] = np.arange(M0)
+    u2l[1, :M1] = np.arange(M1)
+    mi = E.model_inputs(lds, zs, u2l, (6000, 7000), max_causal=1, sharing_param=0.25)
+    pc = E.PostCal(mi)
+    info = pc.setup_info
+    for s in range(2):
+        a = lds[s]
+        assert info["eigen_route"][s] == 0 and info["psd_added"][s] == E.psd_shift(a)[1] == 0.0
+        piv = _elim_pivots(a)
+        assert info["min_pivot_ratio"][s] == piv.min() / np.abs(np.diag(a)).max(), s
+        if a.shape[0] <= 300:
+            assert _bits(info["spsq"][s]) == _bits(_elim_spsq(a, zs[s])), (s, info["spsq"][s])
+    pc.close()
+
+
 @pytest.mark.parametrize("n", [2, 16, 17, 33, 300])
 def test_blocked_pivoting_lu_det_bit_identical(gpu, n, monkeypatch):
     """The blocked partial-pivot elimination (LDS panel with row swaps, swaps
