@@ -33,12 +33,12 @@ int lu_det_device(double* dA, int n, int* dswp, double* ddiag, hipStream_t st, d
 int elim_device(const double* a, int n, const double* z, int check, double* piv, double* zt, int* swap,
                 std::string* err);
 
-// The two studies' first PSD-shift elimination in joint launches (r07): each
+// The two studies' first PSD-shift elimination in joint launches (late r06): each
 // study's thread arrives in ld_study_setup with its shifted copy and z staged
 // on its stream; study 0's thread then enqueues both matrices' panels, one
 // k_lu_step per panel index, on its stream, and study 1's stream waits for
 // them.  The two studies' separate panel launches contended for the CUs (a
-// panel every 18-21 us per study instead of 16 alone, profiles/r07).  A study
+// panel every 18-21 us per study instead of 16 alone, profiles/r06/r06late_a_*).  A study
 // that arrives without a matrix (an early failure; the caller's guard calls
 // leave() when the study's setup returns) leaves the other to its own
 // launches.  Later shift iterations and the pivoting path stay per study.

@@ -238,7 +238,7 @@ constexpr int kStepWaves = 16;  // waves per block
 static_assert(kStepRows + kPanel == 64, "a row wave holds D and its tile rows");
 
 // One matrix of a k_lu_step launch.  A launch carries up to two (the setup's
-// two studies, r07): blockIdx.z picks the matrix, so both studies' panels take
+// two studies, late r06): blockIdx.z picks the matrix, so both studies' panels take
 // one launch each instead of two launches contending for the CUs; a block
 // outside its matrix's trailing part returns at once.
 struct LuSet {
