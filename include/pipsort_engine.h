@@ -115,6 +115,14 @@ int psx_warmup(int device);
  * configs_file != 0 (psx_warmup(d) = psx_warmup_for(d, 3, 0)).  With PSX_TIMING
  * set it prints its phases (context, each code object) on stderr. */
 int psx_warmup_for(int device, int32_t max_causal, int32_t configs_file);
+/* Optional (no reference counterpart), for one-locus processes: on != 0 makes
+ * every handle created afterwards, and the warm-up, share one stream — one
+ * hardware queue — per device.  Every queue a process holds costs ~10-13 ms
+ * when the process exits; the drop-in CLI turns it on before anything else.
+ * Pipelined and multi-rank passes lose their stream priorities and overlap
+ * under it; results are the same.  Call before the first psx_warmup* /
+ * psx_create*. */
+int psx_single_queue(int32_t on);
 
 /* PostCal::PostCal (postcal.h:118-195).  Copies the problem to device `device`,
  * forms Sigma~_s = B_s^T B_s, y_s = B_s^T S'_s and ||S'||^2 on the GPU. */

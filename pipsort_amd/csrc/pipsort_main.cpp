@@ -419,6 +419,11 @@ int main(int argc, char* argv[]) {
     if (devices.empty()) devices.push_back(0);
     const int device = devices[0];
     g_multi = devices.size() > 1;
+    // one locus per process: one stream (hardware queue) per device for the
+    // whole run — each queue costs ~10-13 ms when the process exits
+    // (PSX_SINGLE_QUEUE=0: the engine's own streams, for A/B)
+    const char* sq = getenv("PSX_SINGLE_QUEUE");
+    psx_single_queue(sq ? atoi(sq) : 1);
     // the HIP runtime / contexts come up on a second thread while the inputs
     // are parsed (errors, if any, surface again at psx_create*)
     const int warm_c = sss_flag == 1 ? 0 : totalCausalSNP;  // SSS batches run the generic set kernel

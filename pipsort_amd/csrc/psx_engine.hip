@@ -2116,15 +2116,23 @@ int psx_warmup_for(int device, int32_t max_causal, int32_t configs_file) {
     if ((rc = gpu_ready(device))) return rc;
     HIPCHK(hipFree(nullptr));  // context
     t[1] = now();
-    // one launch loads this translation unit's device code
+    // one launch loads this translation unit's device code; on a pooled
+    // stream (the setup's second study takes it next), not the null stream,
+    // whose hardware queue nothing else would use
     double* d = nullptr;
     HIPCHK(psx::dmalloc(&d, 64 * sizeof(double)));
+    hipStream_t ws = nullptr;
+    HIPCHK(psx::stream_get(&ws, 0));
     ta = now();
-    hipLaunchKernelGGL(k_diag, dim3(1), dim3(64), 0, nullptr, d, 8, d + 8);
+    hipLaunchKernelGGL(k_diag, dim3(1), dim3(64), 0, ws, d, 8, d + 8);
     hipError_t le = hipGetLastError();
     tl = now();
-    hipError_t se = hipDeviceSynchronize();
-    psx::dfree(d);
+    hipError_t se = hipStreamSynchronize(ws);
+    psx::stream_put(ws, 0);
+    {
+        psx::IdleScope idle;  // (ws synchronised)
+        psx::dfree(d);
+    }
     if (le != hipSuccess || se != hipSuccess)
         return fail(PSX_EHIP, std::string("warm-up: ") + hipGetErrorString(le != hipSuccess ? le : se));
     t[2] = now();
@@ -2153,6 +2161,11 @@ int psx_warmup_for(int device, int32_t max_causal, int32_t configs_file) {
 }
 
 int psx_warmup(int device) { return psx_warmup_for(device, 3, 0); }
+
+int psx_single_queue(int32_t on) {
+    psx::set_single_queue(on != 0);
+    return 0;
+}
 
 int psx_lu_det_gpu(const double* a, int32_t m, int device, double* det) {
     if (!a || m <= 0 || !det) return fail(PSX_EINVAL, "bad argument");

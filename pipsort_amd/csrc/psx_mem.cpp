@@ -3,6 +3,7 @@
 // blocks under device -1.
 #include "psx_mem.h"
 
+#include <atomic>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -178,7 +179,9 @@ namespace {
 struct StreamPool {
     std::mutex mu;
     std::map<std::pair<int, int>, std::vector<hipStream_t>> idle;  // (device, priority)
+    std::map<int, hipStream_t> shared;                             // single-queue mode: per device
 };
+std::atomic<bool> g_single_queue{false};
 StreamPool& streams() {
     static StreamPool* p = new StreamPool();
     return *p;
@@ -191,6 +194,16 @@ hipError_t stream_get(hipStream_t* s, int priority) {
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     StreamPool& P = streams();
+    if (g_single_queue.load()) {
+        std::lock_guard<std::mutex> g(P.mu);
+        hipStream_t& x = P.shared[dev];
+        if (!x && (e = hipStreamCreateWithFlags(&x, hipStreamNonBlocking)) != hipSuccess) {
+            x = nullptr;
+            return e;
+        }
+        *s = x;
+        return hipSuccess;
+    }
     {
         std::lock_guard<std::mutex> g(P.mu);
         auto& v = P.idle[{dev, priority}];
@@ -205,6 +218,12 @@ hipError_t stream_get(hipStream_t* s, int priority) {
 
 void stream_put(hipStream_t s, int priority) {
     if (!s) return;
+    {
+        StreamPool& P = streams();
+        std::lock_guard<std::mutex> g(P.mu);
+        for (auto& kv : P.shared)
+            if (kv.second == s) return;  // the single-queue mode's stream stays
+    }
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
         (void)hipStreamDestroy(s);
@@ -214,6 +233,8 @@ void stream_put(hipStream_t s, int priority) {
     std::lock_guard<std::mutex> g(P.mu);
     P.idle[{dev, priority}].push_back(s);
 }
+
+void set_single_queue(bool on) { g_single_queue.store(on); }
 
 void pool_trim() {
     Pool& P = pool();

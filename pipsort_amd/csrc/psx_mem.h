@@ -53,6 +53,12 @@ size_t pool_cached_bytes();
 // synchronises it and keeps it for the next handle.
 hipError_t stream_get(hipStream_t* s, int priority);
 void stream_put(hipStream_t s, int priority);
+// One hardware queue per device for the whole process (psx_single_queue in the
+// C ABI, for one-locus processes such as the CLI): every stream_get hands out
+// the device's one shared stream (normal priority) and stream_put keeps it.
+// Every queue a process holds costs ~10-13 ms when it exits (the kernel driver
+// tears it down: profiles/r06/r06late_c_exit_probe.txt).
+void set_single_queue(bool on);
 
 }  // namespace psx
 

@@ -31,7 +31,7 @@ PSX_EEXCHANGE = -7
 
 # Every symbol declared in include/pipsort_engine.h and include/pipsort_model.h
 EXPORTED = [
-    "psx_abi_version", "psx_overlap_cus", "psx_last_error", "psx_device_count", "psx_pool_trim", "psx_pool_cached_bytes", "psx_warmup", "psx_warmup_for", "psx_create", "psx_destroy",
+    "psx_abi_version", "psx_overlap_cus", "psx_last_error", "psx_device_count", "psx_pool_trim", "psx_pool_cached_bytes", "psx_warmup", "psx_warmup_for", "psx_single_queue", "psx_create", "psx_destroy",
     "psx_set_shard", "psx_run_exhaustive", "psx_run_configs", "psx_run_sss",
     "psx_eval_union_batch", "psx_reset", "psx_get_accum", "psx_partials_bytes",
     "psx_export_partials", "psx_partials_device_ptr", "psx_merge_partials", "psx_get_timing", "psx_count_configs",
@@ -172,6 +172,7 @@ def load_library(path: str = LIB_PATH):
         "psx_pool_cached_bytes": (ctypes.c_int64, []),
         "psx_warmup": (c_int, [c_int]),
         "psx_warmup_for": (c_int, [c_int, c_i32, c_i32]),
+        "psx_single_queue": (c_int, [c_i32]),
         "psx_create": (c_int, [P(_Problem), c_int, P(vp)]),
         "psx_destroy": (None, [vp]),
         "psx_set_shard": (c_int, [vp, c_int, c_int]),

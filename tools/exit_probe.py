@@ -21,7 +21,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=4)
 a = ap.parse_args()
 probe = os.path.join(ROOT, "tools", "init_probe")
-for args in ([], ["0", "0"], ["1024", "0"], ["16384", "0"], ["0", "256"]):
+for args in ([], ["0", "0"], ["1024", "0"], ["16384", "0"], ["0", "256"], ["0", "0", "1"], ["0", "0", "3"],
+             ["0", "0", "6"]):
     ex = []
     for _ in range(a.reps):
         p = subprocess.Popen([probe, "0"] + args, stdout=subprocess.PIPE, text=True)
@@ -31,11 +32,12 @@ for args in ([], ["0", "0"], ["1024", "0"], ["16384", "0"], ["0", "256"]):
         d = json.loads(line)
         ex.append(t - d["end_ms"])
     print(f"init_probe {' '.join(args) or '(bare)'}: exit {statistics.median(ex):.1f} ms "
-          f"(min {min(ex):.1f}, of {a.reps}); device MiB / pinned MiB held: {args or ['0', '0']}", flush=True)
+          f"(min {min(ex):.1f}, of {a.reps}); device MiB / pinned MiB / streams held: {args or ['0', '0']}", flush=True)
 
 import bench  # noqa: E402
 
-for _ in range(2):
+for sq in ("1", "0", "1", "0"):  # the CLI's one queue (default) against the engine's own streams
+    os.environ["PSX_SINGLE_QUEUE"] = sq
     w, same, ph = bench.example_wall()
-    print(f"CLI tests/example: wall {w:.3f} s, outputs match {same}, exit_ms {ph.get('exit_ms') if ph else None}",
+    print(f"CLI tests/example (PSX_SINGLE_QUEUE={sq}): wall {w:.3f} s, outputs match {same}, exit_ms {ph.get('exit_ms') if ph else None}",
           flush=True)

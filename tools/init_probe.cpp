@@ -2,7 +2,8 @@
 // hsa_init alone, then the HIP runtime (hipGetDeviceCount), context
 // (hipFree(0)), first launch.  Prints one JSON line, with the monotonic clock
 // at _exit (end_ms: the parent times the exit, tools/exit_probe.py).  Optional
-// argv[2] / argv[3]: MiB of device / pinned host memory held at exit.
+// argv[2] / argv[3]: MiB of device / pinned host memory held at exit; argv[4]:
+// streams created (hipStreamCreate, one launch each) and held at exit.
 // Developer tool:
 //   hipcc --offload-arch=gfx950 -O2 -o tools/init_probe tools/init_probe.cpp -lhsa-runtime64
 #include <hip/hip_runtime.h>
@@ -42,6 +43,13 @@ int main(int argc, char** argv) {
     void *big = nullptr, *pin = nullptr;
     if (dmb) (void)hipMalloc(&big, dmb << 20);
     if (hmb) (void)hipHostMalloc(&pin, hmb << 20);
+    const int nst = argc > 4 ? atoi(argv[4]) : 0;
+    for (int i = 0; i < nst; i++) {
+        hipStream_t st;
+        (void)hipStreamCreate(&st);
+        hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, st, d);
+        (void)hipStreamSynchronize(st);
+    }
     const double t6 = now_ms();
     printf("{\"hsa_init_ms\": %.2f, \"hip_device_count_ms\": %.2f, \"context_ms\": %.2f, \"malloc_ms\": %.2f, "
            "\"first_launch_ms\": %.2f, \"held_alloc_ms\": %.2f, \"devices\": %d, \"end_ms\": %.3f}\n",
