@@ -720,9 +720,10 @@ __device__ void eval_single(const DevProb& P, int u, Acc5& a, SetRec& r) {
 // in two launches of one-wave blocks (r06; r01-r05 had one launch whose block
 // 0 folded every scalar record in one wave: 86 us of a 0.84 ms single pass at
 // world 1, 26 us of 0.23 ms at world 8, profiles/r06a_*):
-//   k_merge_rec   blocks [0, nch):    scalar chunk c folds kScalChunk consecutive
-//                                     scalar items (the level-1 sets of this shard,
-//                                     then every unit record, srec[0, nsrec)) -> spart[c]
+//   k_merge_rec   blocks [0, nch):    scalar chunk c -> spart[c]: first the level-1
+//                                     sets of this shard, 64 per chunk (one per
+//                                     lane, late r06), then the unit records
+//                                     srec[0, nsrec), kScalChunk per chunk
 //                 block nch + V u + v: slice v of V of SNP u's record run (level A
 //                                     then level B, dense per-SNP runs) -> apart[V u + v]
 //   k_merge_fin   block 0:            scalars = extra (null configuration), then
@@ -750,24 +751,28 @@ __global__ __launch_bounds__(64) void k_merge_rec(DevProb P, int lo, int nsingle
     const int tid = threadIdx.x;
     const int b = blockIdx.x;
     if (ts && b == 0 && tid == 0) ts[1] = wall_clock64();  // a single pass: the sweep's end (its start: ts[0])
-    if (b < nch) {
-        const long n = (long)nsingle + nsrec;
-        const long i0 = (long)b * kScalChunk + tid;
+    const int nchs = (nsingle + T - 1) / T;  // level-1 chunks: one set per lane
+    if (b < nchs) {
+        // the level-1 sets of this shard, one per lane (eval_single is a chain of
+        // divisions and transcendentals: eight of them in series per lane held
+        // the whole merge up at world 1, late r06)
+        const int i = b * T + tid;
+        SetRec a = psx::set_zero();
+        if (i < nsingle) {
+            Acc5 dummy;
+            eval_single(P, lo + i, dummy, a);
+        }
+        psx::wave_fold_set(a);
+        if (tid == 0) spart[b] = a;
+        return;
+    }
+    if (b < nch) {  // the unit set records, kScalChunk per chunk
+        const long i0 = (long)(b - nchs) * kScalChunk + tid;
         SetRec r[kScalChunk / T];
 #pragma unroll
         for (int q = 0; q < kScalChunk / T; q++) {
             const long i = i0 + (long)q * T;
-            if (i >= nsingle && i < n) r[q] = srec[i - nsingle];
-        }
-#pragma unroll
-        for (int q = 0; q < kScalChunk / T; q++) {
-            const long i = i0 + (long)q * T;
-            if (i < nsingle) {
-                Acc5 dummy;
-                eval_single(P, lo + (int)i, dummy, r[q]);
-            } else if (i >= n) {
-                r[q] = psx::set_zero();
-            }
+            r[q] = i < nsrec ? srec[i] : psx::set_zero();
         }
         SetRec a = psx::set_zero();
 #pragma unroll
@@ -1707,7 +1712,7 @@ int fused_pass(psx_engine* e, int* flag, bool async = false) {
     const long nrec = (long)mA->rec_len + (mB ? (long)mB->rec_len : 0);
     const int V = (int)std::min<long>(kMergeWaysMax, std::max<long>(1, (2 * nrec / std::max(e->U, 1) + 511) / 512));
     const long nsingle = hi - lo, nsrec = (long)(nl + nt);
-    const int nch = (int)((nsingle + nsrec + kScalChunk - 1) / kScalChunk);
+    const int nch = (int)((nsingle + 63) / 64 + (nsrec + kScalChunk - 1) / kScalChunk);
     if ((rc = ensure(e->dspart, e->cap_spart, (size_t)std::max(nch, 1)))) return rc;
     if ((rc = ensure(e->dapart, e->cap_apart, (size_t)e->U * V))) return rc;
     // (-DPSX_ABLATE_MERGE, a separate timing build only: the pass's merge is
