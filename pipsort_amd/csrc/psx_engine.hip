@@ -1932,6 +1932,8 @@ int create_impl(const psx_problem* p, const psx_ld_problem* ld, int device, psx_
     const double alloc_ms = since(ta);
     const clk::time_point tb = clk::now();
     psx::LuJoin join;  // the two studies' first elimination in joint launches
+    static const char* lj = getenv("PSX_LU_JOINT");  // A/B: 0 = each study's own launches
+    const bool joint = !(lj && atoi(lj) == 0);
     auto study = [&](int s) {
         struct Leave {  // however this study ends, the other does not wait for it
             psx::LuJoin& j;
@@ -1953,7 +1955,7 @@ int create_impl(const psx_problem* p, const psx_ld_problem* ld, int device, psx_
         if (ld) {
             psx::LdStudyResult& r = x.r;
             std::string err;
-            if (psx::ld_study_setup(ld->ld + boff, ld->z + soff, M, st, x.dS, x.dyl, &r, &err, &join, s))
+            if (psx::ld_study_setup(ld->ld + boff, ld->z + soff, M, st, x.dS, x.dyl, &r, &err, joint ? &join : nullptr, s))
                 return die(PSX_EHIP, "GPU model setup: " + err);
             if (r.path == 0) {
                 lowrank = false;
@@ -2127,13 +2129,15 @@ int psx_warmup_for(int device, int32_t max_causal, int32_t configs_file) {
     double* d = nullptr;
     HIPCHK(psx::dmalloc(&d, 64 * sizeof(double)));
     hipStream_t ws = nullptr;
-    HIPCHK(psx::stream_get(&ws, 0));
+    static const char* wn = getenv("PSX_WARM_NULL");  // A/B: the null stream, as before late r06
+    const bool warm_null = wn && atoi(wn);
+    if (!warm_null) HIPCHK(psx::stream_get(&ws, 0));
     ta = now();
     hipLaunchKernelGGL(k_diag, dim3(1), dim3(64), 0, ws, d, 8, d + 8);
     hipError_t le = hipGetLastError();
     tl = now();
-    hipError_t se = hipStreamSynchronize(ws);
-    psx::stream_put(ws, 0);
+    hipError_t se = warm_null ? hipDeviceSynchronize() : hipStreamSynchronize(ws);
+    if (ws) psx::stream_put(ws, 0);
     {
         psx::IdleScope idle;  // (ws synchronised)
         psx::dfree(d);
