@@ -589,13 +589,31 @@ __global__ __launch_bounds__(64) void k_merge_partials(const Acc5* __restrict__ 
                                                        const int* __restrict__ redo, int* __restrict__ host) {
     const size_t stride = (size_t)ldg + 2;  // ldg Acc5, SetRec, PlanTag
     const int tid = threadIdx.x;
-    const PlanTag& t0 = *reinterpret_cast<const PlanTag*>(parts + ldg + 1);
+    const bool scal = blockIdx.x == gridDim.x - 1;
+    const int u = blockIdx.x * 64 + tid;
+    // the first eight images' entries of this SNP, issued before the tag check
+    // (unconditional loads from clamped indices: conditional ones put a wait
+    // after each image's load, one round trip per rank)
+    const int uc = (!scal && u < U) ? u : 0;
+    Acc5 x[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) x[q] = parts[(size_t)(q < count ? q : 0) * stride + uc];
+    // the tags, one rank per lane, in parallel (late r06: a lane walking the
+    // ranks' tags field by field was a chain of dependent scalar loads, ~1 us
+    // per rank — most of the merge at world 8)
+    const PlanTag* const tag0 = reinterpret_cast<const PlanTag*>(parts + ldg + 1);
+    const unsigned long long h0 = tag0->hash;
     bool bad = false;
-    for (int r = 0; r < count; r++) {
-        const PlanTag& t = *reinterpret_cast<const PlanTag*>(parts + (size_t)r * stride + ldg + 1);
-        bad |= t.magic != kPlanMagic || t.hash != t0.hash || t.world != count || t.rank != r || t.U != U;
+    for (int r0 = 0; r0 < count; r0 += 64) {
+        const int r = r0 + tid;
+        bool b = false;
+        if (r < count) {
+            const PlanTag t = *reinterpret_cast<const PlanTag*>(parts + (size_t)r * stride + ldg + 1);
+            b = (t.magic != kPlanMagic) | (t.hash != h0) | (t.world != count) | (t.rank != r) | (t.U != U);
+        }
+        bad |= __ballot(b) != 0ull;
     }
-    if (blockIdx.x == gridDim.x - 1) {  // the scalars, in rank order on lane 0
+    if (scal) {  // the scalars, in rank order on lane 0
         if (bad) {
             if (tid == 0) {
                 flag[kPlanMismatchWord] = 1;
@@ -606,14 +624,14 @@ __global__ __launch_bounds__(64) void k_merge_partials(const Acc5* __restrict__ 
         SetRec s = psx::set_zero();
         int f = 0;
         for (int r0 = 0; r0 < count; r0 += 64) {
-            SetRec x = psx::set_zero();
-            if (r0 + tid < count) x = *reinterpret_cast<const SetRec*>(parts + (size_t)(r0 + tid) * stride + ldg);
+            SetRec y0 = psx::set_zero();
+            if (r0 + tid < count) y0 = *reinterpret_cast<const SetRec*>(parts + (size_t)(r0 + tid) * stride + ldg);
             const int m = min(64, count - r0);
             for (int q = 0; q < m; q++) {
                 SetRec y;
-                y.m = __shfl(x.m, q); y.m0 = __shfl(x.m0, q); y.m1 = __shfl(x.m1, q); y.pad = __shfl(x.pad, q);
-                y.tot = __shfl(x.tot, q); y.nc0 = __shfl(x.nc0, q); y.nc1 = __shfl(x.nc1, q);
-                y.score = __shfl(x.score, q); y.npat = __shfl(x.npat, q);
+                y.m = __shfl(y0.m, q); y.m0 = __shfl(y0.m0, q); y.m1 = __shfl(y0.m1, q); y.pad = __shfl(y0.pad, q);
+                y.tot = __shfl(y0.tot, q); y.nc0 = __shfl(y0.nc0, q); y.nc1 = __shfl(y0.nc1, q);
+                y.score = __shfl(y0.score, q); y.npat = __shfl(y0.npat, q);
                 psx::fold_set(s, y);
                 f |= y.pad;  // any rank's EXACT flag
             }
@@ -626,19 +644,19 @@ __global__ __launch_bounds__(64) void k_merge_partials(const Acc5* __restrict__ 
         }
         return;
     }
-    const int u = blockIdx.x * 64 + tid;
     if (u >= U) return;
     Acc5 a = {0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    for (int r0 = 0; r0 < count; r0 += 8) {  // eight image loads in flight, folded in rank order
-        Acc5 x[8];
 #pragma unroll
-        for (int q = 0; q < 8; q++)
-            if (r0 + q < count) x[q] = parts[(size_t)(r0 + q) * stride + u];
+    for (int q = 0; q < 8; q++)
+        if (q < count) psx::fold_acc(a, x[q]);
+    for (int r0 = 8; r0 < count; r0 += 8) {  // eight image loads in flight, folded in rank order
+#pragma unroll
+        for (int q = 0; q < 8; q++) x[q] = parts[(size_t)(r0 + q < count ? r0 + q : r0) * stride + u];
 #pragma unroll
         for (int q = 0; q < 8; q++)
             if (r0 + q < count) psx::fold_acc(a, x[q]);
     }
-    if (!bad) acc[u] = a;  // (the image loads do not wait for the tag check)
+    if (!bad) acc[u] = a;
 }
 
 // the partial image (ldg + 2 slots) to a caller's buffer, 16 bytes per thread
