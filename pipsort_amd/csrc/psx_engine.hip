@@ -787,11 +787,17 @@ __global__ __launch_bounds__(64) void k_merge_rec(DevProb P, int lo, int nsingle
     if (b < nch) {  // the unit set records, kScalChunk per chunk
         const long i0 = (long)(b - nchs) * kScalChunk + tid;
         SetRec r[kScalChunk / T];
+        // unconditional loads from clamped indices (a conditional load put a
+        // wait after each one: eight round trips in series per lane), then the
+        // records past the end replaced by zero records
 #pragma unroll
         for (int q = 0; q < kScalChunk / T; q++) {
             const long i = i0 + (long)q * T;
-            r[q] = i < nsrec ? srec[i] : psx::set_zero();
+            r[q] = srec[i < nsrec ? i : nsrec - 1];
         }
+#pragma unroll
+        for (int q = 0; q < kScalChunk / T; q++)
+            if (i0 + (long)q * T >= nsrec) r[q] = psx::set_zero();
         SetRec a = psx::set_zero();
 #pragma unroll
         for (int q = 0; q < kScalChunk / T; q++) psx::fold_set(a, r[q]);
