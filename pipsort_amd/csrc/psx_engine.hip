@@ -206,6 +206,18 @@ __device__ __forceinline__ EvalOps eval_gather(const DevProb& P, const int* __re
         k += v >= 0;
     }
     o.k = k;
+    // Every load below is unconditional (clamped indices, results selected
+    // after) and every study pointer a select between the two kernel-argument
+    // values: indexing P.G[s] with a per-lane s read the pointer from the
+    // kernel arguments by a vector load, and each guarded load waited for the
+    // one before — five dependent round trips per set instead of one (late r06)
+    // (the kernel-argument pointers pinned in scalar registers: otherwise the
+    // compiler folds the selects below back into a per-lane pointer load)
+    const double *G0 = P.G[0], *G1 = P.G[1], *A0 = P.Ad[0], *A1 = P.Ad[1], *Y0 = P.y[0], *Y1 = P.y[1];
+    const unsigned char* PR = P.pres;
+    asm volatile("" : "+s"(G0), "+s"(G1), "+s"(A0), "+s"(A1), "+s"(Y0), "+s"(Y1), "+s"(PR));
+    double gv[2];
+    bool gok[2];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const int e = lane + 64 * h;
@@ -216,7 +228,9 @@ __device__ __forceinline__ EvalOps eval_gather(const DevProb& P, const int* __re
             mi = c == i ? mem[c] : mi;
             mj = c == j ? mem[c] : mj;
         }
-        o.g[h] = (e < 2 * KM * KM && i < k && j < i) ? P.G[s][(size_t)mi * P.ldg + mj] : 0.0;
+        gok[h] = e < 2 * KM * KM && i < k && j < i;
+        const size_t off = gok[h] ? (size_t)mi * P.ldg + mj : 0;
+        gv[h] = (s ? G1 : G0)[off];
     }
     {
         const int s = lane / KM, i = lane % KM;
@@ -224,11 +238,18 @@ __device__ __forceinline__ EvalOps eval_gather(const DevProb& P, const int* __re
 #pragma unroll
         for (int c = 0; c < KM; c++) mi = c == i ? mem[c] : mi;
         const bool ok = lane < 2 * KM && i < k;
-        o.ad = ok ? P.Ad[s][mi] : 0.0;
-        o.y = ok ? P.y[s][mi] : 0.0;
-        o.pr = (lane < KM && lane < k) ? P.pres[mi] : 0u;
+        const bool okp = lane < KM && lane < k;
+        const int ia = ok ? mi : 0, ip = okp ? mi : 0;
+        const double av = (s ? A1 : A0)[ia];
+        const double yv = (s ? Y1 : Y0)[ia];
+        const unsigned pv = PR[ip];
+        o.ad = ok ? av : 0.0;
+        o.y = ok ? yv : 0.0;
+        o.pr = okp ? pv : 0u;
         if (lane < KM) sh.mem[lane] = mi;
     }
+#pragma unroll
+    for (int h = 0; h < 2; h++) o.g[h] = gok[h] ? gv[h] : 0.0;
     return o;
 }
 __device__ __forceinline__ void eval_stage(const EvalOps& o, EvalShm& sh) {
