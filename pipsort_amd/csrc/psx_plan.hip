@@ -222,10 +222,26 @@ __global__ __launch_bounds__(kBT) void k_batch_part(const int* __restrict__ sets
         key[j] = v >= 0 ? v : U;  // no SNP: sorted behind every SNP
         val[j] = i;
     }
-    // the chunk's set records, thread-strided (their loads overlap the sort)
-    SetRec a = set_zero();
-    for (long i = s0 + t; i < s1; i += kBT) fold_set(a, srec[i]);
+    // the chunk's set records, thread-strided (spc <= kBT kBI: at most kBI per
+    // thread), loaded whole from clamped indices before the sort and folded
+    // after it in the same order.  (A fold of srec[i] in the loop let the
+    // compiler split each record into guarded field loads, one round trip per
+    // field, late r06.)
+    SetRec sv[kBI];
+#pragma unroll
+    for (int q = 0; q < kBI; q++) {
+        const long i = s0 + t + (long)q * kBT;
+        sv[q] = srec[i < s1 ? i : s1 - 1];
+    }
+#pragma unroll
+    for (int q = 0; q < kBI; q++)  // (every field materialised: no guarded field loads)
+        asm volatile("" : "+v"(sv[q].m), "+v"(sv[q].m0), "+v"(sv[q].m1), "+v"(sv[q].tot), "+v"(sv[q].nc0),
+                     "+v"(sv[q].nc1), "+v"(sv[q].score), "+v"(sv[q].npat));
     Sort(sh.sort).Sort(key, val, 0, end_bit);  // blocked: thread t holds sorted positions kBI t .. kBI t + kBI - 1
+    SetRec a = set_zero();
+#pragma unroll
+    for (int q = 0; q < kBI; q++)
+        if (s0 + t + (long)q * kBT < s1) fold_set(a, sv[q]);
     Acc5 r[kBI];
 #pragma unroll
     for (int j = 0; j < kBI; j++) r[j] = key[j] < U ? rc[val[j]] : acc_zero();
