@@ -2876,8 +2876,14 @@ __global__ __launch_bounds__(256) void k_sss_post(SssIter it, int lo, int hi, co
                 j = less;
             }
             const int p = i + 1;
-            r[v] = (i >= 0 && p >= lo && p < hi) ? mrec[(size_t)p * it.stride + j] : psx::acc_zero();
+            const bool ok = i >= 0 && p >= lo && p < hi;
+            r[v] = mrec[ok ? (size_t)p * it.stride + j : 0];  // (unconditional: one round trip, late r06)
+            if (!ok) r[v] = psx::acc_zero();
         }
+#pragma unroll
+        for (int v = 0; v <= PSX_KMAX; v++)
+            asm volatile("" : "+v"(r[v].mP), "+v"(r[v].mS), "+v"(r[v].mN), "+v"(r[v].post0), "+v"(r[v].post1),
+                         "+v"(r[v].shared), "+v"(r[v].sll), "+v"(r[v].nsll));
 #pragma unroll
         for (int v = 0; v <= PSX_KMAX; v++) psx::fold_acc(a, r[v]);
         if (a.post0 != 0.0 || a.post1 != 0.0 || a.shared != 0.0 || a.sll != 0.0 || a.nsll != 0.0) {
@@ -2890,7 +2896,25 @@ __global__ __launch_bounds__(256) void k_sss_post(SssIter it, int lo, int hi, co
     if (b == it.U) {  // the scalars: the slice's set records, then the null configurations (rank 0)
         SetRec a = psx::set_zero();
         int nu = 0, nz = 0;  // unseen neighbours, unseen null neighbours
-        for (int p = lo + t; p < hi; p += 256) psx::fold_set(a, srec[p]);  // zero where not evaluated
+        // the slice's set records (zero where not evaluated), eight whole records
+        // in flight per thread, folded in item order (a fold of srec[p] in the
+        // loop split each record into guarded field loads, one round trip per
+        // field, late r06)
+        for (int p0 = lo + t; p0 < hi; p0 += 256 * 8) {
+            SetRec r[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int p = p0 + 256 * q;
+                r[q] = srec[p < hi ? p : hi - 1];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                asm volatile("" : "+v"(r[q].m), "+v"(r[q].m0), "+v"(r[q].m1), "+v"(r[q].tot), "+v"(r[q].nc0),
+                             "+v"(r[q].nc1), "+v"(r[q].score), "+v"(r[q].npat));
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (p0 + 256 * q < hi) psx::fold_set(a, r[q]);
+        }
         for (int i = t; i < it.n_nbd; i += 256) {
             const int mk = mark[i];
             nu += mk != -1;
